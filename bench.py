@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: one day of one-minute 48 kHz recordings per GPU (BASELINE.json configs[2];
+configs[3] = the same sharded over 1/2/4/8 GPUs, one process per GPU).
+
+A step = one pass of the hot path over the rank's batch, inputs resident in HBM:
+  STFT power spectrogram (1024-pt, 50 % hop, float32 [K][T] per file)
+  + block band dB / delta + adaptive threshold detector (reference framing)
+  + per-hour detection counts, summed across ranks with one RCCL all-reduce.
+Weak scaling: every rank owns `--files` files (default 1440 = one day).
+
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (the
+STFT, timed live with HIP events on the stream it runs on) and the CPU baseline
+(the numpy/scipy oracle of the reference path, 1 thread, on a bounded sample).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import datetime
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "meteor-scatter_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+FS = 48000
+SECONDS = 60
+BAND = (950.0, 1050.0)
+NOISE = (650.0, 750.0)
+NPERSEG, NOVERLAP = 1024, 512
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+POOL = 16              # distinct synthetic recordings, replicated over the batch
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--files", type=int, default=1440, help="one-minute files per GPU")
+    ap.add_argument("--cpu-files", type=int, default=100, help="files in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
+    return ap.parse_args()
+
+
+def cpu_baseline(pool, nfiles):
+    """The reference path on the host: scipy.signal.spectrogram (main.py:132-133 call) + the
+    block loop and adaptive detector of main.py:352-527, restated in oracle/, 1 thread."""
+    from oracle import dsp_oracle as O
+    t0 = time.perf_counter()
+    for i in range(nfiles):
+        x = pool[i % len(pool)]
+        O.spectrogram_ref(x, FS, NPERSEG)
+        O.proc_samples_ref(x, FS, 0.2, BAND, NOISE, 512, 4)
+    dt = time.perf_counter() - t0
+    return nfiles * FS * SECONDS / dt / 1e6, dt
+
+
+def load_pmc_traffic(nfiles):
+    """HBM bytes per STFT launch from the committed rocprofv3 PMC summary (profiles/), if it
+    was collected for this workload; FETCH_SIZE doubled per the gfx950 rule."""
+    p = os.path.join(ROOT, "profiles", "stft_pmc.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        if d.get("files") == nfiles and d.get("nperseg") == NPERSEG:
+            return float(d["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from meteorgpu import _lib, synth
+    from meteorgpu.batch import BatchPipeline, Communicator
+
+    ctx = _lib.Context(local)
+    n = FS * SECONDS
+    F = a.files
+    bp = BatchPipeline(ctx, F, n, FS, nperseg=NPERSEG, noverlap=NOVERLAP, freq_band=BAND, noise_band=NOISE,
+                       with_spectrogram=not a.no_spectrogram)
+    pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
+    for i in range(F):
+        bp.upload_file(i, pool[(i + rank) % POOL])
+    # rank r holds day r: file i starts at minute i of 2025-06-(1+r) 00:00 UTC
+    epoch = datetime.datetime(1970, 1, 1)
+    day0 = datetime.datetime(2025, 6, 1) + datetime.timedelta(days=rank)
+    us = lambda t: (t - epoch) // datetime.timedelta(microseconds=1)  # noqa: E731
+    bp.set_start_times(np.array([us(day0 + datetime.timedelta(minutes=i)) for i in range(F)], np.int64),
+                       us(day0))
+    comm = None
+    if world > 1:
+        obj = [Communicator.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = Communicator(ctx, world, obj[0], rank)
+
+    def step():
+        bp.run()
+        if comm is not None:
+            comm.allreduce_i64(bp.d_hist, bp.nbuckets)
+
+    def sync_all():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    sync_all()
+    # correctness guard on the benchmarked data: every file's detector finished cleanly and
+    # the (all-reduced) hour histogram holds every detection of every rank
+    _, counts, status, _ = bp.detections()
+    assert (status == 0).all(), "detector status"
+    ctx.timing(True)
+    ctx.timing_reset()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([int(counts.sum())], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tot)
+        total_dets = int(tot.item())
+    else:
+        total_dets = int(counts.sum())
+    hist = bp.hour_counts()
+    assert int(hist.sum()) == total_dets * (1 if world == 1 else 1), "hour histogram != detections"
+    stft_ms, stft_launches = ctx.timing_get(_lib.K_STFT)
+    blk_ms, blk_launches = ctx.timing_get(_lib.K_BLOCK)
+    det_ms, det_launches = ctx.timing_get(_lib.K_DSCAN)
+
+    samples = world * F * n
+    value = samples * a.steps / elapsed / 1e6
+    out = {
+        "metric": "Msamples/s processed (48 kHz SDR stream) + % HBM roofline, 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: {POOL} seeded 60 s 48 kHz int16 noise+ping recordings replicated over {F} files/GPU",
+        "config": {
+            "workload": "C3 day batch: 1440 x 60 s 48 kHz mono int16 per GPU; STFT 1024/512 density PSD "
+                        "(float32 [513][T]) + block band dB (0.2 s, n_fft 1024, bands 950-1050/650-750 Hz) + "
+                        "adaptive detector + per-hour counts (RCCL all-reduce)" if not a.no_spectrogram else
+                        "C3 day batch, detect-only",
+            "files_per_gpu": F,
+            "samples_per_file": n,
+            "frames_per_file": bp.T,
+            "bins": bp.K,
+            "parallelism": f"files sharded over {world} GPU(s), 1 process per GPU",
+        },
+        "detections_per_step": total_dets,
+    }
+    if not a.no_spectrogram and stft_launches:
+        avg_s = stft_ms / stft_launches / 1e3
+        alg_bytes = F * (n * 2 + bp.K * bp.T * 4)  # samples read once + spectrogram written once
+        achieved = alg_bytes / avg_s / 1e9
+        out["roofline"] = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": load_pmc_traffic(F),
+            "kernel": "stft_psd_kernel<512,8,32,int16>",
+            "kernel_ms": round(avg_s * 1e3, 4),
+            "algorithmic_bytes_per_launch": alg_bytes,
+        }
+    out["kernel_ms_per_step"] = {
+        "stft": round(stft_ms / max(stft_launches, 1), 4),
+        "block_delta": round(blk_ms / max(blk_launches, 1), 4),
+        "detect": round(det_ms / max(det_launches, 1), 4),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
+        v, dt = cpu_baseline(pool, a.cpu_files)
+        out["cpu_baseline"] = {
+            "value": round(v, 2),
+            "unit": "Msamples/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": f"{a.cpu_files} of the 60 s 48 kHz files ({dt:.1f} s): scipy.signal.spectrogram "
+                      f"1024/512 + main.py block loop + adaptive detector (oracle/), 1 thread",
+        }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+/*
+ * msdsp.h — C-ABI of libmsdsp.so, the MI355X (gfx950) implementation of the
+ * meteor-scatter DSP hot path:
+ *
+ *   samples ──► STFT power spectrogram (scipy.signal.spectrogram semantics)
+ *           └─► block framing → symmetric Hann → rFFT crop → band / noise dB → delta
+ *               └─► global / adaptive threshold detector → detections (+ per-hour counts)
+ *
+ * The reference (th-nuernberg/meteor-scatter) is pure Python; its "FFI" for this
+ * path is the numpy/scipy calls inside dsp/src/main.py.  Each entry point below
+ * names the reference lines it replaces.  Conventions:
+ *   - every function returns MSD_OK (0) or a negative MSD_ERR_* code; the message
+ *     of the last failure on the calling thread is in msd_last_error();
+ *   - "_dev" functions take device pointers and enqueue on the context's stream
+ *     (no host synchronisation); the others take host pointers, borrow them for
+ *     the duration of the call only, and return after the results are on the host;
+ *   - a context is bound to one device and one HIP stream; it is not thread-safe.
+ * No torch, numpy or HIP types appear in the signatures.
+ */
+#ifndef MSDSP_H
+#define MSDSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSD_ABI_VERSION 1
+
+#define MSD_OK 0
+#define MSD_ERR_INVALID (-1)     /* bad argument (null pointer, size, ...)                 */
+#define MSD_ERR_HIP (-2)         /* HIP runtime failure                                    */
+#define MSD_ERR_UNSUPPORTED (-3) /* configuration outside what the kernels implement       */
+#define MSD_ERR_ASSERT (-4)      /* a reference `assert` would fire (message says which)   */
+#define MSD_ERR_CAPACITY (-5)    /* output capacity too small                              */
+#define MSD_ERR_INDEX (-6)       /* reference would raise IndexError (empty global input)  */
+#define MSD_ERR_RCCL (-7)        /* RCCL missing or failed                                 */
+
+/* sample formats, as scipy.io.wavfile.read returns them (io/wavfile.py:568-733) */
+#define MSD_U8 1
+#define MSD_I16 2
+#define MSD_I32 3
+#define MSD_F32 4
+#define MSD_F64 5
+
+typedef struct msd_ctx msd_ctx;
+typedef struct msd_stft_plan msd_stft_plan;
+typedef struct msd_block_plan msd_block_plan;
+typedef struct msd_comm msd_comm;
+
+/* ---------------------------------------------------------------- context */
+int msd_abi_version(void);
+const char *msd_last_error(void);
+int msd_device_count(int *count);
+int msd_create(int device, msd_ctx **out);
+void msd_destroy(msd_ctx *ctx);
+int msd_synchronize(msd_ctx *ctx);
+
+/* device memory owned by the caller, allocated through the context's device */
+int msd_dev_alloc(msd_ctx *ctx, size_t bytes, void **dptr);
+int msd_dev_free(msd_ctx *ctx, void *dptr);
+int msd_memcpy_h2d(msd_ctx *ctx, void *dst, const void *src, size_t bytes);
+int msd_memcpy_d2h(msd_ctx *ctx, void *dst, const void *src, size_t bytes);
+int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
+
+/* Per-kernel device timing with HIP events on the context stream.
+ * kernel id: 0 = STFT power, 1 = block delta, 2 = detector stats, 3 = detector scan. */
+int msd_timing_enable(msd_ctx *ctx, int enable);
+int msd_timing_reset(msd_ctx *ctx);
+int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
+
+/* ------------------------------------------------- a7: STFT power spectrogram
+ * Replaces scipy.signal.spectrogram(x, fs, window='hann', nperseg=N,
+ * noverlap=N-hop, nfft=N, detrend='constant', scaling='density', mode='psd')
+ * as called at dsp/src/main.py:52-54 and :132-133.
+ * window: N float32 values of the periodic Hann (scipy get_window, cast to
+ * complex64 by _spectral_helper, i.e. float32); scale = 1/(fs*sum(w^2)) as
+ * scipy computes it.  Output: float32 [K = N/2+1][T], T = (n-N)/hop + 1, with
+ * bins 1..N/2-1 doubled (one-sided, even N). */
+int msd_stft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float *window, double scale,
+                         msd_stft_plan **out);
+void msd_stft_plan_destroy(msd_stft_plan *plan);
+/* frames of an n-sample signal (0 if n < nperseg) */
+int64_t msd_stft_frames(const msd_stft_plan *plan, int64_t n);
+/* batch, device-resident: file f occupies x[off[f] .. off[f]+len[f]) (elements of dtype);
+ * its spectrogram is out[f*K*ld + k*ld + t] (ld >= max T, ld % 32 == 0; columns in
+ * [T_f, ld) are written with zeros). off/len are DEVICE arrays of nfiles int64. */
+int msd_stft_psd_dev(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                     int64_t nfiles, int64_t max_frames, float *out, int64_t ld);
+/* single signal, host buffers: out is dense float32 [K][T] */
+int msd_stft_psd(msd_stft_plan *plan, const void *x, int dtype, int64_t n, float *out, int64_t *frames);
+
+/* --------------------------------------- a2/a3: block band energies → delta
+ * Replaces the per-block loop of dsp/src/main.py:352-393:
+ *   fft_block = np.fft.rfft(block * np.hanning(B), n=Nf); P = |fft_block|^2
+ *   band_dB = 10*log10(sum(P[band]) + 1e-12); noise_dB likewise; delta = band_dB - noise_dB
+ * block_size B = int(fs*block_duration_sec); nfft Nf (already doubled, main.py:353);
+ * window: the first min(B, Nf) values of np.hanning(B) (float64);
+ * band/noise: inclusive bin ranges [lo, hi] of rfftfreq(Nf, 1/fs) selected by the
+ * reference masks (hi < lo means an empty band → energy 1e-12). Arithmetic is float64. */
+int msd_block_plan_create(msd_ctx *ctx, int64_t block_size, int32_t nfft, const double *window, int32_t band_lo,
+                          int32_t band_hi, int32_t noise_lo, int32_t noise_hi, msd_block_plan **out);
+void msd_block_plan_destroy(msd_block_plan *plan);
+/* batch, device-resident; block count of file f = len[f] / B; outputs [nfiles][ld]
+ * (band_db / noise_db may be NULL) */
+int msd_block_delta_dev(msd_block_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                        int64_t nfiles, int64_t max_blocks, double *band_db, double *noise_db, double *delta,
+                        int64_t ld);
+int msd_block_delta(msd_block_plan *plan, const void *x, int dtype, int64_t n, double *band_db, double *noise_db,
+                    double *delta, int64_t *blocks);
+
+/* ------------------------------------------------- a4/a5: threshold detector
+ * adaptive = 0: get_detections()          dsp/src/main.py:396-448
+ * adaptive = 1: get_detections_adaptive() dsp/src/main.py:450-522
+ * Block counts are the host's int(x_sec / block_duration_sec) (main.py:458-461).
+ * mean/std follow numpy (pairwise summation, population std) in float64 without
+ * FMA contraction.  A detection is the block range [start, stop) and the mean of
+ * delta over it (the reference's db_mean). */
+typedef struct {
+    int32_t adaptive;
+    int32_t reserved;
+    double k_std;                 /* threshold_std_factor              */
+    int64_t window_blocks;        /* int(threshold_estimation_window_sec / bs)         */
+    int64_t freeze_before_blocks; /* int(threshold_freeze_before_detection_sec / bs)   */
+    int64_t freeze_after_blocks;  /* int(threshold_freeze_after_detection_sec / bs)    */
+    int64_t fixed_init_blocks;    /* int(threshold_fixed_init_duration_sec / bs)       */
+} msd_det_cfg;
+
+typedef struct {
+    int64_t start; /* first block                           */
+    int64_t stop;  /* one past the last block (t_stop/bs)   */
+    double db;     /* np.mean(delta[start:stop])            */
+} msd_det;
+
+/* optional per-hour histogram of detection starts (main.py:687-696 Counter of
+ * utc_start.replace(minute=0, ...)): bucket = floor((file_start_us[f] +
+ * round(start*block_sec*1e6) - base_us) / bucket_us); outside [0, nbuckets) → dropped */
+typedef struct {
+    const int64_t *file_start_us; /* device, nfiles  */
+    int64_t base_us;
+    int64_t bucket_us;
+    int32_t nbuckets;
+    int32_t reserved;
+    double block_sec;
+    int64_t *counts; /* device, nbuckets, accumulated (not cleared) */
+} msd_hist_cfg;
+
+/* status word per file (device int32): 0 ok, 1 zero-duration global detection (reference
+ * assert at main.py:437), 2 empty global input (IndexError at main.py:412), 3 capacity */
+int msd_detect_dev(msd_ctx *ctx, const double *delta, const int64_t *nblocks, int64_t nfiles, int64_t ld,
+                   const msd_det_cfg *cfg, msd_det *dets, int64_t cap, int64_t *counts, double *thresholds,
+                   double *margin, int32_t *status, const msd_hist_cfg *hist);
+/* single file, host buffers. thresholds (nb) and margin may be NULL.
+ * global mode: *thresholds receives the single threshold in thresholds[0]. */
+int msd_detect(msd_ctx *ctx, const double *delta, int64_t nb, const msd_det_cfg *cfg, msd_det *dets, int64_t cap,
+               int64_t *count, double *thresholds, double *margin);
+
+/* ------------------------------------------ multi-GPU: per-hour count reduction
+ * RCCL (loaded at run time from librccl.so.1), one communicator per (process, GPU). */
+#define MSD_COMM_ID_BYTES 128
+int msd_comm_get_unique_id(char *id /* MSD_COMM_ID_BYTES */);
+int msd_comm_init(msd_ctx *ctx, int nranks, const char *id, int rank, msd_comm **out);
+void msd_comm_destroy(msd_comm *comm);
+/* in-place sum of n int64 on the device, on the context stream */
+int msd_comm_allreduce_i64(msd_comm *comm, int64_t *dbuf, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSDSP_H */

@@ -1,0 +1,101 @@
+// Internal declarations shared by the libmsdsp translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/msdsp.h"
+
+namespace msd {
+
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+int hip_fail(hipError_t e, const char *what);
+
+#define MSD_HIP(call)                                   \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_COUNT = 4 };
+
+struct EventPair {
+    hipEvent_t a, b;
+    int kernel;
+};
+
+}  // namespace msd
+
+struct msd_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    std::vector<msd::EventPair> pending;  // recorded, not yet folded into totals
+    std::vector<hipEvent_t> pool;         // reusable events
+    double total_ms[msd::K_COUNT] = {0, 0, 0, 0};
+    int64_t launches[msd::K_COUNT] = {0, 0, 0, 0};
+    // scratch device buffers for the host-pointer convenience entry points
+    void *scratch[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t scratch_bytes[4] = {0, 0, 0, 0};
+};
+
+struct msd_stft_plan {
+    msd_ctx *ctx = nullptr;
+    int nperseg = 0, hop = 0, M = 0;  // M = nperseg/2 complex points
+    double scale = 0;
+    float *d_window = nullptr;   // [nperseg]
+    float2 *d_tw = nullptr;      // [M]    exp(-2*pi*i*m/M)
+    float2 *d_post = nullptr;    // [M+1]  exp(-2*pi*i*k/(2M))
+};
+
+struct msd_block_plan {
+    msd_ctx *ctx = nullptr;
+    int64_t block_size = 0;
+    int nfft = 0, L = 0;                  // L = min(B, nfft) samples used per block
+    int band_lo = 0, band_hi = -1, noise_lo = 0, noise_hi = -1;
+    int nbins = 0;                        // band bins + noise bins
+    double *d_window = nullptr;           // [L]
+    double2 *d_tw = nullptr;              // [nfft] exp(-2*pi*i*m/nfft)
+    int *d_bins = nullptr;                // [nbins] bin indices, band first
+};
+
+namespace msd {
+
+// scoped timing of one kernel launch on ctx->stream
+struct KernelTimer {
+    msd_ctx *ctx;
+    int kernel;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(msd_ctx *c, int k);
+    ~KernelTimer();
+};
+
+// scratch buffer i of the context grown to at least `bytes`
+int ctx_scratch(msd_ctx *ctx, int slot, size_t bytes, void **out);
+
+// launchers (defined in the kernel translation units)
+int launch_stft(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len, int64_t nfiles,
+                int64_t max_frames, float *out, int64_t ld);
+int launch_block_delta(msd_block_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                       int64_t nfiles, int64_t max_blocks, double *band_db, double *noise_db, double *delta,
+                       int64_t ld);
+int launch_detect(msd_ctx *ctx, const double *delta, const int64_t *nblocks, int64_t nfiles, int64_t ld,
+                  const msd_det_cfg *cfg, msd_det *dets, int64_t cap, int64_t *counts, double *thresholds,
+                  double *margin, int32_t *status, const msd_hist_cfg *hist);
+
+inline size_t dtype_size(int dtype) {
+    switch (dtype) {
+        case MSD_U8: return 1;
+        case MSD_I16: return 2;
+        case MSD_I32: return 4;
+        case MSD_F32: return 4;
+        case MSD_F64: return 8;
+        default: return 0;
+    }
+}
+
+}  // namespace msd

@@ -1,0 +1,139 @@
+// Device restatement of numpy's float64 add.reduce (pairwise summation) so that
+// np.sum / np.mean / np.std over the same float64 inputs give the same bits on
+// the GPU.  numpy: DOUBLE_pairwise_sum (numpy/_core/src/umath/loops_utils.h.src):
+//   n < 8      : res = -0.0; res += a[i] ...
+//   n <= 128   : 8 interleaved accumulators, ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), tail
+//   otherwise  : n2 = n/2 - (n/2)%8; sum(a, n2) + sum(a+n2, n-n2)
+// np.add.reduce(a) starts from the identity 0.0 and adds the pairwise sum of each
+// 8192-element buffer chunk in turn (the ufunc reduction's buffer size):
+//   s = 0.0; for each chunk: s += pairwise(chunk)     (checked on numpy 2.2, n <= 432000)
+// mean = sum/n; std = sqrt(sum((a-mean)^2)/n) (population, numpy _var).
+// FP contraction is switched off inside every function here (no FMA may fuse a
+// multiply numpy rounds separately).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace msd {
+
+// A(i) returns the i-th element (a functor, so (x-mean)^2 can be formed on the fly
+// exactly as numpy materialises it: one rounded subtract, one rounded multiply).
+template <typename A>
+__device__ __forceinline__ double np_pairwise_leaf(const A &a, int64_t base, int64_t n) {
+#pragma clang fp contract(off)
+    if (n < 8) {
+        double res = -0.0;
+        for (int64_t i = 0; i < n; ++i) res += a(base + i);
+        return res;
+    }
+    double r0 = a(base + 0), r1 = a(base + 1), r2 = a(base + 2), r3 = a(base + 3);
+    double r4 = a(base + 4), r5 = a(base + 5), r6 = a(base + 6), r7 = a(base + 7);
+    int64_t i = 8;
+    const int64_t lim = n - (n % 8);
+    for (; i < lim; i += 8) {
+        r0 += a(base + i + 0);
+        r1 += a(base + i + 1);
+        r2 += a(base + i + 2);
+        r3 += a(base + i + 3);
+        r4 += a(base + i + 4);
+        r5 += a(base + i + 5);
+        r6 += a(base + i + 6);
+        r7 += a(base + i + 7);
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; ++i) res += a(base + i);
+    return res;
+}
+
+// Iterative post-order walk of numpy's recursion tree over [base, base+n)
+// (depth <= 48 for n < 2^48).  leaf(b, m) returns the sum of a leaf (m <= 128);
+// the walk combines the leaves exactly as numpy's recursion does.
+template <typename LeafFn>
+__device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
+#pragma clang fp contract(off)
+    if (n <= 128) return leaf(base, n);
+    int64_t st_base[48], st_n[48];
+    double st_left[48];
+    int st_state[48];
+    int sp = 0;
+    st_base[0] = base;
+    st_n[0] = n;
+    st_state[0] = 0;
+    double ret = 0.0;
+    while (sp >= 0) {
+        const int64_t b = st_base[sp], m = st_n[sp];
+        if (m <= 128) {
+            ret = leaf(b, m);
+            --sp;
+            // deliver ret to the parent
+            while (sp >= 0) {
+                if (st_state[sp] == 1) {  // left finished: start the right half
+                    st_left[sp] = ret;
+                    st_state[sp] = 2;
+                    int64_t n2 = st_n[sp] / 2;
+                    n2 -= n2 % 8;
+                    const int np1 = sp + 1;
+                    st_base[np1] = st_base[sp] + n2;
+                    st_n[np1] = st_n[sp] - n2;
+                    st_state[np1] = 0;
+                    sp = np1;
+                    break;
+                } else {  // state 2: both halves done
+                    ret = st_left[sp] + ret;
+                    --sp;
+                }
+            }
+            continue;
+        }
+        // internal node, first visit: descend left
+        st_state[sp] = 1;
+        int64_t n2 = m / 2;
+        n2 -= n2 % 8;
+        const int np1 = sp + 1;
+        st_base[np1] = b;
+        st_n[np1] = n2;
+        st_state[np1] = 0;
+        sp = np1;
+    }
+    return ret;
+}
+
+template <typename A>
+__device__ double np_pairwise(const A &a, int64_t base, int64_t n) {
+    return np_tree_walk(base, n, [&](int64_t b, int64_t m) { return np_pairwise_leaf(a, b, m); });
+}
+
+constexpr int64_t NP_BUFSIZE = 8192;
+
+template <typename A>
+__device__ double np_sum(const A &a, int64_t base, int64_t n) {
+#pragma clang fp contract(off)
+    double s = 0.0;
+    for (int64_t c = 0; c < n; c += NP_BUFSIZE) s += np_pairwise(a, base + c, n - c < NP_BUFSIZE ? n - c : NP_BUFSIZE);
+    return s;
+}
+
+struct ArrRef {
+    const double *p;
+    __device__ double operator()(int64_t i) const { return p[i]; }
+};
+struct SqDevRef {
+    const double *p;
+    double mean;
+    __device__ double operator()(int64_t i) const {
+#pragma clang fp contract(off)
+        const double d = p[i] - mean;
+        return d * d;
+    }
+};
+
+// numpy mean/std of p[base .. base+n)
+__device__ __forceinline__ void np_mean_std(const double *p, int64_t base, int64_t n, double &mean, double &std) {
+#pragma clang fp contract(off)
+    const double s = np_sum(ArrRef{p}, base, n);
+    mean = s / (double)n;
+    const double v = np_sum(SqDevRef{p, mean}, base, n);
+    std = sqrt(v / (double)n);
+}
+
+}  // namespace msd

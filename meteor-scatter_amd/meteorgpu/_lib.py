@@ -1,0 +1,346 @@
+"""ctypes binding of libmsdsp.so (the C-ABI declared in include/msdsp.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
+meteor-scatter_amd/csrc``) and loaded from this directory.  There is no CPU
+fallback: every compute entry point runs the HIP kernels, and a missing library
+or a missing GPU raises ``MsdError`` / ``OSError`` loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).with_name("libmsdsp.so")
+
+MSD_OK = 0
+MSD_ERR_INVALID = -1
+MSD_ERR_HIP = -2
+MSD_ERR_UNSUPPORTED = -3
+MSD_ERR_ASSERT = -4
+MSD_ERR_CAPACITY = -5
+MSD_ERR_INDEX = -6
+MSD_ERR_RCCL = -7
+
+MSD_U8, MSD_I16, MSD_I32, MSD_F32, MSD_F64 = 1, 2, 3, 4, 5
+DTYPE_CODES = {
+    np.dtype(np.uint8): MSD_U8,
+    np.dtype(np.int16): MSD_I16,
+    np.dtype(np.int32): MSD_I32,
+    np.dtype(np.float32): MSD_F32,
+    np.dtype(np.float64): MSD_F64,
+}
+
+K_STFT, K_BLOCK, K_DSTAT, K_DSCAN = 0, 1, 2, 3
+COMM_ID_BYTES = 128
+
+
+class MsdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libmsdsp error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class MsdDet(C.Structure):
+    _fields_ = [("start", C.c_int64), ("stop", C.c_int64), ("db", C.c_double)]
+
+
+DET_DTYPE = np.dtype([("start", np.int64), ("stop", np.int64), ("db", np.float64)])
+
+
+class MsdDetCfg(C.Structure):
+    _fields_ = [
+        ("adaptive", C.c_int32),
+        ("reserved", C.c_int32),
+        ("k_std", C.c_double),
+        ("window_blocks", C.c_int64),
+        ("freeze_before_blocks", C.c_int64),
+        ("freeze_after_blocks", C.c_int64),
+        ("fixed_init_blocks", C.c_int64),
+    ]
+
+
+class MsdHistCfg(C.Structure):
+    _fields_ = [
+        ("file_start_us", C.c_void_p),
+        ("base_us", C.c_int64),
+        ("bucket_us", C.c_int64),
+        ("nbuckets", C.c_int32),
+        ("reserved", C.c_int32),
+        ("block_sec", C.c_double),
+        ("counts", C.c_void_p),
+    ]
+
+
+# (name, restype, argtypes) — every symbol of include/msdsp.h
+_P = C.c_void_p
+_SIGS = [
+    ("msd_abi_version", C.c_int, []),
+    ("msd_last_error", C.c_char_p, []),
+    ("msd_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("msd_create", C.c_int, [C.c_int, C.POINTER(_P)]),
+    ("msd_destroy", None, [_P]),
+    ("msd_synchronize", C.c_int, [_P]),
+    ("msd_dev_alloc", C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
+    ("msd_dev_free", C.c_int, [_P, _P]),
+    ("msd_memcpy_h2d", C.c_int, [_P, _P, _P, C.c_size_t]),
+    ("msd_memcpy_d2h", C.c_int, [_P, _P, _P, C.c_size_t]),
+    ("msd_memset_dev", C.c_int, [_P, _P, C.c_int, C.c_size_t]),
+    ("msd_timing_enable", C.c_int, [_P, C.c_int]),
+    ("msd_timing_reset", C.c_int, [_P]),
+    ("msd_timing_get", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    ("msd_stft_plan_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_double, C.POINTER(_P)]),
+    ("msd_stft_plan_destroy", None, [_P]),
+    ("msd_stft_frames", C.c_int64, [_P, C.c_int64]),
+    ("msd_stft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64]),
+    ("msd_stft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
+    ("msd_block_plan_create", C.c_int,
+     [_P, C.c_int64, C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
+    ("msd_block_plan_destroy", None, [_P]),
+    ("msd_block_delta_dev", C.c_int,
+     [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, _P, _P, C.c_int64]),
+    ("msd_block_delta", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, _P, _P, C.POINTER(C.c_int64)]),
+    ("msd_detect_dev", C.c_int,
+     [_P, _P, _P, C.c_int64, C.c_int64, C.POINTER(MsdDetCfg), _P, C.c_int64, _P, _P, _P, _P,
+      C.POINTER(MsdHistCfg)]),
+    ("msd_detect", C.c_int,
+     [_P, _P, C.c_int64, C.POINTER(MsdDetCfg), _P, C.c_int64, C.POINTER(C.c_int64), _P, _P]),
+    ("msd_comm_get_unique_id", C.c_int, [_P]),
+    ("msd_comm_init", C.c_int, [_P, C.c_int, _P, C.c_int, C.POINTER(_P)]),
+    ("msd_comm_destroy", None, [_P]),
+    ("msd_comm_allreduce_i64", C.c_int, [_P, _P, C.c_int64]),
+]
+SYMBOLS = [s[0] for s in _SIGS]
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libmsdsp.so from the package directory (raises OSError if absent)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise OSError(
+                f"{LIB_PATH} is missing: build it with __graft_entry__.build() or "
+                f"`make -C meteor-scatter_amd/csrc` (there is no CPU fallback)")
+        lib = C.CDLL(str(LIB_PATH), mode=os.RTLD_LOCAL | getattr(os, "RTLD_NOW", 2))
+        for name, res, args in _SIGS:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != MSD_OK:
+        msg = load().msd_last_error()
+        raise MsdError(rc, msg.decode() if msg else "")
+
+
+def ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def dtype_code(dt) -> int:
+    dt = np.dtype(dt)
+    if dt.byteorder == ">":
+        raise ValueError("big-endian samples are not supported")
+    try:
+        return DTYPE_CODES[dt.newbyteorder("=")]
+    except KeyError:
+        raise TypeError(f"unsupported sample dtype {dt}") from None
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(load().msd_device_count(C.byref(n)))
+    return n.value
+
+
+class Context:
+    """A device + HIP stream (msd_ctx).  Not thread-safe."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        check(self.lib.msd_create(int(device), C.byref(h)))
+        self.h = h
+        self.device = int(device)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.msd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        check(self.lib.msd_synchronize(self.h))
+
+    # ---- device memory
+    def alloc(self, nbytes: int) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
+    def timing(self, enable: bool = True):
+        check(self.lib.msd_timing_enable(self.h, 1 if enable else 0))
+
+    def timing_reset(self):
+        check(self.lib.msd_timing_reset(self.h))
+
+    def timing_get(self, kernel: int):
+        ms = C.c_double(0)
+        n = C.c_int64(0)
+        check(self.lib.msd_timing_get(self.h, int(kernel), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(ctx.lib.msd_dev_alloc(ctx.h, C.c_size_t(self.nbytes), C.byref(p)))
+        self.ptr = p
+
+    def free(self):
+        if self.ptr:
+            check(self.ctx.lib.msd_dev_free(self.ctx.h, self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if self.ptr and self.ctx.h:
+                self.ctx.lib.msd_dev_free(self.ctx.h, self.ptr)
+        except Exception:
+            pass
+
+    def at(self, byte_offset: int):
+        return C.c_void_p(self.ptr.value + int(byte_offset))
+
+    def upload(self, a: np.ndarray, byte_offset: int = 0):
+        a = np.ascontiguousarray(a)
+        if byte_offset + a.nbytes > self.nbytes:
+            raise ValueError("upload overflows device buffer")
+        check(self.ctx.lib.msd_memcpy_h2d(self.ctx.h, self.at(byte_offset), ptr(a), C.c_size_t(a.nbytes)))
+
+    def download(self, out: np.ndarray, byte_offset: int = 0) -> np.ndarray:
+        if not out.flags.c_contiguous:
+            raise ValueError("download target must be contiguous")
+        if byte_offset + out.nbytes > self.nbytes:
+            raise ValueError("download overflows device buffer")
+        check(self.ctx.lib.msd_memcpy_d2h(self.ctx.h, ptr(out), self.at(byte_offset), C.c_size_t(out.nbytes)))
+        return out
+
+    def memset(self, value: int = 0):
+        check(self.ctx.lib.msd_memset_dev(self.ctx.h, self.ptr, int(value), C.c_size_t(self.nbytes)))
+
+
+class StftPlan:
+    def __init__(self, ctx: Context, nperseg: int, hop: int, window: np.ndarray, scale: float):
+        self.ctx = ctx
+        w = np.ascontiguousarray(window, dtype=np.float32)
+        if w.shape != (nperseg,):
+            raise ValueError("window length must equal nperseg")
+        h = C.c_void_p()
+        check(ctx.lib.msd_stft_plan_create(ctx.h, int(nperseg), int(hop), ptr(w), float(scale), C.byref(h)))
+        self.h = h
+        self.nperseg, self.hop = int(nperseg), int(hop)
+        self.nbins = nperseg // 2 + 1
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.msd_stft_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def frames(self, n: int) -> int:
+        return int(self.ctx.lib.msd_stft_frames(self.h, int(n)))
+
+    def run(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x)
+        T = self.frames(x.shape[0])
+        out = np.empty((self.nbins, T), dtype=np.float32)
+        t = C.c_int64(0)
+        check(self.ctx.lib.msd_stft_psd(self.h, ptr(x), dtype_code(x.dtype), int(x.shape[0]), ptr(out),
+                                        C.byref(t)))
+        return out
+
+    def run_dev(self, x: DeviceBuffer, dtype, off: DeviceBuffer, length: DeviceBuffer, nfiles: int,
+                max_frames: int, out: DeviceBuffer, ld: int):
+        check(self.ctx.lib.msd_stft_psd_dev(self.h, x.ptr, dtype_code(dtype), off.ptr, length.ptr, int(nfiles),
+                                            int(max_frames), out.ptr, int(ld)))
+
+
+class BlockPlan:
+    def __init__(self, ctx: Context, block_size: int, nfft: int, window: np.ndarray, band: tuple[int, int],
+                 noise: tuple[int, int]):
+        self.ctx = ctx
+        w = np.ascontiguousarray(window, dtype=np.float64)
+        h = C.c_void_p()
+        check(ctx.lib.msd_block_plan_create(ctx.h, int(block_size), int(nfft), ptr(w), int(band[0]), int(band[1]),
+                                            int(noise[0]), int(noise[1]), C.byref(h)))
+        self.h = h
+        self.block_size = int(block_size)
+        self.nfft = int(nfft)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.msd_block_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, x: np.ndarray):
+        x = np.ascontiguousarray(x)
+        nb = x.shape[0] // self.block_size
+        band = np.empty(nb, np.float64)
+        noise = np.empty(nb, np.float64)
+        delta = np.empty(nb, np.float64)
+        got = C.c_int64(0)
+        check(self.ctx.lib.msd_block_delta(self.h, ptr(x), dtype_code(x.dtype), int(x.shape[0]), ptr(band),
+                                           ptr(noise), ptr(delta), C.byref(got)))
+        return band, noise, delta
+
+    def run_dev(self, x: DeviceBuffer, dtype, off: DeviceBuffer, length: DeviceBuffer, nfiles: int,
+                max_blocks: int, band, noise, delta: DeviceBuffer, ld: int):
+        check(self.ctx.lib.msd_block_delta_dev(self.h, x.ptr, dtype_code(dtype), off.ptr, length.ptr, int(nfiles),
+                                               int(max_blocks), band.ptr if band else None,
+                                               noise.ptr if noise else None, delta.ptr, int(ld)))
+
+
+def det_cfg(adaptive: bool, k_std: float, window_blocks: int = 0, freeze_before: int = 0, freeze_after: int = 0,
+            fixed_init: int = 0) -> MsdDetCfg:
+    return MsdDetCfg(1 if adaptive else 0, 0, float(k_std), int(window_blocks), int(freeze_before),
+                     int(freeze_after), int(fixed_init))
+
+
+def detect(ctx: Context, delta: np.ndarray, cfg: MsdDetCfg, cap: int | None = None):
+    """Single-file detector on host delta: returns (dets[start, stop, db], thresholds, margin)."""
+    d = np.ascontiguousarray(delta, dtype=np.float64)
+    nb = d.shape[0]
+    if cap is None:
+        cap = nb // 2 + 2
+    dets = np.zeros(cap, dtype=DET_DTYPE)
+    thr = np.empty(max(nb, 1) if cfg.adaptive else 1, np.float64)
+    count = C.c_int64(0)
+    margin = C.c_double(0)
+    check(ctx.lib.msd_detect(ctx.h, ptr(d), int(nb), C.byref(cfg), ptr(dets), int(cap), C.byref(count), ptr(thr),
+                             C.byref(margin)))
+    return dets[: count.value], thr[:nb] if cfg.adaptive else thr, margin.value

@@ -1,0 +1,70 @@
+"""Generate the golden vectors under tests/golden/ (committed; rerun to refresh).
+
+The reference (th-nuernberg/meteor-scatter) ships no audio and no tests, and
+running it was denied in this environment.  Its arithmetic is
+entirely numpy/scipy, so the golden vectors are those third-party calls, made
+exactly as the reference makes them, on seeded synthetic inputs:
+
+  blocks_*.npz : np.fft.rfft(block * np.hanning(B), n=Nf) → |.|^2 band sums → dB
+                 (dsp/src/main.py:376-393) for the 6 kHz reference configuration
+                 (mb_files, main.py:825-899) and a 48 kHz configuration
+  spec_*.npz   : scipy.signal.spectrogram(x, fs, 'hann', nperseg=N, noverlap=N//2,
+                 nfft=N, scaling='density', mode='psd') (main.py:132-133), float32
+
+Run:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+from scipy.signal import spectrogram
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "meteor-scatter_amd"))
+from meteorgpu.synth import synth_real  # noqa: E402  (seeded generator, host-only)
+
+
+def blocks(x, fs, bs, band, noise, n_fft):
+    nfft = 2 * n_fft
+    B = int(fs * bs)
+    freqs = np.fft.rfftfreq(nfft, d=1 / fs)
+    mb = (freqs >= band[0]) & (freqs <= band[1])
+    mn = (freqs >= noise[0]) & (freqs <= noise[1])
+    out = np.empty((len(x) // B, 3))
+    for i in range(len(x) // B):
+        blk = x[i * B:(i + 1) * B]
+        p = np.abs(np.fft.rfft(blk * np.hanning(len(blk)), n=nfft)) ** 2
+        out[i, 0] = 10 * np.log10(np.sum(p[mb]) + 1e-12)
+        out[i, 1] = 10 * np.log10(np.sum(p[mn]) + 1e-12)
+    out[:, 2] = out[:, 0] - out[:, 1]
+    return out
+
+
+def main():
+    # 6 kHz, the reference's own configuration (main.py:827-833, 865-899)
+    x6, _ = synth_real(seed=1, fs=6000, duration_s=20.0, f0=1003.0, rate_per_min=12, band_hz=20.0)
+    b6 = blocks(x6, 6000, 0.2, (993, 1013), (690, 710), 512)
+    np.savez_compressed(os.path.join(HERE, "blocks_6k.npz"), x=x6, fs=6000, bs=0.2, band=(993, 1013),
+                        noise=(690, 710), n_fft=512, expected=b6)
+    # 48 kHz configuration with bands that hold FFT bins (SURVEY §0 degenerate-config warning)
+    x48, _ = synth_real(seed=2001, fs=48000, duration_s=3.0, f0=1000.0, rate_per_min=30)
+    b48 = blocks(x48, 48000, 0.2, (950, 1050), (650, 750), 512)
+    np.savez_compressed(os.path.join(HERE, "blocks_48k.npz"), x=x48, fs=48000, bs=0.2, band=(950, 1050),
+                        noise=(650, 750), n_fft=512, expected=b48)
+    # STFT spectrogram, 48 kHz, N=1024 / hop 512 (C1 shape, shortened)
+    xs = x48[:24000]
+    f, t, S = spectrogram(xs, fs=48000, window="hann", nperseg=1024, noverlap=512, nfft=1024,
+                          scaling="density", mode="psd")
+    np.savez_compressed(os.path.join(HERE, "spec_48k_1024.npz"), x=xs, fs=48000, nperseg=1024, f=f, t=t, S=S)
+    # STFT spectrogram, 6 kHz, N=256, float32 input
+    xf = (x6[:6000].astype(np.float32) / 32768.0).astype(np.float32)
+    f, t, S = spectrogram(xf, fs=6000, window="hann", nperseg=256, noverlap=128, nfft=256,
+                          scaling="density", mode="psd")
+    np.savez_compressed(os.path.join(HERE, "spec_6k_256_f32.npz"), x=xf, fs=6000, nperseg=256, f=f, t=t, S=S)
+    for name in sorted(os.listdir(HERE)):
+        if name.endswith(".npz"):
+            print(name, os.path.getsize(os.path.join(HERE, name)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,312 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the
+golden vectors.  Bar:
+  * detector: bit-exact thresholds, block indices and dB means for the same delta;
+  * band/noise/delta dB (float64 direct DFT vs pocketfft): |diff| <= 1e-9 dB;
+  * end to end: identical detection timestamps (CSV t/UTC columns), dB within 1e-9;
+  * spectrogram vs scipy: per frame max|diff| <= 1e-5 * max|S| (float32 FFT).
+"""
+import datetime
+import os
+
+import numpy as np
+import pytest
+
+from meteorgpu import _lib, dsp, synth, wav
+from meteorgpu.batch import BatchPipeline
+from oracle import dsp_oracle as O
+from tests.detector_kats import ADAPTIVE, GLOBAL
+
+pytestmark = pytest.mark.gpu
+
+DB_TOL = 1e-9
+SPEC_TOL = 1e-5
+
+
+def _golden(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def _frame_err(S, ref):
+    return (np.abs(S.astype(np.float64) - ref.astype(np.float64)).max(axis=0) /
+            np.maximum(np.abs(ref).max(axis=0), 1e-30)).max()
+
+
+# ------------------------------------------------------------------ a2/a3 block powers
+@pytest.mark.parametrize("name", ["blocks_6k.npz", "blocks_48k.npz"])
+def test_block_powers_golden(golden_dir, name):
+    g = _golden(golden_dir, name)
+    band, noise, delta, _ = dsp.block_powers(g["x"], int(g["fs"]), float(g["bs"]), tuple(g["band"]),
+                                             tuple(g["noise"]), int(g["n_fft"]))
+    exp = g["expected"]
+    assert np.abs(band - exp[:, 0]).max() <= DB_TOL
+    assert np.abs(noise - exp[:, 1]).max() <= DB_TOL
+    assert np.abs(delta - exp[:, 2]).max() <= DB_TOL
+
+
+BLOCK_CASES = [
+    # fs, block_sec, band, noise, n_fft, dtype, n
+    (6000, 0.2, (993, 1013), (690, 710), 512, np.int16, 6000 * 30 + 777),      # reference config, ragged
+    (48000, 0.2, (950, 1050), (650, 750), 512, np.int16, 48000 * 4),          # 48 kHz, crop 9600 → 1024
+    (48000, 0.2, (990, 1010), (690, 710), 512, np.int16, 48000 * 2),          # zero-bin bands → -120 dB
+    (6000, 0.05, (900, 1100), (500, 700), 512, np.float32, 6000 * 10 + 3),    # B=300 < Nf: zero padding
+    (4000, 0.2, (950, 1050), (650, 750), 2048, np.float64, 4000 * 10),        # Nf=4096, L=800
+    (6000, 0.2, (993, 1013), (690, 710), 512, np.uint8, 6000 * 5),
+    (6000, 0.2, (993, 1013), (690, 710), 512, np.int32, 6000 * 5),
+    (5000, 0.3, (0, 2500), (100, 200), 300, np.int16, 5000 * 6),              # Nf=600 (not 2^k), wide band
+]
+
+
+@pytest.mark.parametrize("case", BLOCK_CASES, ids=[f"{c[0]}Hz-{np.dtype(c[5]).name}-{i}" for i, c in
+                                                    enumerate(BLOCK_CASES)])
+def test_block_powers_vs_oracle(case):
+    fs, bs, band_hz, noise_hz, n_fft, dt, n = case
+    x, _ = synth.synth_real(seed=100 + n % 97, fs=fs, duration_s=n / fs, f0=sum(band_hz) / 2, rate_per_min=20)
+    x = x[:n]
+    if np.dtype(dt) == np.uint8:
+        x = ((x.astype(np.int32) >> 8) + 128).astype(np.uint8)
+    elif np.dtype(dt) == np.int32:
+        x = x.astype(np.int32) << 8
+    else:
+        x = x.astype(dt)
+    rb, rn, rd = O.block_powers_ref(x, fs, bs, band_hz, noise_hz, n_fft)
+    b, nz, d, B = dsp.block_powers(x, fs, bs, band_hz, noise_hz, n_fft)
+    assert B == int(fs * bs) and b.shape == rb.shape
+    assert np.abs(b - rb).max() <= DB_TOL
+    assert np.abs(nz - rn).max() <= DB_TOL
+    assert np.abs(d - rd).max() <= DB_TOL
+
+
+# ------------------------------------------------------------------ a4/a5 detector KATs
+@pytest.mark.parametrize("case", GLOBAL, ids=[c[0] for c in GLOBAL])
+def test_global_detector_kats(case):
+    name, delta, k, exp, exp_thr, err = case
+    d = np.array(delta, dtype=np.float64)
+    if err is not None:
+        with pytest.raises(err):
+            dsp.get_detections(d, k, 1.0)
+        return
+    dets, thr = dsp.get_detections(d, k, 1.0)
+    _, rthr = O.get_detections_ref(d, k, 1.0)
+    assert thr == rthr
+    assert [(int(x.t_start), int(x.t_stop)) for x in dets] == [(s, e) for s, e, _ in exp]
+    assert [float(x.dB) for x in dets] == [db for *_, db in exp]
+
+
+@pytest.mark.parametrize("case", ADAPTIVE, ids=[c[0] for c in ADAPTIVE])
+def test_adaptive_detector_kats(case):
+    name, delta, k, (w, fb, fa, f0), exp, exp_thr = case
+    d = np.array(delta, dtype=np.float64)
+    dets, thr = dsp.get_detections_adaptive(d, k, 1.0, w, fb, fa, f0)
+    _, rthr = O.get_detections_adaptive_ref(d, k, 1.0, w, fb, fa, f0)
+    assert [(int(x.t_start), int(x.t_stop)) for x in dets] == [(s, e) for s, e, _ in exp]
+    assert [float(x.dB) for x in dets] == [db for *_, db in exp]
+    np.testing.assert_array_equal(np.array(thr, float), np.array(rthr, float))
+
+
+def _random_delta(seed, nb, bursts=20):
+    rng = np.random.default_rng(seed)
+    d = rng.standard_normal(nb) * 1.5 + rng.uniform(-3, 3)
+    for _ in range(bursts):
+        i = rng.integers(0, max(1, nb))
+        d[i:i + rng.integers(1, 30)] += rng.uniform(3, 25)
+    return d
+
+
+@pytest.mark.parametrize("nb", [1, 2, 7, 300, 1000, 5000, 20000, 70000])
+@pytest.mark.parametrize("bs", [0.2, 0.1])
+def test_adaptive_detector_bit_exact(nb, bs):
+    d = _random_delta(nb, nb, bursts=max(1, nb // 100))
+    start = datetime.datetime(2025, 6, 25, 7, 51, 41)
+    dets, thr = dsp.get_detections_adaptive(d, 4, bs, 120, 3, 20, 10, wav_start_date_time=start)
+    rdets, rthr = O.get_detections_adaptive_ref(d, 4, bs, 120, 3, 20, 10, wav_start_date_time=start)
+    np.testing.assert_array_equal(np.array(thr, float), np.array(rthr, float))
+    assert len(dets) == len(rdets)
+    for a, r in zip(dets, rdets):
+        assert (a.t_start, a.t_stop, a.dur_s, a.utc_start, a.utc_stop) == (r[0], r[1], r[2], r[4], r[5])
+        assert a.dB == r[3]
+
+
+@pytest.mark.parametrize("nb", [2, 300, 9000, 300000])
+@pytest.mark.parametrize("k", [1.0, 3.5])
+def test_global_detector_bit_exact(nb, k):
+    d = _random_delta(nb + 1, nb, bursts=max(1, nb // 50))
+    d[-1] = -10.0  # keep the last block below (the reference asserts otherwise)
+    dets, thr = dsp.get_detections(d, k, 0.2)
+    rdets, rthr = O.get_detections_ref(d, k, 0.2)
+    assert thr == rthr
+    assert [(x.t_start, x.t_stop, x.dur_s) for x in dets] == [tuple(r[:3]) for r in rdets]
+    assert [x.dB for x in dets] == [r[3] for r in rdets]
+
+
+def test_global_detector_zero_duration_asserts():
+    d = np.zeros(50)
+    d[-1] = 100.0
+    with pytest.raises(AssertionError, match="Detection duration must be greater than 0"):
+        dsp.get_detections(d, 1.0, 0.2)
+    with pytest.raises(AssertionError, match="UTC start time must be before stop time"):
+        dsp.get_detections(d, 1.0, 0.2, wav_start_date_time=datetime.datetime(2025, 1, 1))
+
+
+# ------------------------------------------------------------------ end to end (a1-a6)
+E2E = [
+    # fs, seconds, band, noise, adaptive, k
+    (6000, 600, (993, 1013), (690, 710), True, 4),      # mb_files configuration, 10 minutes
+    (6000, 300, (996, 1016), (940, 960), True, 3.5),    # tl_files-like bands
+    (6000, 300, (993, 1013), (690, 710), False, 4),     # global threshold
+    (48000, 60, (950, 1050), (650, 750), True, 4),      # C1/C2: one 60 s 48 kHz file
+]
+
+
+@pytest.mark.parametrize("case", E2E, ids=[f"{c[0]}Hz-{c[1]}s-{'adaptive' if c[4] else 'global'}" for c in E2E])
+def test_proc_wav_file_csv_matches_oracle(tmp_path, case):
+    fs, secs, band, noise, adaptive, k = case
+    x, pings = synth.synth_real(seed=1000 + secs + fs // 1000, fs=fs, duration_s=secs, f0=sum(band) / 2,
+                                band_hz=band[1] - band[0], rate_per_min=6)
+    x[-int(fs * 2):] = (x[-int(fs * 2):] // 4)  # quiet tail: keeps the global detector off the last block
+    p = tmp_path / "expoFull_gqrx_20250625_075141_49969000.wav"
+    wav.write(p, fs, x)
+    start = wav.start_datetime_from_name(str(p))
+    out_csv = tmp_path / "ours.csv"
+    res = dsp.proc_wav_file(str(p), 0.2, band, noise, 512, k, out_csv_file=str(out_csv), wav_start_date_time=start,
+                            disable_show_and_write=True, flag_adaptive_threshold=adaptive,
+                            required_sample_rate=fs, out_audacity_lbl_file=str(tmp_path / "lbl.txt"))
+    rdets, rthr, rb, rn, rd = O.proc_samples_ref(x, fs, 0.2, band, noise, 512, k, start, adaptive)
+    assert np.abs(res.delta_power - rd).max() <= DB_TOL
+    assert res.min_margin > 1e-7, "decision margin too small for a meaningful parity check"
+    O.write_csv_ref(rdets, tmp_path / "ref.csv")
+    ours = (out_csv).read_text().splitlines()
+    ref = (tmp_path / "ref.csv").read_text().splitlines()
+    assert len(ours) == len(ref) and len(ref) >= 2, "synthetic input should produce detections"
+    for lo, lr in zip(ours[1:], ref[1:]):
+        fo, fr = lo.split(","), lr.split(",")
+        assert fo[0:3] == fr[0:3] and fo[4:] == fr[4:]       # t_start, t_stop, dur_s, utc_start, utc_stop
+        assert abs(float(fo[3]) - float(fr[3])) <= DB_TOL   # dB
+    assert (tmp_path / "lbl.txt").read_text() == O.audacity_ref(rdets)
+
+
+# ------------------------------------------------------------------ a7 spectrogram
+@pytest.mark.parametrize("name", ["spec_48k_1024.npz", "spec_6k_256_f32.npz"])
+def test_spectrogram_golden(golden_dir, name):
+    g = _golden(golden_dir, name)
+    N = int(g["nperseg"])
+    f, t, S = dsp.spectrogram(g["x"], fs=int(g["fs"]), window="hann", nperseg=N, noverlap=N // 2, nfft=N,
+                              scaling="density", mode="psd")
+    assert S.dtype == np.float32 and S.shape == g["S"].shape
+    np.testing.assert_array_equal(f, g["f"])
+    np.testing.assert_array_equal(t, g["t"])
+    assert _frame_err(S, g["S"]) <= SPEC_TOL
+
+
+SPEC_CASES = [
+    # fs, nperseg, noverlap, dtype, n
+    (48000, 1024, 512, np.int16, 48000 * 3 + 100),
+    (48000, 1024, 768, np.int16, 48000),
+    (48000, 1024, 0, np.int16, 48000),
+    (6000, 256, 128, np.int16, 6000 * 5),
+    (6000, 512, 256, np.float32, 6000 * 5),
+    (6000, 2048, 1024, np.int16, 6000 * 10),
+    (6000, 2048, 1024, np.uint8, 6000 * 10),
+    (4000, 1024, 512, np.float32, 4000 * 3 + 1),
+    (48000, 1024, 511, np.int16, 48000),   # odd hop: unaligned frame starts (scalar loads)
+]
+
+
+@pytest.mark.parametrize("case", SPEC_CASES, ids=[f"{c[1]}-{c[2]}-{np.dtype(c[3]).name}" for c in SPEC_CASES])
+def test_spectrogram_vs_scipy(case):
+    fs, N, nov, dt, n = case
+    x, _ = synth.synth_real(seed=N + nov, fs=fs, duration_s=n / fs + 1, f0=1000.0, rate_per_min=30)
+    x = x[:n]
+    if np.dtype(dt) == np.float32:
+        x = (x / 32768.0).astype(np.float32)
+    elif np.dtype(dt) == np.uint8:
+        x = ((x.astype(np.int32) >> 8) + 128).astype(np.uint8)
+    from scipy.signal import spectrogram as sp_spec
+    fr, tr, Sr = sp_spec(x, fs=fs, window="hann", nperseg=N, noverlap=nov, nfft=N, scaling="density", mode="psd")
+    f, t, S = dsp.spectrogram(x, fs=fs, window="hann", nperseg=N, noverlap=nov, nfft=N)
+    assert S.shape == Sr.shape and S.dtype == Sr.dtype == np.float32
+    np.testing.assert_array_equal(f, fr)
+    np.testing.assert_array_equal(t, tr)
+    assert _frame_err(S, Sr) <= SPEC_TOL
+
+
+def test_spectrogram_constant_input_is_zero():
+    # constant detrend removes a DC-only signal entirely
+    x = np.full(48000, 1234, np.int16)
+    _, _, S = dsp.spectrogram(x, fs=48000, nperseg=1024, noverlap=512)
+    assert np.abs(S).max() <= 1e-6
+
+
+# ------------------------------------------------------------------ batch pipeline (C2/C3 shape)
+def test_batch_pipeline_matches_single_file_path():
+    ctx = dsp.context(0)
+    fs, n, F = 48000, 48000 * 60, 6
+    bp = BatchPipeline(ctx, F, n, fs)
+    xs = []
+    for i in range(F):
+        x, _ = synth.synth_real(seed=3000 + i, fs=fs, duration_s=60, f0=1000.0, rate_per_min=8)
+        xs.append(x)
+        bp.upload_file(i, x)
+    base = datetime.datetime(2025, 6, 25, 0, 0, 0)
+    starts = [base + datetime.timedelta(minutes=59 + i) for i in range(F)]  # straddles the 01:00 boundary
+    epoch = datetime.datetime(1970, 1, 1)
+    start_us = np.array([(s - epoch) // datetime.timedelta(microseconds=1) for s in starts], np.int64)
+    bp.set_start_times(start_us, (base - epoch) // datetime.timedelta(microseconds=1))
+    bp.run()
+    ctx.synchronize()
+    deltas = bp.delta()
+    dets, counts, status, margin = bp.detections()
+    assert (status == 0).all()
+    total = 0
+    from collections import Counter
+    ref_hours = Counter()
+    for i in range(F):
+        _, _, S = dsp.spectrogram(xs[i], fs=fs, nperseg=1024, noverlap=512)
+        np.testing.assert_array_equal(bp.spectrogram(i), S)
+        _, _, d, _ = dsp.block_powers(xs[i], fs, 0.2, (950, 1050), (650, 750), 512)
+        np.testing.assert_array_equal(deltas[i], d)
+        rdets, _ = O.get_detections_adaptive_ref(d, 4.0, 0.2, wav_start_date_time=starts[i])
+        assert [(int(a["start"]), int(a["stop"])) for a in dets[i]] == \
+               [(int(round(r[0] / 0.2)), int(round(r[1] / 0.2))) for r in rdets]
+        assert [a["db"] for a in dets[i]] == [r[3] for r in rdets]
+        total += len(rdets)
+        for h, c in O.count_per_hour_ref(rdets).items():
+            ref_hours[(h - base) // datetime.timedelta(hours=1)] += c
+    hist = bp.hour_counts()
+    assert hist.sum() == total > 0
+    for h in range(24):
+        assert hist[h] == ref_hours.get(h, 0)
+
+
+def test_full_day_batch_properties():
+    """C3 at full size (1440 x 60 s @ 48 kHz, 8.3 GB in, 16.6 GB spectrogram) through
+    size-independent properties: replicated files give identical outputs at every offset
+    (no 32-bit index overflow), per-frame Parseval on sampled frames, delta equal to the
+    single-file path, histogram total equal to the detection count."""
+    ctx = dsp.context(0)
+    fs, n, F = 48000, 48000 * 60, 1440
+    bp = BatchPipeline(ctx, F, n, fs)
+    pool = [synth.synth_real(seed=4000 + j, fs=fs, duration_s=60, f0=1000.0)[0] for j in range(4)]
+    for i in range(F):
+        bp.upload_file(i, pool[i % 4])
+    bp.run()
+    ctx.synchronize()
+    dets, counts, status, margin = bp.detections()
+    assert (status == 0).all()
+    assert bp.hour_counts().sum() == counts.sum()
+    deltas = bp.delta()
+    for j in range(4):
+        np.testing.assert_array_equal(counts[j::4], counts[j])
+        np.testing.assert_array_equal(deltas[j::4], np.broadcast_to(deltas[j], deltas[j::4].shape))
+    for i in (0, 1, 717, 1438, 1439):
+        S = bp.spectrogram(i)
+        np.testing.assert_array_equal(S, bp.spectrogram(i % 4))
+        x = pool[i % 4].astype(np.float64)
+        w = dsp.hann_periodic(1024).astype(np.float32).astype(np.float64)
+        scale = 1.0 / (fs * np.sum(w * w))
+        for t in (0, 1, 2811, S.shape[1] - 1):
+            v = x[t * 512:t * 512 + 1024]
+            v = (v - v.mean()) * w
+            want = scale * 1024 * np.sum(v * v)   # Parseval on the one-sided, doubled spectrum
+            assert abs(S[:, t].astype(np.float64).sum() - want) <= 1e-5 * want
+    _, _, d0, _ = dsp.block_powers(pool[1], fs, 0.2, (950, 1050), (650, 750), 512)
+    np.testing.assert_array_equal(deltas[1437], d0)
