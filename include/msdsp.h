@@ -65,6 +65,11 @@ int msd_memcpy_h2d(msd_ctx *ctx, void *dst, const void *src, size_t bytes);
 int msd_memcpy_d2h(msd_ctx *ctx, void *dst, const void *src, size_t bytes);
 int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
 
+/* Options: MSD_OPT_GENERIC_STFT = 1 → use the generic STFT kernel even where a
+ * specialised one exists (A/B testing of the kernels; results must agree). */
+#define MSD_OPT_GENERIC_STFT 1
+int msd_set_option(msd_ctx *ctx, int option, int value);
+
 /* Per-kernel device timing with HIP events on the context stream.
  * kernel id: 0 = STFT power, 1 = block delta, 2 = detector stats, 3 = detector scan. */
 int msd_timing_enable(msd_ctx *ctx, int enable);

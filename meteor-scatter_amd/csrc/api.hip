@@ -220,6 +220,14 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes) {
     return MSD_OK;
 }
 
+int msd_set_option(msd_ctx *ctx, int option, int value) {
+    if (!ctx) return fail(MSD_ERR_INVALID, "null ctx");
+    switch (option) {
+        case MSD_OPT_GENERIC_STFT: ctx->force_generic = value != 0; return MSD_OK;
+        default: return fail(MSD_ERR_INVALID, "msd_set_option: unknown option");
+    }
+}
+
 int msd_timing_enable(msd_ctx *ctx, int enable) {
     if (!ctx) return fail(MSD_ERR_INVALID, "null ctx");
     ctx->timing = enable != 0;

@@ -19,7 +19,7 @@ namespace msd {
 namespace {
 
 constexpr int BD_WAVES = 4;
-constexpr int BD_MAXBINS = 256;  // per band
+constexpr int BD_MAXBINS = 4096;  // band + noise bins (dynamic LDS: BD_WAVES * nbins doubles)
 
 template <typename T>
 __device__ __forceinline__ double to_d(T v) {
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(BD_WAVES * 64) void block_delta_kernel(
     int64_t blocks_per_file, int64_t B, int L, int nfft, const double *__restrict__ g_win,
     const double2 *__restrict__ g_tw, const int *__restrict__ bins, int nband, int nnoise, double *__restrict__ band_db,
     double *__restrict__ noise_db, double *__restrict__ delta, int64_t ld) {
-    __shared__ double pbuf[BD_WAVES][2 * BD_MAXBINS];
+    extern __shared__ double pbuf_all[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * BD_WAVES + wave;
@@ -76,6 +76,7 @@ __global__ __launch_bounds__(BD_WAVES * 64) void block_delta_kernel(
     for (int q = 0; q < SPL; ++q) v[q] = (n0 + q < L) ? v[q] * g_win[n0 + q] : 0.0;
 
     const int nbins = nband + nnoise;
+    double *pb = pbuf_all + wave * nbins;
     for (int j = 0; j < nbins; ++j) {
         const int k = bins[j];
         // r = exp(-2*pi*i*k*n0/nfft), step = exp(-2*pi*i*k/nfft)
@@ -94,12 +95,11 @@ __global__ __launch_bounds__(BD_WAVES * 64) void block_delta_kernel(
         im = wave_sum_d(im);
         if (lane == 0) {
             const double h = hypot(re, im);  // np.abs(complex) then **2
-            pbuf[wave][j] = h * h;
+            pb[j] = h * h;
         }
     }
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
-        const double *pb = pbuf[wave];
         const double be = np_sum(ArrRef{pb}, 0, nband) + 1e-12;
         const double ne = np_sum(ArrRef{pb}, nband, nnoise) + 1e-12;
         const double bd = 10.0 * log10(be);
@@ -117,7 +117,14 @@ int launch_bd(msd_block_plan *p, const void *x, const int64_t *off, const int64_
     const int64_t waves = nfiles * max_blocks;
     const int64_t grid = (waves + BD_WAVES - 1) / BD_WAVES;
     if (grid > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "block_delta: grid too large");
-    hipLaunchKernelGGL((block_delta_kernel<T, SPL>), dim3((unsigned)grid), dim3(BD_WAVES * 64), 0, p->ctx->stream,
+    const size_t lds = sizeof(double) * BD_WAVES * (size_t)(p->nbins > 0 ? p->nbins : 1);
+    static bool attr_set = false;
+    if (!attr_set) {
+        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(block_delta_kernel<T, SPL>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(double) * BD_WAVES * BD_MAXBINS)));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((block_delta_kernel<T, SPL>), dim3((unsigned)grid), dim3(BD_WAVES * 64), lds, p->ctx->stream,
                        static_cast<const T *>(x), off, len, nfiles, max_blocks, p->block_size, p->L, p->nfft,
                        p->d_window, p->d_tw, p->d_bins, p->band_hi - p->band_lo + 1 > 0 ? p->band_hi - p->band_lo + 1 : 0,
                        p->noise_hi - p->noise_lo + 1 > 0 ? p->noise_hi - p->noise_lo + 1 : 0, band_db, noise_db,
@@ -145,8 +152,8 @@ int launch_block_delta(msd_block_plan *p, const void *x, int dtype, const int64_
     if (nfiles == 0 || max_blocks == 0) return MSD_OK;
     const int nband = p->band_hi >= p->band_lo ? p->band_hi - p->band_lo + 1 : 0;
     const int nnoise = p->noise_hi >= p->noise_lo ? p->noise_hi - p->noise_lo + 1 : 0;
-    if (nband > BD_MAXBINS || nnoise > BD_MAXBINS)
-        return fail(MSD_ERR_UNSUPPORTED, "block_delta: at most 256 FFT bins per band");
+    if (nband + nnoise > BD_MAXBINS)
+        return fail(MSD_ERR_UNSUPPORTED, "block_delta: at most 4096 FFT bins in the two bands together");
     KernelTimer timer(p->ctx, K_BLOCK);
     switch (dtype) {
         case MSD_U8: return launch_bd_t<uint8_t>(p, x, off, len, nfiles, max_blocks, band_db, noise_db, delta, ld);

@@ -34,6 +34,7 @@ struct msd_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool timing = false;
+    bool force_generic = false;  // MSD_OPT_GENERIC_STFT
     std::vector<msd::EventPair> pending;  // recorded, not yet folded into totals
     std::vector<hipEvent_t> pool;         // reusable events
     double total_ms[msd::K_COUNT] = {0, 0, 0, 0};
@@ -80,6 +81,8 @@ int ctx_scratch(msd_ctx *ctx, int slot, size_t bytes, void **out);
 // launchers (defined in the kernel translation units)
 int launch_stft(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len, int64_t nfiles,
                 int64_t max_frames, float *out, int64_t ld);
+int launch_stft1024(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                    int64_t nfiles, float *out, int64_t ld);
 int launch_block_delta(msd_block_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                        int64_t nfiles, int64_t max_blocks, double *band_db, double *noise_db, double *delta,
                        int64_t ld);

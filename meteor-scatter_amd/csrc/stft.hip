@@ -299,6 +299,11 @@ int launch_stft(msd_stft_plan *p, const void *x, int dtype, const int64_t *off, 
     (void)max_frames;
     if (nfiles == 0) return MSD_OK;
     KernelTimer timer(p->ctx, K_STFT);
+    if (!p->ctx->force_generic) {
+        const int fast = launch_stft1024(p, x, dtype, off, len, nfiles, out, ld);
+        if (fast < 0) return fast;
+        if (fast == 1) return MSD_OK;
+    }
     switch (p->nperseg) {
         case 256: return launch_m<128, 8, 32>(p, x, dtype, off, len, nfiles, out, ld);
         case 512: return launch_m<256, 8, 32>(p, x, dtype, off, len, nfiles, out, ld);

@@ -34,6 +34,7 @@ DTYPE_CODES = {
 }
 
 K_STFT, K_BLOCK, K_DSTAT, K_DSCAN = 0, 1, 2, 3
+OPT_GENERIC_STFT = 1
 COMM_ID_BYTES = 128
 
 
@@ -89,6 +90,7 @@ _SIGS = [
     ("msd_memcpy_h2d", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("msd_memcpy_d2h", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("msd_memset_dev", C.c_int, [_P, _P, C.c_int, C.c_size_t]),
+    ("msd_set_option", C.c_int, [_P, C.c_int, C.c_int]),
     ("msd_timing_enable", C.c_int, [_P, C.c_int]),
     ("msd_timing_reset", C.c_int, [_P]),
     ("msd_timing_get", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
@@ -188,6 +190,9 @@ class Context:
     # ---- device memory
     def alloc(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
+
+    def set_option(self, option: int, value: int):
+        check(self.lib.msd_set_option(self.h, int(option), int(value)))
 
     def timing(self, enable: bool = True):
         check(self.lib.msd_timing_enable(self.h, 1 if enable else 0))

@@ -52,7 +52,7 @@ BLOCK_CASES = [
     (4000, 0.2, (950, 1050), (650, 750), 2048, np.float64, 4000 * 10),        # Nf=4096, L=800
     (6000, 0.2, (993, 1013), (690, 710), 512, np.uint8, 6000 * 5),
     (6000, 0.2, (993, 1013), (690, 710), 512, np.int32, 6000 * 5),
-    (5000, 0.3, (0, 2500), (100, 200), 300, np.int16, 5000 * 6),              # Nf=600 (not 2^k), wide band
+    (5000, 0.3, (0, 2500), (100, 200), 300, np.int16, 5000 * 6),              # Nf=600 (not 2^k), 301+21 bins
 ]
 
 
@@ -310,3 +310,21 @@ def test_full_day_batch_properties():
             assert abs(S[:, t].astype(np.float64).sum() - want) <= 1e-5 * want
     _, _, d0, _ = dsp.block_powers(pool[1], fs, 0.2, (950, 1050), (650, 750), 512)
     np.testing.assert_array_equal(deltas[1437], d0)
+
+
+@pytest.mark.parametrize("dt", [np.int16, np.float32, np.uint8])
+def test_stft_fast_path_matches_generic_kernel(dt):
+    """The specialised N=1024 kernel and the generic Stockham kernel agree (A/B switch)."""
+    x, _ = synth.synth_real(seed=77, fs=48000, duration_s=5.0, f0=1000.0, rate_per_min=60)
+    if np.dtype(dt) == np.float32:
+        x = (x / 32768.0).astype(np.float32)
+    elif np.dtype(dt) == np.uint8:
+        x = ((x.astype(np.int32) >> 8) + 128).astype(np.uint8)
+    ctx = dsp.context(0)
+    _, _, fast = dsp.spectrogram(x, fs=48000, nperseg=1024, noverlap=512)
+    ctx.set_option(_lib.OPT_GENERIC_STFT, 1)
+    try:
+        _, _, gen = dsp.spectrogram(x, fs=48000, nperseg=1024, noverlap=512)
+    finally:
+        ctx.set_option(_lib.OPT_GENERIC_STFT, 0)
+    assert _frame_err(fast, gen) <= 2e-6
