@@ -2,36 +2,42 @@
 // configuration: scipy.signal.spectrogram(x, fs, 'hann', 1024, 512) as called at
 // dsp/src/main.py:52-54 / :132-133 and BASELINE configs C1-C4).
 //
-// One wave = one frame at a time, 64 lanes x 8 complex points, all three radix-8
-// Stockham passes in registers:
-//   load   lane j holds z[j + 64 r] = x[2(j+64r)] + i x[2(j+64r)+1] (r = 0..7): one
-//          4-byte sample pair per lane per instruction, 256 B coalesced per wave;
-//   detrend/window in registers (frame mean: exact integer wave reduction);
-//   pass 1 (no twiddle) → LDS transpose → pass 2 → LDS transpose → pass 3 → lane j
-//          holds Z[j + 64 r] in natural order;
-//   post   conjugate partner Z[512-k] from lane (64-j) by ds_bpermute, real-spectrum
-//          split, |X|^2 * scale (x2 off DC/Nyquist) → LDS tile [513][32+1];
-// one workgroup = 16 waves = 32 frames per tile, 2 frames per wave; the tile is
-// written out as 128-B row segments (one dword per lane).  Workgroups are persistent
-// and walk a contiguous range of tiles, so the half-frame shared by neighbouring
-// tiles is re-read from L2, and each wave prefetches its next frame's samples
-// while computing the current one.
+// Mapping.  A wave transforms two frames at once (two independent
+// instruction streams, interleaved by the compiler), 64 lanes x 8 complex points
+// per frame, every radix-8 Stockham pass in registers:
+//   load    lane l holds z[l + 64 r] = x[2(l+64r)] + i x[2(l+64r)+1] (r = 0..7): one
+//           sample pair per lane per instruction, 256 B coalesced per wave;
+//   detrend frame mean from an exact integer reduction: DPP adds inside each row of
+//           16 lanes, then four v_readlane (no LDS round trip);
+//   pass 1  → LDS transpose → pass 2 → LDS transpose → pass 3: lane l computes the
+//           pass-3 butterfly pi(l) (pi(0)=0, pi(1)=32, pi(2i)=i, pi(2i+1)=64-i), so it
+//           holds Z[pi(l) + 64 r] and the conjugate partner Z[512 - k] lives in the
+//           adjacent lane l^1 (one DPP quad_perm per value);
+//   post    real-spectrum split, |X|^2 * scale (x2 off DC / Nyquist) → LDS tile
+//           [513][32] (row pitch 34: conflict-free 8-B writes of the frame pair).
+// One workgroup = 16 waves (4 per SIMD: one wave alone issues a VALU op only every
+// ~4 cycles, so the SIMD needs several) = one tile of 32 consecutive frames, one
+// frame pair per wave.  The tile leaves as 128-B row segments.  Workgroups are
+// persistent and walk a contiguous range of tiles (the half frame shared by
+// neighbouring tiles is re-read from L2); each wave loads its next tile's frame pair
+// into the sample registers as soon as the current pair is windowed.
 #include "msd_internal.h"
+
+#include <cstdlib>
 
 namespace msd {
 namespace {
 
-constexpr int F_NW = 16;             // waves per workgroup
-constexpr int F_TT = 32;             // frames per tile
-constexpr int F_FPW = F_TT / F_NW;   // frames per wave per tile (2)
-constexpr int F_K = 513;             // one-sided bins
-constexpr int F_PITCH = F_TT + 1;    // tile row pitch (floats): conflict-free dword writes
-constexpr int F_SCR = 640;           // float2 per wave scratch (padded 512)
+constexpr int F_NW = 16;                  // waves per workgroup (4 per SIMD)
+constexpr int F_TT = 32;                  // frames per tile
+constexpr int F_K = 513;                  // one-sided bins
+constexpr int F_PITCH = F_TT + 2;         // tile row pitch (floats)
+constexpr int F_SCRF = 576;               // float2 per frame scratch (phys(511) + 1, padded)
 constexpr int F_TILE_BYTES = ((F_K * F_PITCH * 4 + 15) / 16) * 16;
-constexpr int F_SCR_BYTES = F_NW * F_SCR * 8;
-// per-lane tables, laid out [r][lane] so that every read is lane-contiguous:
-// window pairs w[2(j+64r)], w[2(j+64r)+1]; pass-2 twiddles W64^{(j&7) r}; pass-3 W512^{j r}
-constexpr int F_TAB_OFF = F_TILE_BYTES + F_SCR_BYTES;
+constexpr int F_SCR_OFF = F_TILE_BYTES;
+constexpr int F_TAB_OFF = F_SCR_OFF + F_NW * F_SCRF * 8;
+// tables laid out [r][lane] (lane-contiguous reads): window pairs (8 rows),
+// pass-2 twiddles W64^{(l&7) r} and pass-3 twiddles W512^{pi(l) r} (rows r = 1..7)
 constexpr int F_LDS = F_TAB_OFF + (8 + 7 + 7) * 64 * 8;
 static_assert(F_LDS <= 160 * 1024, "LDS budget");
 
@@ -64,7 +70,9 @@ __device__ __forceinline__ void dft8(float2 *v) {
     v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
 }
 
-__device__ __forceinline__ int phys(int n) { return n + ((n >> 3) << 1); }
+// scratch index with 2 float2 of padding per 16: conflict-free 16-B pass-1 writes and
+// 8-B pass-2 writes, at most 2-way on the lane-contiguous reads
+__device__ __forceinline__ int phys(int n) { return n + ((n >> 4) << 1); }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -72,7 +80,27 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// raw sample pair storage per input type, and its conversion
+// DPP: v + v[lane ^ 1], v[lane ^ 2], mirrored half rows, mirrored rows → each lane
+// holds the sum of its row of 16
+__device__ __forceinline__ int row_sum_i(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);  // row_mirror
+    return v;
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum_f(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    v += dpp_f<0x141>(v);
+    v += dpp_f<0x140>(v);
+    return v;
+}
+
 template <typename T>
 struct PairIO;
 template <>
@@ -80,33 +108,60 @@ struct PairIO<int16_t> {
     using raw_t = uint32_t;
     static constexpr bool kInt = true;
     __device__ static raw_t load(const int16_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
-    __device__ static float lo(raw_t r) { return (float)(int16_t)(r & 0xffffu); }
-    __device__ static float hi(raw_t r) { return (float)(int16_t)(r >> 16); }
+    __device__ static raw_t zero() { return 0u; }
     __device__ static int ilo(raw_t r) { return (int)(int16_t)(r & 0xffffu); }
     __device__ static int ihi(raw_t r) { return (int)(int16_t)(r >> 16); }
+    __device__ static float lo(raw_t r) { return (float)ilo(r); }
+    __device__ static float hi(raw_t r) { return (float)ihi(r); }
 };
 template <>
 struct PairIO<uint8_t> {
     using raw_t = uint32_t;
     static constexpr bool kInt = true;
     __device__ static raw_t load(const uint8_t *p) { return *reinterpret_cast<const uint16_t *>(p); }
-    __device__ static float lo(raw_t r) { return (float)(r & 0xffu); }
-    __device__ static float hi(raw_t r) { return (float)((r >> 8) & 0xffu); }
+    __device__ static raw_t zero() { return 0u; }
     __device__ static int ilo(raw_t r) { return (int)(r & 0xffu); }
     __device__ static int ihi(raw_t r) { return (int)((r >> 8) & 0xffu); }
+    __device__ static float lo(raw_t r) { return (float)ilo(r); }
+    __device__ static float hi(raw_t r) { return (float)ihi(r); }
 };
 template <>
 struct PairIO<float> {
     using raw_t = float2;
     static constexpr bool kInt = false;
     __device__ static raw_t load(const float *p) { return *reinterpret_cast<const float2 *>(p); }
-    __device__ static float lo(raw_t r) { return r.x; }
-    __device__ static float hi(raw_t r) { return r.y; }
+    __device__ static raw_t zero() { return make_float2(0.f, 0.f); }
     __device__ static int ilo(raw_t) { return 0; }
     __device__ static int ihi(raw_t) { return 0; }
+    __device__ static float lo(raw_t r) { return r.x; }
+    __device__ static float hi(raw_t r) { return r.y; }
+};
+
+// per-file geometry kept in scalar registers while a workgroup walks its tiles
+struct FileCur {
+    int64_t f, ti;  // file, tile within file
+    int64_t nfr;    // frames in the file
+    int64_t base;   // element offset of the file
 };
 
 template <typename T>
+__device__ __forceinline__ void load_pair(const T *__restrict__ x, const FileCur &fc, int64_t t, int hop, int l,
+                                          typename PairIO<T>::raw_t (&raw)[2][8]) {
+    using IO = PairIO<T>;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        if (t + q < fc.nfr) {  // wave-uniform
+            const T *p = x + fc.base + (t + q) * (int64_t)hop + 2 * l;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) raw[q][r] = IO::load(p + 128 * r);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) raw[q][r] = IO::zero();
+        }
+    }
+}
+
+template <typename T, int MODE>  // MODE: 0 [K][T] out, 1 experiment frame-major, 2 experiment no store
 __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len,
     int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float scale4,
@@ -117,178 +172,198 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *tile = reinterpret_cast<float *>(smem);
     const int tid = threadIdx.x;
-    const int j = tid & 63;
+    const int l = tid & 63;
     const int wave = tid >> 6;
-    float2 *scr = reinterpret_cast<float2 *>(smem + F_TILE_BYTES) + wave * F_SCR;
-
-    // per-lane constant tables in LDS ([r][lane]): window pairs, pass-2/3 twiddles
+    float2 *scr = reinterpret_cast<float2 *>(smem + F_SCR_OFF) + wave * F_SCRF;
     float2 *t_win = reinterpret_cast<float2 *>(smem + F_TAB_OFF);
     float2 *t_tw2 = t_win + 8 * 64 - 64;  // rows r = 1..7
     float2 *t_tw3 = t_tw2 + 7 * 64;
+    auto pi_of = [](int i) { return i == 0 ? 0 : i == 1 ? 32 : (i & 1) ? 64 - (i >> 1) : (i >> 1); };
     for (int i = tid; i < 8 * 64; i += F_NW * 64) {
-        const int r = i >> 6, l = i & 63;
-        t_win[i] = *reinterpret_cast<const float2 *>(g_win + 2 * (l + 64 * r));
+        const int r = i >> 6, li = i & 63;
+        t_win[i] = *reinterpret_cast<const float2 *>(g_win + 2 * (li + 64 * r));
         if (r > 0) {
-            t_tw2[i] = g_tw[8 * (l & 7) * r];
-            t_tw3[i] = g_tw[l * r];
+            t_tw2[i] = g_tw[8 * (li & 7) * r];
+            t_tw3[i] = g_tw[pi_of(li) * r];
         }
     }
+    const int pi = pi_of(l);
+    const float2 pb = g_post[pi];  // exp(-2*pi*i*pi(l)/1024)
     __syncthreads();
-    const float2 pb = g_post[j];  // exp(-2*pi*i*j/1024)
-    const int partner = (64 - j) & 63;
 
     const int64_t tb = (int64_t)blockIdx.x * tiles_per_wg;
     const int64_t te = tb + tiles_per_wg < ntiles ? tb + tiles_per_wg : ntiles;
-
-    // frame sequence of this wave: (tile, fb) for tile in [tb, te), fb in [0, F_FPW)
-    auto frame_src = [&](int64_t tl, int fb, bool &valid) -> const T * {
-        const int64_t f = tl / tiles_per_file;
-        const int64_t t = (tl - f * tiles_per_file) * F_TT + wave * F_FPW + fb;
+    if (tb >= te) return;
+    auto file_at = [&](int64_t f, int64_t ti) {
+        FileCur c;
+        c.f = f;
+        c.ti = ti;
         const int64_t n = len[f];
-        const int64_t nfr = n >= 1024 ? (n - 1024) / hop + 1 : 0;
-        valid = t < nfr;
-        return x + off[f] + t * (int64_t)hop;
+        c.nfr = n >= 1024 ? (n - 1024) / hop + 1 : 0;
+        c.base = off[f];
+        return c;
     };
-    raw_t cur[8], nxt[8];
-    bool cur_ok = false, nxt_ok = false;
-    if (tb < te) {
-        const T *p = frame_src(tb, 0, cur_ok);
-        if (cur_ok) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) cur[r] = IO::load(p + 2 * (j + 64 * r));
-        }
-    }
+    auto advance = [&](const FileCur &c) {
+        return c.ti + 1 < tiles_per_file ? FileCur{c.f, c.ti + 1, c.nfr, c.base} : file_at(c.f + 1, 0);
+    };
+    FileCur cur = file_at(tb / tiles_per_file, tb % tiles_per_file);
+    const int wcol = wave * 2;  // the two tile columns (frames) of this wave
+
+    raw_t raw[2][8];
+    load_pair<T>(x, cur, cur.ti * F_TT + wcol, hop, l, raw);
 
     for (int64_t tl = tb; tl < te; ++tl) {
+        const bool has_next = tl + 1 < te;
+        const FileCur nxt = has_next ? advance(cur) : cur;
+        float2 v[2][8];
+        // ---- detrend + window (consumes raw)
+        {
+            float mean[2];
 #pragma unroll
-        for (int fb = 0; fb < F_FPW; ++fb) {
-            // prefetch the next frame of the sequence
-            {
-                const int64_t ntl = fb + 1 < F_FPW ? tl : tl + 1;
-                const int nfb = fb + 1 < F_FPW ? fb + 1 : 0;
-                nxt_ok = false;
-                if (ntl < te) {
-                    const T *p = frame_src(ntl, nfb, nxt_ok);
-                    if (nxt_ok) {
-#pragma unroll
-                        for (int r = 0; r < 8; ++r) nxt[r] = IO::load(p + 2 * (j + 64 * r));
-                    }
-                }
-            }
-            float pw[9];
-            if (cur_ok) {
-                float2 v[8];
-                float mean;
+            for (int q = 0; q < 2; ++q) {
                 if constexpr (IO::kInt) {
                     int s = 0;
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) s += IO::ilo(cur[r]) + IO::ihi(cur[r]);
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-                    mean = (float)((double)s * (1.0 / 1024.0));
+                    for (int r = 0; r < 8; ++r) s += IO::ilo(raw[q][r]) + IO::ihi(raw[q][r]);
+                    s = row_sum_i(s);
+                    const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
+                                    __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
+                    mean[q] = (float)((double)tot * (1.0 / 1024.0));
                 } else {
                     float s = 0.f;
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) s += IO::lo(cur[r]) + IO::hi(cur[r]);
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-                    mean = s * (1.0f / 1024.0f);
+                    for (int r = 0; r < 8; ++r) s += IO::lo(raw[q][r]) + IO::hi(raw[q][r]);
+                    s = row_sum_f(s);
+                    auto rl = [](float a, int lane) {
+                        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), lane));
+                    };
+                    const float tot = (rl(s, 0) + rl(s, 16)) + (rl(s, 32) + rl(s, 48));
+                    mean[q] = tot * (1.0f / 1024.0f);
                 }
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const float2 w = t_win[r * 64 + j];
-                    v[r] = make_float2((IO::lo(cur[r]) - mean) * w.x, (IO::hi(cur[r]) - mean) * w.y);
-                }
-                // pass 1 (Ns = 1): out[8 j + r]
-                dft8(v);
-#pragma unroll
-                for (int r = 0; r < 8; r += 2)
-                    *reinterpret_cast<float4 *>(&scr[phys(8 * j + r)]) = make_float4(v[r].x, v[r].y, v[r + 1].x,
-                                                                                       v[r + 1].y);
-                wave_sync();
-#pragma unroll
-                for (int r = 0; r < 8; ++r) v[r] = scr[phys(j + 64 * r)];
-                wave_sync();
-                // pass 2 (Ns = 8): out[64 (j>>3) + (j&7) + 8 r]
-#pragma unroll
-                for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], t_tw2[r * 64 + j]);
-                dft8(v);
-                const int o2 = 64 * (j >> 3) + (j & 7);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) scr[phys(o2 + 8 * r)] = v[r];
-                wave_sync();
-#pragma unroll
-                for (int r = 0; r < 8; ++r) v[r] = scr[phys(j + 64 * r)];
-                wave_sync();
-                // pass 3 (Ns = 64): lane j holds Z[j + 64 r]
-#pragma unroll
-                for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], t_tw3[r * 64 + j]);
-                dft8(v);
-                // X' = 2X = (Z + conj Zm) + W^k (-i)(Z - conj Zm), Zm = Z[(512 - k) mod 512] from lane
-                // (64 - j) register 7 - r (lane 0 pairs with itself: register (8 - r) & 7); W^k = pb * W16^r
-                float2 wk = pb;
-                const float2 w16 = make_float2(0.92387953251128675613f, -0.38268343236508977173f);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const float2 sv = v[7 - r];
-                    float2 m = make_float2(__shfl(sv.x, partner, 64), __shfl(sv.y, partner, 64));
-                    if (j == 0) m = v[(8 - r) & 7];
-                    const float2 z = v[r];
-                    const float2 e = make_float2(z.x + m.x, z.y - m.y);
-                    const float2 o = make_float2(z.y + m.y, m.x - z.x);  // -i (z - conj m)
-                    const float2 X = cadd(e, cmul(wk, o));
-                    pw[r] = (X.x * X.x + X.y * X.y) * (2.0f * scale4);
-                    if (r == 0 && j == 0) {
-                        pw[0] = (X.x * X.x + X.y * X.y) * scale4;
-                        const float2 Xn = csub(e, o);  // k = 512: W = -1
-                        pw[8] = (Xn.x * Xn.x + Xn.y * Xn.y) * scale4;
-                    }
-                    wk = cmul(wk, w16);
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 9; ++r) pw[r] = 0.f;
             }
-            {
-                const int c = wave * F_FPW + fb;
 #pragma unroll
-                for (int r = 0; r < 8; ++r) tile[(j + 64 * r) * F_PITCH + c] = pw[r];
-                if (j == 0) tile[512 * F_PITCH + c] = pw[8];
-            }
-            cur_ok = nxt_ok;
+            for (int r = 0; r < 8; ++r) {
+                const float2 w = t_win[r * 64 + l];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-        }
-        __syncthreads();
-        // write the tile: rows k = 0..512, 32 floats (128 B) each; one dword per lane,
-        // conflict-free LDS reads at pitch 33, two full row segments per wave store
-        {
-            const int64_t f = tl / tiles_per_file;
-            const int64_t t0 = (tl - f * tiles_per_file) * F_TT;
-            float *of = out + f * (int64_t)F_K * ld + t0;
-            const int q = tid & 31;
-#pragma unroll
-            for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 32) {
-                const int k = k0 + (tid >> 5);
-                if (k < F_K) of[(int64_t)k * ld + q] = tile[k * F_PITCH + q];
+                for (int q = 0; q < 2; ++q)
+                    v[q][r] = make_float2((IO::lo(raw[q][r]) - mean[q]) * w.x, (IO::hi(raw[q][r]) - mean[q]) * w.y);
             }
         }
+        // ---- prefetch the next tile's frame pair into the (now free) sample registers
+        if (has_next) load_pair<T>(x, nxt, nxt.ti * F_TT + wcol, hop, l, raw);
+
+        // ---- pass 1 (Ns = 1): out[8 l + r].  One scratch per wave: frame A's transpose is
+        // read back before frame B's is written (LDS executes a wave's accesses in order)
+        dft8(v[0]);
+        dft8(v[1]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int r = 0; r < 8; r += 2)
+                *reinterpret_cast<float4 *>(&scr[phys(8 * l + r)]) =
+                    make_float4(v[q][r].x, v[q][r].y, v[q][r + 1].x, v[q][r + 1].y);
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[q][r] = scr[phys(l + 64 * r)];
+            wave_sync();
+        }
+        // ---- pass 2 (Ns = 8): out[64 (l>>3) + (l&7) + 8 r]
+        const int o2 = 64 * (l >> 3) + (l & 7);
+#pragma unroll
+        for (int r = 1; r < 8; ++r) {
+            const float2 w = t_tw2[r * 64 + l];
+            v[0][r] = cmul(v[0][r], w);
+            v[1][r] = cmul(v[1][r], w);
+        }
+        dft8(v[0]);
+        dft8(v[1]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) scr[phys(o2 + 8 * r)] = v[q][r];
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[q][r] = scr[phys(pi + 64 * r)];
+            wave_sync();
+        }
+        // ---- pass 3 (Ns = 64): butterfly pi(l) → lane holds Z[pi(l) + 64 r]
+#pragma unroll
+        for (int r = 1; r < 8; ++r) {
+            const float2 w = t_tw3[r * 64 + l];
+            v[0][r] = cmul(v[0][r], w);
+            v[1][r] = cmul(v[1][r], w);
+        }
+        dft8(v[0]);
+        dft8(v[1]);
+        // ---- post: X' = 2X = (Z + conj Zm) + W^k (-i)(Z - conj Zm), Zm = Z[(512 - k) mod 512]:
+        // lanes >= 2: lane l^1, register 7-r; lane 1 (k = 32 + 64 r): own register 7-r;
+        // lane 0 (k = 64 r): own register (8-r)&7.  W^k = pb * W16^r.  Each bin's pair of
+        // powers goes straight to the tile (frame A, frame B) as one 8-B write.
+        const float2 w16 = make_float2(0.92387953251128675613f, -0.38268343236508977173f);
+        float2 wk = pb;
+        float nyq[2];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            float pw[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float2 sv = v[q][7 - r];
+                float2 m = make_float2(dpp_f<0xB1>(sv.x), dpp_f<0xB1>(sv.y));
+                if (l < 2) m = (l == 0) ? v[q][(8 - r) & 7] : sv;
+                const float2 z = v[q][r];
+                const float2 e = make_float2(z.x + m.x, z.y - m.y);
+                const float2 o = make_float2(z.y + m.y, m.x - z.x);  // -i (z - conj m)
+                const float2 X = cadd(e, cmul(wk, o));
+                const float p2 = X.x * X.x + X.y * X.y;
+                pw[q] = p2 * (2.0f * scale4);
+                if (r == 0) {  // lane 0: DC (no doubling) and Nyquist k = 512 (W = -1)
+                    const float2 Xn = csub(e, o);
+                    nyq[q] = (Xn.x * Xn.x + Xn.y * Xn.y) * scale4;
+                    if (l == 0) pw[q] = p2 * scale4;
+                }
+            }
+            *reinterpret_cast<float2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = make_float2(pw[0], pw[1]);
+            wk = cmul(wk, w16);
+        }
+        if (l == 0) *reinterpret_cast<float2 *>(&tile[512 * F_PITCH + wcol]) = make_float2(nyq[0], nyq[1]);
         __syncthreads();
+        // ---- tile → HBM: 513 rows x 32 floats (128 B), 16 lanes x 8 B per row
+        if constexpr (MODE == 2) {
+        } else if constexpr (MODE == 1) {  // experiment: frame-major tile, 65.7 KB contiguous
+            float *of = out + ((cur.f * tiles_per_file + cur.ti) * (int64_t)F_TT) * F_K;
+            for (int o = tid; o < F_TT * F_K; o += F_NW * 64) {
+                const int c = o / F_K, k = o - c * F_K;
+                of[o] = tile[k * F_PITCH + c];
+            }
+        } else {
+            float *of = out + cur.f * (int64_t)F_K * ld + cur.ti * F_TT;
+            const int qq = tid & 15;
+#pragma unroll
+            for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 16) {
+                const int k = k0 + (tid >> 4);
+                if (k < F_K)
+                    *reinterpret_cast<float2 *>(&of[(int64_t)k * ld + 2 * qq]) =
+                        *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 2 * qq]);
+            }
+        }
+        __syncthreads();
+        cur = nxt;
     }
 }
 
 template <typename T>
 int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int64_t *len, int64_t nfiles, float *out,
                   int64_t ld) {
-    auto kern = stft1024_kernel<T>;
+    static const int mode = getenv("MSD_EXP_TMAJOR") ? 1 : getenv("MSD_EXP_NOSTORE") ? 2 : 0;
+    auto kern = mode == 1 ? stft1024_kernel<T, 1> : mode == 2 ? stft1024_kernel<T, 2> : stft1024_kernel<T, 0>;
     static bool attr_set = false;
     if (!attr_set) {
         MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
         attr_set = true;
     }
-    int dev = p->ctx->device, cus = 256;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    int cus = 256;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->ctx->device);
     const int64_t tiles_per_file = ld / F_TT;
     const int64_t ntiles = tiles_per_file * nfiles;
     int64_t wgs = cus;  // one 16-wave workgroup per CU (LDS-bound residency)

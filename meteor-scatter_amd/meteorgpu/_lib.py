@@ -13,7 +13,7 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).with_name("libmsdsp.so")
+LIB_PATH = Path(os.environ.get("MSD_LIB_PATH") or Path(__file__).with_name("libmsdsp.so"))
 
 MSD_OK = 0
 MSD_ERR_INVALID = -1
