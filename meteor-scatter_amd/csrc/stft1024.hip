@@ -10,9 +10,9 @@
 //   detrend frame mean from an exact integer reduction: DPP adds inside each row of
 //           16 lanes, then four v_readlane (no LDS round trip);
 //   pass 1  → LDS transpose → pass 2 → LDS transpose → pass 3: lane l computes the
-//           pass-3 butterfly pi(l) (pi(0)=0, pi(1)=32, pi(2i)=i, pi(2i+1)=64-i), so it
-//           holds Z[pi(l) + 64 r] and the conjugate partner Z[512 - k] lives in the
-//           adjacent lane l^1 (one DPP quad_perm per value);
+//           pass-3 butterfly pi(l) (a table: conjugate pairs j, 64-j in adjacent lanes,
+//           pi(0)=0, pi(1)=32), so it holds Z[pi(l) + 64 r] and the conjugate partner
+//           Z[512 - k] lives in lane l^1 (one DPP quad_perm per value);
 //   post    real-spectrum split, |X|^2 * scale (x2 off DC / Nyquist) → LDS tile
 //           [513][32] (row pitch 34: conflict-free 8-B writes of the frame pair).
 // One workgroup = 16 waves (4 per SIMD: one wave alone issues a VALU op only every
@@ -32,13 +32,14 @@ constexpr int F_NW = 16;                  // waves per workgroup (4 per SIMD)
 constexpr int F_TT = 32;                  // frames per tile
 constexpr int F_K = 513;                  // one-sided bins
 constexpr int F_PITCH = F_TT + 2;         // tile row pitch (floats)
-constexpr int F_SCRF = 576;               // float2 per frame scratch (phys(511) + 1, padded)
+constexpr int F_SCRF = 576;               // float2 per frame scratch (phys(511) = 571)
 constexpr int F_TILE_BYTES = ((F_K * F_PITCH * 4 + 15) / 16) * 16;
 constexpr int F_SCR_OFF = F_TILE_BYTES;
 constexpr int F_TAB_OFF = F_SCR_OFF + F_NW * F_SCRF * 8;
 // tables laid out [r][lane] (lane-contiguous reads): window pairs (8 rows),
-// pass-2 twiddles W64^{(l&7) r} and pass-3 twiddles W512^{pi(l) r} (rows r = 1..7)
-constexpr int F_LDS = F_TAB_OFF + (8 + 7 + 7) * 64 * 8;
+// pass-2 twiddles W64^{(l&7) r} and pass-3 twiddles W512^{pi(l) r} (rows r = 1..7),
+// post twiddles W1024^{pi(l) + 64 r} (8 rows)
+constexpr int F_LDS = F_TAB_OFF + (8 + 7 + 7 + 8) * 64 * 8;
 static_assert(F_LDS <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -70,9 +71,22 @@ __device__ __forceinline__ void dft8(float2 *v) {
     v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
 }
 
-// scratch index with 2 float2 of padding per 16: conflict-free 16-B pass-1 writes and
-// 8-B pass-2 writes, at most 2-way on the lane-contiguous reads
-__device__ __forceinline__ int phys(int n) { return n + ((n >> 4) << 1); }
+// Transpose-scratch layout (float2 index): bit 4 of n flips bits 1 and 3, plus 4 float2 of
+// padding per 32.  Together with the pass-3 lane table below it makes all four transpose
+// access patterns (16-B pass-1 writes, 8-B reads, 8-B pass-2 writes, pass-3 reads) free of
+// bank conflicts under the gfx950 LDS model — found by tools/lds_swizzle_search.py.
+__device__ __forceinline__ int phys(int n) { return (n ^ (((n >> 4) & 1) * 10)) + ((n >> 5) << 2); }
+
+// pass-3 butterfly of each lane: conjugate pairs (j, 64-j) in adjacent lanes, (0, 32) in
+// lanes 0/1, grouped so that the pass-3 reads are conflict-free (tools/lds_swizzle_search.py)
+__constant__ int8_t k_pass3_lane[64] = {0,  32, 1,  63, 3,  61, 5,  59, 6,  58, 7,  57, 12, 52, 14, 50,
+                                        13, 51, 15, 49, 16, 48, 18, 46, 25, 39, 26, 38, 27, 37, 28, 36,
+                                        2,  62, 4,  60, 8,  56, 9,  55, 10, 54, 11, 53, 17, 47, 19, 45,
+                                        20, 44, 21, 43, 22, 42, 23, 41, 24, 40, 29, 35, 30, 34, 31, 33};
+
+// workgroup barrier that orders LDS only: waits for this wave's LDS accesses, not for
+// its global stores (the tile write-out) or loads (the prefetch) still in flight
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -178,7 +192,8 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     float2 *t_win = reinterpret_cast<float2 *>(smem + F_TAB_OFF);
     float2 *t_tw2 = t_win + 8 * 64 - 64;  // rows r = 1..7
     float2 *t_tw3 = t_tw2 + 7 * 64;
-    auto pi_of = [](int i) { return i == 0 ? 0 : i == 1 ? 32 : (i & 1) ? 64 - (i >> 1) : (i >> 1); };
+    float2 *t_post = t_tw3 + 8 * 64;  // rows r = 0..7 (t_tw3 rows end at 7 * 64 + 64)
+    auto pi_of = [](int i) { return (int)k_pass3_lane[i]; };
     for (int i = tid; i < 8 * 64; i += F_NW * 64) {
         const int r = i >> 6, li = i & 63;
         t_win[i] = *reinterpret_cast<const float2 *>(g_win + 2 * (li + 64 * r));
@@ -186,9 +201,9 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             t_tw2[i] = g_tw[8 * (li & 7) * r];
             t_tw3[i] = g_tw[pi_of(li) * r];
         }
+        t_post[i] = g_post[pi_of(li) + 64 * r];
     }
     const int pi = pi_of(l);
-    const float2 pb = g_post[pi];  // exp(-2*pi*i*pi(l)/1024)
     __syncthreads();
 
     const int64_t tb = (int64_t)blockIdx.x * tiles_per_wg;
@@ -297,14 +312,13 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         dft8(v[1]);
         // ---- post: X' = 2X = (Z + conj Zm) + W^k (-i)(Z - conj Zm), Zm = Z[(512 - k) mod 512]:
         // lanes >= 2: lane l^1, register 7-r; lane 1 (k = 32 + 64 r): own register 7-r;
-        // lane 0 (k = 64 r): own register (8-r)&7.  W^k = pb * W16^r.  Each bin's pair of
-        // powers goes straight to the tile (frame A, frame B) as one 8-B write.
-        const float2 w16 = make_float2(0.92387953251128675613f, -0.38268343236508977173f);
-        float2 wk = pb;
-        float nyq[2];
+        // lane 0 (k = 64 r): own register (8-r)&7.  W^k from the LDS table.  The powers stay in
+        // registers until the tile is free (the previous tile's write-out has read it), so a
+        // wave's transform overlaps the other waves' write-out.
+        float pw[2][9];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            float pw[2];
+            const float2 wk = t_post[r * 64 + l];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const float2 sv = v[q][7 - r];
@@ -315,18 +329,20 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 const float2 o = make_float2(z.y + m.y, m.x - z.x);  // -i (z - conj m)
                 const float2 X = cadd(e, cmul(wk, o));
                 const float p2 = X.x * X.x + X.y * X.y;
-                pw[q] = p2 * (2.0f * scale4);
+                pw[q][r] = p2 * (2.0f * scale4);
                 if (r == 0) {  // lane 0: DC (no doubling) and Nyquist k = 512 (W = -1)
                     const float2 Xn = csub(e, o);
-                    nyq[q] = (Xn.x * Xn.x + Xn.y * Xn.y) * scale4;
-                    if (l == 0) pw[q] = p2 * scale4;
+                    pw[q][8] = (Xn.x * Xn.x + Xn.y * Xn.y) * scale4;
+                    if (l == 0) pw[q][0] = p2 * scale4;
                 }
             }
-            *reinterpret_cast<float2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = make_float2(pw[0], pw[1]);
-            wk = cmul(wk, w16);
         }
-        if (l == 0) *reinterpret_cast<float2 *>(&tile[512 * F_PITCH + wcol]) = make_float2(nyq[0], nyq[1]);
-        __syncthreads();
+        lds_barrier();  // the previous tile's write-out has finished reading the tile
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            *reinterpret_cast<float2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = make_float2(pw[0][r], pw[1][r]);
+        if (l == 0) *reinterpret_cast<float2 *>(&tile[512 * F_PITCH + wcol]) = make_float2(pw[0][8], pw[1][8]);
+        lds_barrier();  // tile complete
         // ---- tile → HBM: 513 rows x 32 floats (128 B), 16 lanes x 8 B per row
         if constexpr (MODE == 2) {
         } else if constexpr (MODE == 1) {  // experiment: frame-major tile, 65.7 KB contiguous
@@ -336,17 +352,22 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 of[o] = tile[k * F_PITCH + c];
             }
         } else {
-            float *of = out + cur.f * (int64_t)F_K * ld + cur.ti * F_TT;
-            const int qq = tid & 15;
+            // scalar base + 32-bit lane offsets (k*ld*4 < 2^32 for ld < 2^21); 8 lanes x 16 B
+            // per row: two 8-B LDS reads (pitch 34 keeps rows 8-B aligned) → one 16-B store
+            char *of = reinterpret_cast<char *>(out + cur.f * (int64_t)F_K * ld + cur.ti * F_TT);
+            const int qq = tid & 7;
+            const uint32_t ldb = (uint32_t)ld * 4u;
 #pragma unroll
-            for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 16) {
-                const int k = k0 + (tid >> 4);
-                if (k < F_K)
-                    *reinterpret_cast<float2 *>(&of[(int64_t)k * ld + 2 * qq]) =
-                        *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 2 * qq]);
+            for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 8) {
+                const int k = k0 + (tid >> 3);
+                if (k < F_K) {
+                    const float2 a = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq]);
+                    const float2 b = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq + 2]);
+                    *reinterpret_cast<float4 *>(of + ((uint32_t)k * ldb + 16u * (uint32_t)qq)) =
+                        make_float4(a.x, a.y, b.x, b.y);
+                }
             }
         }
-        __syncthreads();
         cur = nxt;
     }
 }

@@ -17,7 +17,7 @@ for f in sorted(glob.glob(f"{root}/p*/pmc_counter_collection.csv")):
         vals[k][c].append(v)
 out = {}
 for k, cs in vals.items():
-    short = k.split("(")[0].replace("void ", "").replace("msd::(anonymous namespace)::", "")
+    short = k.replace("void ", "").replace("msd::(anonymous namespace)::", "").split("(")[0]
     avg = {c: sum(v) / len(v) for c, v in cs.items()}
     out[short] = avg
     print(short)
