@@ -146,6 +146,8 @@ int msd_create(int device, msd_ctx **out) {
     MSD_HIP(hipSetDevice(device));
     auto *c = new msd_ctx();
     c->device = device;
+    hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device);
+    if (c->num_cu <= 0) c->num_cu = 256;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -401,7 +403,28 @@ int msd_block_plan_create(msd_ctx *ctx, int64_t block_size, int32_t nfft, const 
         const double a = -2.0 * M_PI * (double)m / (double)nfft;
         tw[m] = make_double2(std::cos(a), std::sin(a));
     }
+    // fast-path constants (block_delta.hip, block_delta2_kernel)
+    const int spl = L <= 256 ? 16 : L <= 512 ? 32 : L <= 1024 ? 64 : L <= 2048 ? 128 : 256;
+    p->spl = spl;
+    std::vector<double> bconst;
+    for (int k : bins) {
+        const double th = 2.0 * M_PI * (double)(k % nfft) / (double)nfft;
+        bconst.push_back(2.0 * std::cos(th));
+        bconst.push_back(std::cos(th));
+        bconst.push_back(-std::sin(th));
+    }
+    for (int k : bins) {
+        for (int seg = 0; seg < 16; ++seg) {
+            const int64_t m = ((int64_t)k * (seg * spl + spl - 1)) % nfft;
+            const double a = -2.0 * M_PI * (double)m / (double)nfft;
+            bconst.push_back(std::cos(a));
+            bconst.push_back(std::sin(a));
+        }
+    }
     hipError_t e = hipMalloc(&p->d_window, sizeof(double) * L);
+    if (e == hipSuccess) e = hipMalloc(&p->d_bconst, sizeof(double) * (bconst.size() + 1));
+    if (e == hipSuccess && !bconst.empty())
+        e = hipMemcpy(p->d_bconst, bconst.data(), sizeof(double) * bconst.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(double2) * nfft);
     if (e == hipSuccess) e = hipMalloc(&p->d_bins, sizeof(int) * (bins.size() + 1));
     if (e == hipSuccess) e = hipMemcpy(p->d_window, window, sizeof(double) * L, hipMemcpyHostToDevice);
@@ -423,6 +446,7 @@ void msd_block_plan_destroy(msd_block_plan *p) {
     hipFree(p->d_window);
     hipFree(p->d_tw);
     hipFree(p->d_bins);
+    hipFree(p->d_bconst);
     delete p;
 }
 

@@ -32,6 +32,7 @@ struct EventPair {
 
 struct msd_ctx {
     int device = 0;
+    int num_cu = 256;  // compute units (persistent-grid sizing)
     hipStream_t stream = nullptr;
     bool timing = false;
     bool force_generic = false;  // MSD_OPT_GENERIC_STFT
@@ -62,6 +63,10 @@ struct msd_block_plan {
     double *d_window = nullptr;           // [L]
     double2 *d_tw = nullptr;              // [nfft] exp(-2*pi*i*m/nfft)
     int *d_bins = nullptr;                // [nbins] bin indices, band first
+    // fast path (nbins <= 64): per bin {2cos th, cos th, -sin th}, then per (bin, 16-lane
+    // segment) the rotation exp(-i th (seg*SPL + SPL - 1)) — host-computed in float64
+    double *d_bconst = nullptr;
+    int spl = 0;                          // samples per lane segment of the fast path
 };
 
 namespace msd {

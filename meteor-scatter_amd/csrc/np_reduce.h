@@ -113,6 +113,13 @@ __device__ double np_sum(const A &a, int64_t base, int64_t n) {
     return s;
 }
 
+// np.sum for n <= 128 (a single pairwise leaf; no recursion stack)
+template <typename A>
+__device__ __forceinline__ double np_sum_small(const A &a, int64_t base, int64_t n) {
+#pragma clang fp contract(off)
+    return n == 0 ? 0.0 : 0.0 + np_pairwise_leaf(a, base, n);
+}
+
 struct ArrRef {
     const double *p;
     __device__ double operator()(int64_t i) const { return p[i]; }
