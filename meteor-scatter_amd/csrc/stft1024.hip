@@ -310,15 +310,20 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         }
         dft8(v[0]);
         dft8(v[1]);
-        // ---- post: X' = 2X = (Z + conj Zm) + W^k (-i)(Z - conj Zm), Zm = Z[(512 - k) mod 512]:
-        // lanes >= 2: lane l^1, register 7-r; lane 1 (k = 32 + 64 r): own register 7-r;
-        // lane 0 (k = 64 r): own register (8-r)&7.  W^k from the LDS table.  The powers stay in
-        // registers until the tile is free (the previous tile's write-out has read it), so a
+        // ---- post: X' = 2X = (Z + conj Zm) + W^k (-i)(Z - conj Zm), Zm = Z[(512 - k) mod 512],
+        // and from the same e, o the mirror bin X'[512 - k] = conj(e - W^k o).  Lane l owns the
+        // four pairs (k = pi(l) + 64 r, 512 - k), r = 0..3: Zm sits in lane l^1, register 7-r
+        // (one DPP quad_perm per value); lane 1 (k = 32 + 64 r): own register 7-r; lane 0
+        // (k = 64 r): own register (8-r)&7, its r = 0 pair being DC / Nyquist (no doubling), and
+        // it alone also owns the self-mirrored bin 256.  W^k from the LDS table.  The powers stay
+        // in registers until the tile is free (the previous tile's write-out has read it), so a
         // wave's transform overlaps the other waves' write-out.
-        float pw[2][9];
+        float pa[2][4], pb[2][4], p256[2];
+        const float sc0 = l == 0 ? scale4 : 2.0f * scale4;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < 4; ++r) {
             const float2 wk = t_post[r * 64 + l];
+            const float sc = r == 0 ? sc0 : 2.0f * scale4;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const float2 sv = v[q][7 - r];
@@ -327,21 +332,25 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 const float2 z = v[q][r];
                 const float2 e = make_float2(z.x + m.x, z.y - m.y);
                 const float2 o = make_float2(z.y + m.y, m.x - z.x);  // -i (z - conj m)
-                const float2 X = cadd(e, cmul(wk, o));
-                const float p2 = X.x * X.x + X.y * X.y;
-                pw[q][r] = p2 * (2.0f * scale4);
-                if (r == 0) {  // lane 0: DC (no doubling) and Nyquist k = 512 (W = -1)
-                    const float2 Xn = csub(e, o);
-                    pw[q][8] = (Xn.x * Xn.x + Xn.y * Xn.y) * scale4;
-                    if (l == 0) pw[q][0] = p2 * scale4;
-                }
+                const float2 t = cmul(wk, o);
+                const float2 X1 = cadd(e, t), X2 = csub(e, t);
+                pa[q][r] = (X1.x * X1.x + X1.y * X1.y) * sc;
+                pb[q][r] = (X2.x * X2.x + X2.y * X2.y) * sc;
             }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {  // lane 0: X'[256] = 2 conj(Z[256]) → |X'|^2 = 4 |Z[256]|^2
+            const float2 z = v[q][4];
+            p256[q] = (z.x * z.x + z.y * z.y) * (8.0f * scale4);
         }
         lds_barrier();  // the previous tile's write-out has finished reading the tile
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-            *reinterpret_cast<float2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = make_float2(pw[0][r], pw[1][r]);
-        if (l == 0) *reinterpret_cast<float2 *>(&tile[512 * F_PITCH + wcol]) = make_float2(pw[0][8], pw[1][8]);
+        for (int r = 0; r < 4; ++r) {
+            *reinterpret_cast<float2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = make_float2(pa[0][r], pa[1][r]);
+            *reinterpret_cast<float2 *>(&tile[(512 - pi - 64 * r) * F_PITCH + wcol]) =
+                make_float2(pb[0][r], pb[1][r]);
+        }
+        if (l == 0) *reinterpret_cast<float2 *>(&tile[256 * F_PITCH + wcol]) = make_float2(p256[0], p256[1]);
         lds_barrier();  // tile complete
         // ---- tile → HBM: 513 rows x 32 floats (128 B), 16 lanes x 8 B per row
         if constexpr (MODE == 2) {
