@@ -23,6 +23,7 @@
 // into the sample registers as soon as the current pair is windowed.
 #include "msd_internal.h"
 
+#include <cmath>
 #include <cstdlib>
 
 namespace msd {
@@ -57,11 +58,10 @@ __device__ __forceinline__ void dft4(float2 &a0, float2 &a1, float2 &a2, float2 
     a3 = csub(t1, t3);
 }
 
-// in-place forward DFT of 8 points, natural order in and out
-__device__ __forceinline__ void dft8(float2 *v) {
+// second half of a forward 8-point DFT: a_j = v_j + v_{j+4}, b_j = v_j - v_{j+4} given
+__device__ __forceinline__ void dft8_tail(float2 *v, float2 a0, float2 a1, float2 a2, float2 a3, float2 b0, float2 b1,
+                                          float2 b2, float2 b3) {
     const float s = 0.70710678118654752440f;
-    float2 a0 = cadd(v[0], v[4]), a1 = cadd(v[1], v[5]), a2 = cadd(v[2], v[6]), a3 = cadd(v[3], v[7]);
-    float2 b0 = csub(v[0], v[4]), b1 = csub(v[1], v[5]), b2 = csub(v[2], v[6]), b3 = csub(v[3], v[7]);
     b1 = make_float2((b1.x + b1.y) * s, (b1.y - b1.x) * s);
     b2 = mul_mi(b2);
     b3 = make_float2((b3.y - b3.x) * s, -(b3.x + b3.y) * s);
@@ -69,6 +69,25 @@ __device__ __forceinline__ void dft8(float2 *v) {
     dft4(b0, b1, b2, b3);
     v[0] = a0; v[2] = a1; v[4] = a2; v[6] = a3;
     v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
+}
+
+// in-place forward DFT of 8 points, natural order in and out
+__device__ __forceinline__ void dft8(float2 *v) {
+    dft8_tail(v, cadd(v[0], v[4]), cadd(v[1], v[5]), cadd(v[2], v[6]), cadd(v[3], v[7]), csub(v[0], v[4]),
+              csub(v[1], v[5]), csub(v[2], v[6]), csub(v[3], v[7]));
+}
+
+// dft8 of the windowed points d_j * w_j (componentwise), the window product of v_{j+4} shared
+// by the first-stage sum and difference: 3 ops per component pair instead of 4
+__device__ __forceinline__ void dft8_windowed(float2 *v, const float2 *d, const float2 *w) {
+    float2 a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float px = d[j + 4].x * w[j + 4].x, py = d[j + 4].y * w[j + 4].y;
+        a[j] = make_float2(__builtin_fmaf(d[j].x, w[j].x, px), __builtin_fmaf(d[j].y, w[j].y, py));
+        b[j] = make_float2(__builtin_fmaf(d[j].x, w[j].x, -px), __builtin_fmaf(d[j].y, w[j].y, -py));
+    }
+    dft8_tail(v, a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]);
 }
 
 // Transpose-scratch layout (float2 index): bit 4 of n flips bits 1 and 3, plus 4 float2 of
@@ -97,15 +116,15 @@ __device__ __forceinline__ void wave_sync() {
 // DPP: v + v[lane ^ 1], v[lane ^ 2], mirrored half rows, mirrored rows → each lane
 // holds the sum of its row of 16
 __device__ __forceinline__ int row_sum_i(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
-    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);  // row_mirror
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true);  // row_half_mirror
+    v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true);  // row_mirror
     return v;
 }
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float row_sum_f(float v) {
     v += dpp_f<0xB1>(v);
@@ -175,10 +194,10 @@ __device__ __forceinline__ void load_pair(const T *__restrict__ x, const FileCur
     }
 }
 
-template <typename T, int MODE>  // MODE: 0 [K][T] out, 1 experiment frame-major, 2 experiment no store
+template <typename T, int MODE>  // MODE: 0 [K][T] out; experiments: 1 frame-major, 2 no store, 3 L2-resident store
 __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len,
-    int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float scale4,
+    int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float wscale,
     const float *__restrict__ g_win, const float2 *__restrict__ g_tw, const float2 *__restrict__ g_post,
     float *__restrict__ out, int64_t ld) {
     using IO = PairIO<T>;
@@ -196,7 +215,8 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     auto pi_of = [](int i) { return (int)k_pass3_lane[i]; };
     for (int i = tid; i < 8 * 64; i += F_NW * 64) {
         const int r = i >> 6, li = i & 63;
-        t_win[i] = *reinterpret_cast<const float2 *>(g_win + 2 * (li + 64 * r));
+        const float2 gw = *reinterpret_cast<const float2 *>(g_win + 2 * (li + 64 * r));
+        t_win[i] = make_float2(gw.x * wscale, gw.y * wscale);  // window * sqrt(scale / 2)
         if (r > 0) {
             t_tw2[i] = g_tw[8 * (li & 7) * r];
             t_tw3[i] = g_tw[pi_of(li) * r];
@@ -226,12 +246,45 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 
     raw_t raw[2][8];
     load_pair<T>(x, cur, cur.ti * F_TT + wcol, hop, l, raw);
+    // ---- tile → HBM: 513 rows x 32 floats (128 B), 8 lanes x 16 B per row.  Issued one
+    // iteration late (after the next tile's detrend), so the stores drain during that tile's
+    // transform and the prefetched samples waited for at the top of the loop are never younger
+    // than a tile's stores.
+    auto write_out = [&](const FileCur &wc) {
+        if constexpr (MODE == 2) {
+        } else if constexpr (MODE == 1) {  // experiment: frame-major tile, 65.7 KB contiguous
+            float *of = out + ((wc.f * tiles_per_file + wc.ti) * (int64_t)F_TT) * F_K;
+            for (int o = tid; o < F_TT * F_K; o += F_NW * 64) {
+                const int c = o / F_K, k = o - c * F_K;
+                of[o] = tile[k * F_PITCH + c];
+            }
+        } else {
+            // scalar base + 32-bit lane offsets (k*ld*4 < 2^32 for ld < 2^21); 8 lanes x 16 B
+            // per row: two 8-B LDS reads (pitch 34 keeps rows 8-B aligned) → one 16-B store
+            char *of = MODE == 3 ? reinterpret_cast<char *>(out + blockIdx.x * F_TT)  // experiment: L2-resident
+                                 : reinterpret_cast<char *>(out + wc.f * (int64_t)F_K * ld + wc.ti * F_TT);
+            const int qq = tid & 7;
+            const uint32_t ldb = (uint32_t)ld * 4u;
+#pragma unroll
+            for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 8) {
+                const int k = k0 + (tid >> 3);
+                if (k < F_K) {
+                    const float2 a = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq]);
+                    const float2 b = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq + 2]);
+                    *reinterpret_cast<float4 *>(of + ((uint32_t)k * ldb + 16u * (uint32_t)qq)) =
+                        make_float4(a.x, a.y, b.x, b.y);
+                }
+            }
+        }
+    };
+    FileCur prev = cur;
+    bool have_prev = false;
 
     for (int64_t tl = tb; tl < te; ++tl) {
         const bool has_next = tl + 1 < te;
         const FileCur nxt = has_next ? advance(cur) : cur;
-        float2 v[2][8];
-        // ---- detrend + window (consumes raw)
+        float2 v[2][8], wv[8];
+        // ---- detrend (consumes raw); the window is applied inside pass 1
         {
             float mean[2];
 #pragma unroll
@@ -258,19 +311,20 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             }
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
-                const float2 w = t_win[r * 64 + l];
+                wv[r] = t_win[r * 64 + l];
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
-                    v[q][r] = make_float2((IO::lo(raw[q][r]) - mean[q]) * w.x, (IO::hi(raw[q][r]) - mean[q]) * w.y);
+                    v[q][r] = make_float2(IO::lo(raw[q][r]) - mean[q], IO::hi(raw[q][r]) - mean[q]);
             }
         }
+        if (have_prev) write_out(prev);
         // ---- prefetch the next tile's frame pair into the (now free) sample registers
         if (has_next) load_pair<T>(x, nxt, nxt.ti * F_TT + wcol, hop, l, raw);
 
         // ---- pass 1 (Ns = 1): out[8 l + r].  One scratch per wave: frame A's transpose is
         // read back before frame B's is written (LDS executes a wave's accesses in order)
-        dft8(v[0]);
-        dft8(v[1]);
+        dft8_windowed(v[0], v[0], wv);
+        dft8_windowed(v[1], v[1], wv);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
 #pragma unroll
@@ -319,11 +373,12 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         // in registers until the tile is free (the previous tile's write-out has read it), so a
         // wave's transform overlaps the other waves' write-out.
         float pa[2][4], pb[2][4], p256[2];
-        const float sc0 = l == 0 ? scale4 : 2.0f * scale4;
+        // the window carries sqrt(scale / 2): |X'|^2 is the doubled one-sided density; lane 0's
+        // r = 0 pair (DC, Nyquist) is not doubled
+        const float sc0 = l == 0 ? 0.5f : 1.0f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float2 wk = t_post[r * 64 + l];
-            const float sc = r == 0 ? sc0 : 2.0f * scale4;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const float2 sv = v[q][7 - r];
@@ -334,15 +389,27 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 const float2 o = make_float2(z.y + m.y, m.x - z.x);  // -i (z - conj m)
                 const float2 t = cmul(wk, o);
                 const float2 X1 = cadd(e, t), X2 = csub(e, t);
-                pa[q][r] = (X1.x * X1.x + X1.y * X1.y) * sc;
-                pb[q][r] = (X2.x * X2.x + X2.y * X2.y) * sc;
+                pa[q][r] = X1.x * X1.x + X1.y * X1.y;
+                pb[q][r] = X2.x * X2.x + X2.y * X2.y;
+                if (r == 0) {
+                    pa[q][r] *= sc0;
+                    pb[q][r] *= sc0;
+                }
             }
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {  // lane 0: X'[256] = 2 conj(Z[256]) → |X'|^2 = 4 |Z[256]|^2
             const float2 z = v[q][4];
-            p256[q] = (z.x * z.x + z.y * z.y) * (8.0f * scale4);
+            p256[q] = (z.x * z.x + z.y * z.y) * 4.0f;
         }
+#ifdef MSD_EXP_PAD  // experiment: extra VALU per frame pair
+        {
+            float dmy = pa[0][0];
+#pragma unroll
+            for (int i = 0; i < MSD_EXP_PAD; ++i) asm volatile("v_add_f32 %0, %0, %1" : "+v"(dmy) : "v"(pb[0][1]));
+            pa[0][0] = dmy;
+        }
+#endif
         lds_barrier();  // the previous tile's write-out has finished reading the tile
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -352,40 +419,21 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         }
         if (l == 0) *reinterpret_cast<float2 *>(&tile[256 * F_PITCH + wcol]) = make_float2(p256[0], p256[1]);
         lds_barrier();  // tile complete
-        // ---- tile → HBM: 513 rows x 32 floats (128 B), 16 lanes x 8 B per row
-        if constexpr (MODE == 2) {
-        } else if constexpr (MODE == 1) {  // experiment: frame-major tile, 65.7 KB contiguous
-            float *of = out + ((cur.f * tiles_per_file + cur.ti) * (int64_t)F_TT) * F_K;
-            for (int o = tid; o < F_TT * F_K; o += F_NW * 64) {
-                const int c = o / F_K, k = o - c * F_K;
-                of[o] = tile[k * F_PITCH + c];
-            }
-        } else {
-            // scalar base + 32-bit lane offsets (k*ld*4 < 2^32 for ld < 2^21); 8 lanes x 16 B
-            // per row: two 8-B LDS reads (pitch 34 keeps rows 8-B aligned) → one 16-B store
-            char *of = reinterpret_cast<char *>(out + cur.f * (int64_t)F_K * ld + cur.ti * F_TT);
-            const int qq = tid & 7;
-            const uint32_t ldb = (uint32_t)ld * 4u;
-#pragma unroll
-            for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 8) {
-                const int k = k0 + (tid >> 3);
-                if (k < F_K) {
-                    const float2 a = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq]);
-                    const float2 b = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq + 2]);
-                    *reinterpret_cast<float4 *>(of + ((uint32_t)k * ldb + 16u * (uint32_t)qq)) =
-                        make_float4(a.x, a.y, b.x, b.y);
-                }
-            }
-        }
+        prev = cur;
+        have_prev = true;
         cur = nxt;
     }
+    write_out(prev);  // the last tile (complete since the loop's final barrier)
 }
 
 template <typename T>
 int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int64_t *len, int64_t nfiles, float *out,
                   int64_t ld) {
-    static const int mode = getenv("MSD_EXP_TMAJOR") ? 1 : getenv("MSD_EXP_NOSTORE") ? 2 : 0;
-    auto kern = mode == 1 ? stft1024_kernel<T, 1> : mode == 2 ? stft1024_kernel<T, 2> : stft1024_kernel<T, 0>;
+    static const int mode = getenv("MSD_EXP_TMAJOR") ? 1 : getenv("MSD_EXP_NOSTORE") ? 2 : getenv("MSD_EXP_L2STORE") ? 3 : 0;
+    auto kern = mode == 1   ? stft1024_kernel<T, 1>
+                : mode == 2 ? stft1024_kernel<T, 2>
+                : mode == 3 ? stft1024_kernel<T, 3>
+                            : stft1024_kernel<T, 0>;
     static bool attr_set = false;
     if (!attr_set) {
         MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -401,7 +449,7 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
     const int64_t per = (ntiles + wgs - 1) / wgs;
     wgs = (ntiles + per - 1) / per;
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(F_NW * 64), F_LDS, p->ctx->stream, static_cast<const T *>(x),
-                       off, len, tiles_per_file, ntiles, per, p->hop, static_cast<float>(p->scale * 0.25),
+                       off, len, tiles_per_file, ntiles, per, p->hop, static_cast<float>(std::sqrt(p->scale * 0.5)),
                        p->d_window, p->d_tw, p->d_post, out, ld);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
