@@ -1,0 +1,13 @@
+#!/bin/bash
+# One round's measurements on the GPU box: the default bench line, a rocprofv3 kernel-trace
+# summary of a short bench, and the PMC passes (tools/pmc_stft.sh).  Usage: tools/profile_round.sh TAG
+set -u
+TAG=${1:-r1}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/round_$TAG
+mkdir -p "$OUT"
+timeout -k 10 400 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- \
+    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/kt.log" 2>&1 || exit 1
+bash "$ROOT/tools/pmc_stft.sh" "$TAG"
