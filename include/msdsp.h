@@ -71,7 +71,8 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.
- * kernel id: 0 = STFT power, 1 = block delta, 2 = detector stats, 3 = detector scan. */
+ * kernel id: 0 = STFT power, 1 = block delta, 2 = detector stats, 3 = detector scan,
+ * 4 = Welch band powers, 5 = live detector. */
 int msd_timing_enable(msd_ctx *ctx, int enable);
 int msd_timing_reset(msd_ctx *ctx);
 int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
@@ -161,6 +162,76 @@ int msd_detect_dev(msd_ctx *ctx, const double *delta, const int64_t *nblocks, in
  * global mode: *thresholds receives the single threshold in thresholds[0]. */
 int msd_detect(msd_ctx *ctx, const double *delta, int64_t nb, const msd_det_cfg *cfg, msd_det *dets, int64_t cap,
                int64_t *count, double *thresholds, double *margin);
+
+/* ------------------------------------------------ a8: Welch band powers (phase 2)
+ * Replaces, per processing block of dsp/src/live/backend/processor.py:177-206 and :349-369:
+ *   f, psd = scipy.signal.welch(block, fs, nfft=n_fft)     (hann, nperseg 256, noverlap 128,
+ *                                                           constant detrend, density, mean)
+ *   P_band = np.sum(psd[(f >= lo) & (f <= hi)]);  dB = 10*log10(P_band) if P_band > 0 else -inf
+ * Samples are converted to float64 and multiplied by sample_scale first (soundfile's float
+ * conversion: 1/32768 for PCM16).  window: nperseg float64 (scipy get_window('hann', nperseg));
+ * scale: 1/(fs*sum(win^2)) as scipy computes it.  Bands are inclusive bin ranges of
+ * rfftfreq(nfft, 1/fs); hi < lo = empty band (P = 0 → -inf).  Arithmetic is float64. */
+#define MSD_WELCH_MAX_BANDS 8
+typedef struct {
+    int32_t block_size; /* int(proc_block_sec * fs) */
+    int32_t nperseg;    /* scipy default 256 (or block_size if shorter) */
+    int32_t noverlap;   /* scipy default nperseg // 2 */
+    int32_t nfft;       /* n_fft (>= nperseg) */
+    double sample_scale;
+    double scale;
+    int32_t nbands;
+    int32_t reserved;
+    int32_t band_lo[MSD_WELCH_MAX_BANDS];
+    int32_t band_hi[MSD_WELCH_MAX_BANDS];
+} msd_welch_cfg;
+typedef struct msd_welch_plan msd_welch_plan;
+int msd_welch_plan_create(msd_ctx *ctx, const msd_welch_cfg *cfg, const double *window, msd_welch_plan **out);
+void msd_welch_plan_destroy(msd_welch_plan *plan);
+/* batch, device-resident (off/len device int64 arrays as for the STFT); blocks of file f:
+ * (len[f] - block_size) / block_size + 1 (the reference's range(0, n - bs + 1, bs));
+ * band_db[(f*nbands + j)*ld + b].  psd (may be NULL): the per-block Welch PSD of the band
+ * bins, band after band, psd[(f*ld + b)*nslots + slot], nslots = sum of band widths. */
+int msd_welch_bands_dev(msd_welch_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                        int64_t nfiles, int64_t max_blocks, double *band_db, int64_t ld, double *psd);
+/* single signal, host buffers: band_db [nbands][nb] */
+int msd_welch_bands(msd_welch_plan *plan, const void *x, int dtype, int64_t n, double *band_db, int64_t *blocks);
+
+/* --------------------------------------------- a9: live detector state machine
+ * Replaces processor.py:391-507 (states aggregates.py:4-24) over per-block band dB
+ * rows (signal, noise 1, noise 2):
+ *   over = sig - mean(n1, n2); hist = the previous min(W, b) values of over (W = 0: all);
+ *   thr = mean(hist) + k*std(hist)  (NaN on the first block), replaced by the locked
+ *   threshold while Tracking, and while Detection with until > block end;
+ *   Init → Detection once block_start >= init_wait; Detection → Tracking when over > thr
+ *   (lock = thr + 0*std, start = block start, trigger block not in the history);
+ *   Tracking appends over and ends when over < thr: emit if mean >= min_db and
+ *   duration >= min_dur, then Detection(lock, until = block start + after_wait).
+ * Block b starts at (b*block_size)/fs seconds. */
+typedef struct {
+    int32_t block_size;
+    int32_t avg_win_blocks; /* int(avg_win_sec / proc_block_sec), processor.py:58 */
+    double fs;              /* the file's integer sample rate */
+    double k_std;
+    double init_wait_sec;
+    double after_tracking_wait_sec;
+    double min_db_mean;
+    double min_dur_sec;
+} msd_live_cfg;
+typedef struct { /* aggregates.py:66-74 DetectedMeteor (+ the block indices) */
+    int64_t start_block;
+    int64_t stop_block;
+    double time_start, time_stop, duration;
+    double db_min, db_max, db_mean, db_std;
+} msd_meteor;
+/* band_db: [(f*3 + j)*ld + b] as msd_welch_bands_dev writes it (3 bands); thresholds / over
+ * (may be NULL): [f*ld + b]; counts: meteors found per file (may exceed cap: only cap kept,
+ * status 3). */
+int msd_live_detect_dev(msd_ctx *ctx, const double *band_db, const int64_t *nblocks, int64_t nfiles, int64_t ld,
+                        const msd_live_cfg *cfg, msd_meteor *out, int64_t cap, int64_t *counts, double *thresholds,
+                        double *over, int32_t *status);
+int msd_live_detect(msd_ctx *ctx, const double *band_db /* [3][nb] */, int64_t nb, const msd_live_cfg *cfg,
+                    msd_meteor *out, int64_t cap, int64_t *count, double *thresholds, double *over);
 
 /* ------------------------------------------ multi-GPU: per-hour count reduction
  * RCCL (loaded at run time from librccl.so.1), one communicator per (process, GPU). */

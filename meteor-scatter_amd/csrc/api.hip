@@ -61,17 +61,6 @@ int ctx_scratch(msd_ctx *ctx, int slot, size_t bytes, void **out) {
     return MSD_OK;
 }
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) hipSetDevice(prev);
-    }
-};
-
 // ---------------------------------------------------------------- RCCL (dlopen)
 struct Rccl {
     void *h = nullptr;

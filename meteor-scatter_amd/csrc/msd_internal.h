@@ -21,7 +21,7 @@ int hip_fail(hipError_t e, const char *what);
         if (e_ != hipSuccess) return hip_fail(e_, #call); \
     } while (0)
 
-enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_COUNT = 4 };
+enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_WELCH = 4, K_LIVE = 5, K_COUNT = 6 };
 
 struct EventPair {
     hipEvent_t a, b;
@@ -38,8 +38,8 @@ struct msd_ctx {
     bool force_generic = false;  // MSD_OPT_GENERIC_STFT
     std::vector<msd::EventPair> pending;  // recorded, not yet folded into totals
     std::vector<hipEvent_t> pool;         // reusable events
-    double total_ms[msd::K_COUNT] = {0, 0, 0, 0};
-    int64_t launches[msd::K_COUNT] = {0, 0, 0, 0};
+    double total_ms[msd::K_COUNT] = {};
+    int64_t launches[msd::K_COUNT] = {};
     // scratch device buffers for the host-pointer convenience entry points
     void *scratch[4] = {nullptr, nullptr, nullptr, nullptr};
     size_t scratch_bytes[4] = {0, 0, 0, 0};
@@ -69,7 +69,28 @@ struct msd_block_plan {
     int spl = 0;                          // samples per lane segment of the fast path
 };
 
+struct msd_welch_plan {
+    msd_ctx *ctx = nullptr;
+    msd_welch_cfg cfg{};
+    int nseg = 0, step = 0;       // segments per block, nperseg - noverlap
+    int nslots = 0;               // bins computed per block (band ranges concatenated)
+    double *d_window = nullptr;   // [nperseg]
+    double *d_bins = nullptr;     // [nslots][4]: cos w, sin w, 2 cos w, doubling factor (1 or 2)
+};
+
 namespace msd {
+
+// makes `dev` current for the scope
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 // scoped timing of one kernel launch on ctx->stream
 struct KernelTimer {

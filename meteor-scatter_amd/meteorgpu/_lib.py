@@ -33,7 +33,7 @@ DTYPE_CODES = {
     np.dtype(np.float64): MSD_F64,
 }
 
-K_STFT, K_BLOCK, K_DSTAT, K_DSCAN = 0, 1, 2, 3
+K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE = 0, 1, 2, 3, 4, 5
 OPT_GENERIC_STFT = 1
 COMM_ID_BYTES = 128
 
@@ -76,6 +76,42 @@ class MsdHistCfg(C.Structure):
     ]
 
 
+WELCH_MAX_BANDS = 8
+
+
+class MsdWelchCfg(C.Structure):
+    _fields_ = [
+        ("block_size", C.c_int32),
+        ("nperseg", C.c_int32),
+        ("noverlap", C.c_int32),
+        ("nfft", C.c_int32),
+        ("sample_scale", C.c_double),
+        ("scale", C.c_double),
+        ("nbands", C.c_int32),
+        ("reserved", C.c_int32),
+        ("band_lo", C.c_int32 * WELCH_MAX_BANDS),
+        ("band_hi", C.c_int32 * WELCH_MAX_BANDS),
+    ]
+
+
+class MsdLiveCfg(C.Structure):
+    _fields_ = [
+        ("block_size", C.c_int32),
+        ("avg_win_blocks", C.c_int32),
+        ("fs", C.c_double),
+        ("k_std", C.c_double),
+        ("init_wait_sec", C.c_double),
+        ("after_tracking_wait_sec", C.c_double),
+        ("min_db_mean", C.c_double),
+        ("min_dur_sec", C.c_double),
+    ]
+
+
+METEOR_DTYPE = np.dtype([("start_block", np.int64), ("stop_block", np.int64), ("time_start", np.float64),
+                         ("time_stop", np.float64), ("duration", np.float64), ("db_min", np.float64),
+                         ("db_max", np.float64), ("db_mean", np.float64), ("db_std", np.float64)])
+
+
 # (name, restype, argtypes) — every symbol of include/msdsp.h
 _P = C.c_void_p
 _SIGS = [
@@ -110,6 +146,14 @@ _SIGS = [
       C.POINTER(MsdHistCfg)]),
     ("msd_detect", C.c_int,
      [_P, _P, C.c_int64, C.POINTER(MsdDetCfg), _P, C.c_int64, C.POINTER(C.c_int64), _P, _P]),
+    ("msd_welch_plan_create", C.c_int, [_P, C.POINTER(MsdWelchCfg), _P, C.POINTER(_P)]),
+    ("msd_welch_plan_destroy", None, [_P]),
+    ("msd_welch_bands_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64, _P]),
+    ("msd_welch_bands", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
+    ("msd_live_detect_dev", C.c_int,
+     [_P, _P, _P, C.c_int64, C.c_int64, C.POINTER(MsdLiveCfg), _P, C.c_int64, _P, _P, _P, _P]),
+    ("msd_live_detect", C.c_int,
+     [_P, _P, C.c_int64, C.POINTER(MsdLiveCfg), _P, C.c_int64, C.POINTER(C.c_int64), _P, _P]),
     ("msd_comm_get_unique_id", C.c_int, [_P]),
     ("msd_comm_init", C.c_int, [_P, C.c_int, _P, C.c_int, C.POINTER(_P)]),
     ("msd_comm_destroy", None, [_P]),
@@ -349,3 +393,65 @@ def detect(ctx: Context, delta: np.ndarray, cfg: MsdDetCfg, cap: int | None = No
     check(ctx.lib.msd_detect(ctx.h, ptr(d), int(nb), C.byref(cfg), ptr(dets), int(cap), C.byref(count), ptr(thr),
                              C.byref(margin)))
     return dets[: count.value], thr[:nb] if cfg.adaptive else thr, margin.value
+
+
+class WelchPlan:
+    """Per-block Welch band powers (include/msdsp.h a8)."""
+
+    def __init__(self, ctx: Context, cfg: MsdWelchCfg, window: np.ndarray):
+        self.ctx = ctx
+        w = np.ascontiguousarray(window, dtype=np.float64)
+        if w.shape != (cfg.nperseg,):
+            raise ValueError("window length must equal nperseg")
+        h = C.c_void_p()
+        check(ctx.lib.msd_welch_plan_create(ctx.h, C.byref(cfg), ptr(w), C.byref(h)))
+        self.h = h
+        self.cfg = cfg
+        self.nbands = int(cfg.nbands)
+        self.block_size = int(cfg.block_size)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.msd_welch_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def blocks(self, n: int) -> int:
+        return (n - self.block_size) // self.block_size + 1 if n >= self.block_size else 0
+
+    def run(self, x: np.ndarray) -> np.ndarray:
+        """band dB [nbands][nb] of one signal (host buffers)."""
+        x = np.ascontiguousarray(x)
+        nb = self.blocks(x.shape[0])
+        out = np.empty((self.nbands, nb), np.float64)
+        got = C.c_int64(0)
+        check(self.ctx.lib.msd_welch_bands(self.h, ptr(x), dtype_code(x.dtype), int(x.shape[0]), ptr(out),
+                                           C.byref(got)))
+        return out
+
+    def run_dev(self, x: DeviceBuffer, dtype, off: DeviceBuffer, length: DeviceBuffer, nfiles: int,
+                max_blocks: int, band_db: DeviceBuffer, ld: int, psd: DeviceBuffer | None = None):
+        check(self.ctx.lib.msd_welch_bands_dev(self.h, x.ptr, dtype_code(dtype), off.ptr, length.ptr, int(nfiles),
+                                               int(max_blocks), band_db.ptr, int(ld), psd.ptr if psd else None))
+
+
+def live_detect(ctx: Context, band_db: np.ndarray, cfg: MsdLiveCfg, cap: int | None = None):
+    """Live-detector state machine on host band dB rows [3][nb]: (meteors, thresholds, over)."""
+    b = np.ascontiguousarray(band_db, dtype=np.float64)
+    if b.ndim != 2 or b.shape[0] != 3:
+        raise ValueError("band_db must be [3][nb] (signal, noise 1, noise 2)")
+    nb = b.shape[1]
+    if cap is None:
+        cap = nb // 2 + 2
+    out = np.zeros(cap, dtype=METEOR_DTYPE)
+    thr = np.empty(max(nb, 1), np.float64)
+    over = np.empty(max(nb, 1), np.float64)
+    count = C.c_int64(0)
+    check(ctx.lib.msd_live_detect(ctx.h, ptr(b), int(nb), C.byref(cfg), ptr(out), int(cap), C.byref(count),
+                                  ptr(thr), ptr(over)))
+    return out[: count.value], thr[:nb], over[:nb]

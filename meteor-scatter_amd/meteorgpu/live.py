@@ -1,0 +1,290 @@
+"""Drop-in for the reference's phase-2 live detector, dsp/src/live/backend/processor.py
+(``wav_file_process``) with the dataclasses of dsp/src/live/backend/aggregates.py.
+
+The per-block Welch PSD band powers (a8, processor.py:206 and :349-369) and the state
+machine (a9, processor.py:391-507) run on the GPU through libmsdsp
+(``msd_welch_bands*``, ``msd_live_detect*``); there is no CPU fallback.  The plots
+(``enable_ui_plots``) and the per-detection spectrogram image export
+(``ConfigSpecExport.output_dir``) are figures, not the data path: asking for them raises
+``NotImplementedError``.
+
+Lower-level pieces: ``welch_band_db`` (band dB rows of one signal), ``live_detect`` (the
+state machine over band dB rows), ``LiveBatch`` (many recordings resident in HBM).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib, wav
+from .dsp import context, hann_periodic
+
+
+# ------------------------------------------------------------------ aggregates.py:4-74
+@dataclass
+class State:
+    pass
+
+
+@dataclass
+class StateInitialization(State):
+    history_channel_dB: list = field(default_factory=list)
+
+
+@dataclass
+class StateDetection(State):
+    locked_threshold: float = -1.0
+    use_locked_threshold_until_secs: float = -1.0
+
+
+@dataclass
+class StateTracking(State):
+    locked_threshold: float
+    time_start_detection: float
+    history_over_noise_sig_dB: list
+
+
+@dataclass
+class Config:
+    pass
+
+
+@dataclass
+class ConfigDetection(Config):
+    proc_block_sec: float = 0.2
+    n_fft: int = 4096
+    signal_freq: int = 1000
+    channel_width: int = 100
+    noise_channel_offset: int = 300
+    avg_win_sec: float = 8
+    init_detection_wait_sec: float = 8 * 1.0
+    after_tracking_wait_sec: float = 8 * 1.5
+    threshold_std_factor: float = 4
+    detection_db_over_noise_mean_min: float = -1
+    detection_dur_min_sec: float = -1
+
+
+@dataclass
+class ConfigVisualization(Config):
+    enable_ui_plots: bool = True
+    realtime_factor: float = 16
+    flag_realtime_animation: bool = True
+    max_range_sec: int = 60
+    limit_freq_offset_wf2_and_export: int = 100
+    wf_offset_vmin: int = 20
+    wf_offset_vmax: int = 20
+    enable_debug_logs: bool = False
+
+
+@dataclass
+class ConfigSpecExport(Config):
+    output_dir: str = ""
+    time_before_meteor_sec: int = 3
+    time_after_meteor_sec: int = 3
+
+
+@dataclass
+class DetectedMeteor:
+    time_start: float
+    time_stop: float
+    duration: float
+    db_min: float
+    db_max: float
+    db_mean: float
+    db_std: float
+
+
+# ------------------------------------------------------------------ configuration
+def band_edges(cfg: ConfigDetection):
+    """processor.py:32-45: [start, stop] in Hz of the signal band and the two noise bands."""
+    half = cfg.channel_width / 2
+    ms = (cfg.signal_freq - half, cfg.signal_freq + half)
+    n1 = ((cfg.signal_freq - cfg.noise_channel_offset) - half, (cfg.signal_freq - cfg.noise_channel_offset) + half)
+    n2 = ((cfg.signal_freq + cfg.noise_channel_offset) - half, (cfg.signal_freq + cfg.noise_channel_offset) + half)
+    return ms, n1, n2
+
+
+def _mask_bins(nfft: int, fs, lo: float, hi: float) -> tuple[int, int]:
+    """Inclusive bin range of (freqs >= lo) & (freqs <= hi) over scipy's welch frequencies
+    (sp_fft.rfftfreq(nfft, 1/fs)); (0, -1) when empty."""
+    freqs = np.fft.rfftfreq(nfft, 1 / fs)
+    idx = np.nonzero((freqs >= lo) & (freqs <= hi))[0]
+    if idx.size == 0:
+        return 0, -1
+    assert idx[-1] - idx[0] + 1 == idx.size
+    return int(idx[0]), int(idx[-1])
+
+
+def welch_cfg(fs, cfg: ConfigDetection, sample_scale: float = 1.0):
+    """scipy.signal.welch(block, fs, nfft=n_fft) defaults (window 'hann', nperseg 256 capped at
+    the block length, noverlap nperseg//2) → (msd_welch_cfg, window)."""
+    bs = int(cfg.proc_block_sec * fs)
+    if bs < 1:
+        raise ValueError("proc_block_sec * fs must give at least one sample per block")
+    nperseg = 256 if bs >= 256 else bs
+    noverlap = nperseg // 2
+    nfft = int(cfg.n_fft)
+    if nfft < nperseg:
+        raise ValueError("nfft must be greater than or equal to nperseg.")  # scipy's message
+    win = hann_periodic(nperseg)
+    wc = win.astype(np.complex128)
+    scale = np.real(1.0 / (fs * (wc * wc).sum()))  # scipy: win cast to the complex out dtype
+    c = _lib.MsdWelchCfg()
+    c.block_size, c.nperseg, c.noverlap, c.nfft = bs, nperseg, noverlap, nfft
+    c.sample_scale = float(sample_scale)
+    c.scale = float(scale)
+    c.nbands = 3
+    for j, (lo, hi) in enumerate(band_edges(cfg)):
+        c.band_lo[j], c.band_hi[j] = _mask_bins(nfft, fs, lo, hi)
+    return c, win
+
+
+def live_cfg(fs, cfg: ConfigDetection) -> _lib.MsdLiveCfg:
+    c = _lib.MsdLiveCfg()
+    c.block_size = int(cfg.proc_block_sec * fs)
+    c.avg_win_blocks = int(cfg.avg_win_sec / cfg.proc_block_sec)  # processor.py:58
+    c.fs = float(fs)
+    c.k_std = float(cfg.threshold_std_factor)
+    c.init_wait_sec = float(cfg.init_detection_wait_sec)
+    c.after_tracking_wait_sec = float(cfg.after_tracking_wait_sec)
+    c.min_db_mean = float(cfg.detection_db_over_noise_mean_min)
+    c.min_dur_sec = float(cfg.detection_dur_min_sec)
+    return c
+
+
+def _device_samples(data: np.ndarray):
+    """Samples as the kernels take them + the factor that turns them into soundfile's float64
+    (PCM16 / 32768, PCM32 and 24-bit-in-int32 / 2^31, 8-bit (x - 128) / 128)."""
+    if data.dtype == np.int16:
+        return data, 1.0 / 32768.0
+    if data.dtype == np.int32:
+        return data, 1.0 / 2147483648.0
+    if data.dtype == np.uint8:
+        return data.astype(np.int16) - 128, 1.0 / 128.0
+    if data.dtype in (np.float32, np.float64):
+        return data, 1.0
+    raise TypeError(f"unsupported sample dtype {data.dtype}")
+
+
+# ------------------------------------------------------------------ a8 / a9 entry points
+def welch_band_db(x: np.ndarray, fs, config_detection: ConfigDetection, sample_scale: float = 1.0,
+                  device: int = 0) -> np.ndarray:
+    """Per-block (signal, noise 1, noise 2) dB, float64 [3][nb] (processor.py:206, :349-369)."""
+    c, win = welch_cfg(fs, config_detection, sample_scale)
+    plan = _lib.WelchPlan(context(device), c, win)
+    try:
+        return plan.run(np.ascontiguousarray(x))
+    finally:
+        plan.close()
+
+
+def live_detect(band_db: np.ndarray, fs, config_detection: ConfigDetection, device: int = 0):
+    """The state machine (processor.py:391-507): (list[DetectedMeteor], thresholds, over_noise)."""
+    rows, thr, over = _lib.live_detect(context(device), band_db, live_cfg(fs, config_detection))
+    mets = [DetectedMeteor(float(r["time_start"]), float(r["time_stop"]), float(r["duration"]), float(r["db_min"]),
+                           float(r["db_max"]), float(r["db_mean"]), float(r["db_std"])) for r in rows]
+    return mets, thr, over
+
+
+def wav_file_process(wav_file_path: str,
+                     config_detection: ConfigDetection,
+                     config_visualization: ConfigVisualization,
+                     config_spec_export: ConfigSpecExport,
+                     wav_file_start_sec: float = 0,
+                     wav_file_stop_sec: float = -1,
+                     *,
+                     required_sample_rate=4000,
+                     device: int = 0):
+    """GPU drop-in for processor.py:14-543 (same arguments, asserts and printed results).
+    Returns the detected meteors (the reference returns None and only prints them)."""
+    assert os.path.exists(wav_file_path), f"File not found: {wav_file_path}"
+    if config_spec_export.output_dir != "":
+        assert os.path.exists(config_spec_export.output_dir), \
+            f"Output Directory not found: {config_spec_export.output_dir}"
+    if config_visualization.enable_ui_plots or config_spec_export.output_dir != "":
+        raise NotImplementedError("UI plots and the spectrogram image export are not part of the GPU drop-in; "
+                                  "set enable_ui_plots=False and output_dir=''")
+    file_sample_rate, data = wav.read(wav_file_path)
+    if required_sample_rate is not None:
+        assert file_sample_rate == required_sample_rate, f"Invalid Sample Rate: {file_sample_rate}"
+    start = int(wav_file_start_sec * file_sample_rate)
+    if wav_file_stop_sec != -1:
+        data = data[start:int(wav_file_stop_sec * file_sample_rate)]
+    else:
+        data = data[start:]
+    if data.ndim > 1:
+        print("WARNING: Multichannel file detected. Using first channel only.")
+        data = data[:, 0]
+    x, sample_scale = _device_samples(np.ascontiguousarray(data))
+    bdb = welch_band_db(x, file_sample_rate, config_detection, sample_scale, device)
+    meteors, _, _ = live_detect(bdb, file_sample_rate, config_detection, device)
+    for i, m in enumerate(meteors):
+        print("Detected Meteor:", m, "Now Detected Meteors:", i + 1)
+    return meteors
+
+
+# ------------------------------------------------------------------ batch (device-resident)
+class LiveBatch:
+    """Many equal-format recordings resident in HBM: one Welch launch + one detector launch.
+
+    HBM: x [nfiles][n_pad] samples, band_db [nfiles][3][ld], over / thr [nfiles][ld],
+    meteors [nfiles][cap]."""
+
+    def __init__(self, ctx: _lib.Context, nfiles: int, n_per_file: int, fs, cfg: ConfigDetection,
+                 dtype=np.int16, sample_scale: float = 1.0 / 32768.0, cap: int = 1024):
+        self.ctx, self.nfiles, self.n, self.fs = ctx, int(nfiles), int(n_per_file), fs
+        self.dtype = np.dtype(dtype)
+        wc, win = welch_cfg(fs, cfg, sample_scale)
+        self.plan = _lib.WelchPlan(ctx, wc, win)
+        self.lcfg = live_cfg(fs, cfg)
+        self.nb = self.plan.blocks(self.n)
+        self.ld = max(1, self.nb)
+        self.cap = int(cap)
+        es = self.dtype.itemsize
+        self.n_pad = (self.n + 7) // 8 * 8
+        F = self.nfiles
+        self.d_x = ctx.alloc(F * self.n_pad * es)
+        self.d_off = ctx.alloc(F * 8)
+        self.d_len = ctx.alloc(F * 8)
+        self.d_nb = ctx.alloc(F * 8)
+        self.d_off.upload(np.arange(F, dtype=np.int64) * self.n_pad)
+        self.d_len.upload(np.full(F, self.n, np.int64))
+        self.d_nb.upload(np.full(F, self.nb, np.int64))
+        self.d_band = ctx.alloc(F * 3 * self.ld * 8)
+        self.d_over = ctx.alloc(F * self.ld * 8)
+        self.d_thr = ctx.alloc(F * self.ld * 8)
+        self.d_met = ctx.alloc(F * self.cap * _lib.METEOR_DTYPE.itemsize)
+        self.d_counts = ctx.alloc(F * 8)
+        self.d_status = ctx.alloc(F * 4)
+
+    def upload_file(self, i: int, x: np.ndarray):
+        x = np.ascontiguousarray(x, dtype=self.dtype)
+        if x.shape != (self.n,):
+            raise ValueError("file length differs from the batch's")
+        self.d_x.upload(x, byte_offset=i * self.n_pad * self.dtype.itemsize)
+
+    def run(self):
+        lib, h = self.ctx.lib, self.ctx.h
+        self.plan.run_dev(self.d_x, self.dtype, self.d_off, self.d_len, self.nfiles, self.nb, self.d_band, self.ld)
+        _lib.check(lib.msd_live_detect_dev(h, self.d_band.ptr, self.d_nb.ptr, self.nfiles, self.ld, self.lcfg,
+                                           self.d_met.ptr, self.cap, self.d_counts.ptr, self.d_thr.ptr,
+                                           self.d_over.ptr, self.d_status.ptr))
+
+    def band_db(self) -> np.ndarray:
+        out = np.empty((self.nfiles, 3, self.ld), np.float64)
+        self.d_band.download(out)
+        return out[:, :, : self.nb]
+
+    def meteors(self):
+        counts = np.empty(self.nfiles, np.int64)
+        self.d_counts.download(counts)
+        rows = np.empty((self.nfiles, self.cap), _lib.METEOR_DTYPE)
+        self.d_met.download(rows)
+        return [rows[i, : min(counts[i], self.cap)] for i in range(self.nfiles)], counts
+
+    def thresholds(self) -> np.ndarray:
+        out = np.empty((self.nfiles, self.ld), np.float64)
+        self.d_thr.download(out)
+        return out[:, : self.nb]

@@ -10,8 +10,12 @@ exactly as the reference makes them, on seeded synthetic inputs:
                  (mb_files, main.py:825-899) and a 48 kHz configuration
   spec_*.npz   : scipy.signal.spectrogram(x, fs, 'hann', nperseg=N, noverlap=N//2,
                  nfft=N, scaling='density', mode='psd') (main.py:132-133), float32
+  live_4k.npz  : per processing block, scipy.signal.welch(block, fs, nfft=n_fft) on the
+                 soundfile float64 of PCM16 samples (x / 32768), the three inclusive band
+                 masks and np.sum → dB (dsp/src/live/backend/processor.py:206, :349-369),
+                 plus two blocks' full Welch PSD
 
-Run:  python tests/golden/make_golden.py
+Run:  python tests/golden/make_golden.py [name ...]   (default: all)
 """
 import os
 import sys
@@ -40,7 +44,34 @@ def blocks(x, fs, bs, band, noise, n_fft):
     return out
 
 
-def main():
+def live_golden():
+    from scipy.signal import welch
+    fs, bs, n_fft, f0 = 4000, 0.2, 4096, 1000
+    x, _ = synth_real(seed=4242, fs=fs, duration_s=40.0, f0=f0, sigma=300.0, rate_per_min=12, band_hz=100.0,
+                      snr_db=(15, 30), dur_s=(0.4, 2.0))
+    xf = x.astype(np.float64) / 32768.0                       # soundfile's PCM16 → float64
+    B = int(bs * fs)
+    bands = [(f0 - 50, f0 + 50), (f0 - 300 - 50, f0 - 300 + 50), (f0 + 300 - 50, f0 + 300 + 50)]
+    rows, psd2 = [], []
+    for k, i in enumerate(range(0, len(xf) - B + 1, B)):
+        f, p = welch(xf[i:i + B], fs, nfft=n_fft)
+        r = []
+        for lo, hi in bands:
+            P = np.sum(p[(f >= lo) & (f <= hi)])
+            r.append(10 * np.log10(P) if P > 0 else -np.inf)
+        rows.append(r)
+        if k in (3, 77):
+            psd2.append(p)
+    np.savez_compressed(os.path.join(HERE, "live_4k.npz"), x=x, fs=fs, bs=bs, n_fft=n_fft, f0=f0,
+                        bands=np.array(bands, dtype=np.float64), expected=np.array(rows).T,
+                        psd_blocks=np.array([3, 77]), psd=np.array(psd2))
+
+
+def main(names=()):
+    if not names or "live" in names:
+        live_golden()
+    if names and "core" not in names:
+        return
     # 6 kHz, the reference's own configuration (main.py:827-833, 865-899)
     x6, _ = synth_real(seed=1, fs=6000, duration_s=20.0, f0=1003.0, rate_per_min=12, band_hz=20.0)
     b6 = blocks(x6, 6000, 0.2, (993, 1013), (690, 710), 512)
@@ -67,4 +98,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -1,0 +1,152 @@
+"""GPU parity of the phase-2 live detector: the HIP Welch band powers
+and state machine, called through the C-ABI, against the scipy golden and the oracle.
+
+Bars: band dB within DB_TOL of scipy (float64 Goertzel vs pocketfft rounding); the state
+machine bit-exact on identical band rows; end to end, identical detection blocks and
+times, dB statistics within STAT_TOL."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import live_oracle as L
+
+pytestmark = pytest.mark.gpu
+
+DB_TOL = 1e-9
+STAT_TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def live():
+    from meteorgpu import live as LV
+    return LV
+
+
+def _ref_cfg(c):
+    return L.ConfigDetectionRef(**{k: getattr(c, k) for k in L.ConfigDetectionRef.__dataclass_fields__})
+
+
+def test_welch_band_db_golden(live, golden_dir):
+    g = np.load(os.path.join(golden_dir, "live_4k.npz"))
+    cfg = live.ConfigDetection(n_fft=int(g["n_fft"]), signal_freq=int(g["f0"]))
+    got = live.welch_band_db(g["x"], int(g["fs"]), cfg, sample_scale=1 / 32768)
+    assert got.shape == g["expected"].shape
+    np.testing.assert_allclose(got, g["expected"], rtol=0, atol=DB_TOL)
+
+
+@pytest.mark.parametrize("fs,bs,nfft,f0,dtype", [
+    (4000, 0.2, 4096, 1000, np.int16),
+    (4000, 0.5, 4096, 1020, np.int16),
+    (4000, 0.2, 2048, 1025, np.float64),
+    (8000, 0.1, 1024, 1500, np.int16),
+    (4000, 0.05, 512, 1000, np.int16),     # 200-sample blocks: nperseg capped at the block
+])
+def test_welch_band_db_vs_oracle(live, fs, bs, nfft, f0, dtype):
+    from meteorgpu import synth
+    x, _ = synth.synth_real(seed=int(fs * bs) + nfft, fs=fs, duration_s=6.0, f0=f0, sigma=500, rate_per_min=20)
+    if dtype == np.float64:
+        xin, sc = x.astype(np.float64) / 32768.0, 1.0
+    else:
+        xin, sc = x, 1 / 32768
+    cfg = live.ConfigDetection(proc_block_sec=bs, n_fft=nfft, signal_freq=f0)
+    got = live.welch_band_db(xin, fs, cfg, sample_scale=sc)
+    ref = L.welch_band_db_ref(x.astype(np.float64) / 32768.0, fs, _ref_cfg(cfg))
+    np.testing.assert_allclose(got, ref, rtol=0, atol=DB_TOL)
+
+
+def test_state_machine_bit_exact_on_oracle_rows(live, golden_dir):
+    g = np.load(os.path.join(golden_dir, "live_4k.npz"))
+    cfg = live.ConfigDetection(n_fft=int(g["n_fft"]), signal_freq=int(g["f0"]),
+                               detection_db_over_noise_mean_min=1, detection_dur_min_sec=0.5)
+    rows = g["expected"]
+    m, thr, over = live.live_detect(rows, int(g["fs"]), cfg)
+    rm, rthr, rover = L.live_detect_ref(rows, int(g["fs"]), int(cfg.proc_block_sec * g["fs"]), _ref_cfg(cfg))
+    np.testing.assert_array_equal(over, rover)
+    np.testing.assert_array_equal(thr, rthr)                      # NaN positions included
+    assert len(m) == len(rm) == 2
+    for a, b in zip(m, rm):
+        assert (a.time_start, a.time_stop, a.duration, a.db_min, a.db_max, a.db_mean, a.db_std) == \
+               (b.time_start, b.time_stop, b.duration, b.db_min, b.db_max, b.db_mean, b.db_std)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+@pytest.mark.parametrize("kw", [dict(), dict(avg_win_sec=0.1), dict(after_tracking_wait_sec=0.0),
+                                dict(detection_db_over_noise_mean_min=4, detection_dur_min_sec=0.4)])
+def test_state_machine_random_rows(live, seed, kw):
+    rng = np.random.default_rng(seed)
+    nb = 600
+    sig = rng.normal(0, 1, nb)
+    for s in rng.integers(50, nb - 10, 12):
+        sig[s:s + rng.integers(1, 8)] += rng.uniform(5, 30)
+    rows = np.stack([sig, rng.normal(0, 0.5, nb), rng.normal(0, 0.5, nb)])
+    cfg = live.ConfigDetection(**kw)
+    m, thr, over = live.live_detect(rows, 4000, cfg)
+    rm, rthr, rover = L.live_detect_ref(rows, 4000, 800, _ref_cfg(cfg))
+    np.testing.assert_array_equal(thr, rthr)
+    assert [(a.time_start, a.time_stop, a.db_min, a.db_max, a.db_mean, a.db_std) for a in m] == \
+           [(b.time_start, b.time_stop, b.db_min, b.db_max, b.db_mean, b.db_std) for b in rm]
+
+
+def test_state_machine_edge_rows(live):
+    cfg = live.ConfigDetection(init_detection_wait_sec=0.0)
+    for rows in (np.zeros((3, 0)), np.ones((3, 1)), np.stack([np.full(40, 1.0), np.full(40, -np.inf),
+                                                                 np.full(40, -np.inf)])):
+        m, thr, over = live.live_detect(rows, 4000, cfg)
+        rm, rthr, rover = L.live_detect_ref(rows, 4000, 800, _ref_cfg(cfg))
+        np.testing.assert_array_equal(thr, rthr)
+        np.testing.assert_array_equal(over, rover)
+        assert len(m) == len(rm)
+
+
+def test_wav_file_process_end_to_end(live, tmp_path):
+    from meteorgpu import synth, wav
+    x, _ = synth.synth_real(seed=77, fs=4000, duration_s=90.0, f0=1020.0, sigma=300.0, rate_per_min=10,
+                            band_hz=100.0, snr_db=(15, 30), dur_s=(0.4, 2.0))
+    p = tmp_path / "live.wav"
+    wav.write(p, 4000, x)
+    cfg = live.ConfigDetection(proc_block_sec=0.2, n_fft=4096, detection_db_over_noise_mean_min=1,
+                               detection_dur_min_sec=0.5, signal_freq=1020)
+    got = live.wav_file_process(str(p), cfg, live.ConfigVisualization(enable_ui_plots=False),
+                                live.ConfigSpecExport(output_dir=""))
+    ref, _, _ = L.wav_file_process_ref(x.astype(np.float64) / 32768.0, 4000, _ref_cfg(cfg))
+    assert len(ref) > 0 and len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert (a.time_start, a.time_stop, a.duration) == (b.time_start, b.time_stop, b.duration)
+        for f in ("db_min", "db_max", "db_mean", "db_std"):
+            assert math.isclose(getattr(a, f), getattr(b, f), rel_tol=STAT_TOL, abs_tol=STAT_TOL)
+
+
+def test_wav_file_process_asserts(live, tmp_path):
+    from meteorgpu import wav
+    p = tmp_path / "a.wav"
+    wav.write(p, 6000, np.zeros(6000, np.int16))
+    with pytest.raises(AssertionError, match="Invalid Sample Rate: 6000"):
+        live.wav_file_process(str(p), live.ConfigDetection(), live.ConfigVisualization(enable_ui_plots=False),
+                              live.ConfigSpecExport())
+    with pytest.raises(NotImplementedError):
+        live.wav_file_process(str(p), live.ConfigDetection(), live.ConfigVisualization(),
+                              live.ConfigSpecExport(), required_sample_rate=None)
+
+
+def test_live_batch_matches_single(live):
+    from meteorgpu import _lib, synth
+    from meteorgpu.dsp import context
+    cfg = live.ConfigDetection(detection_db_over_noise_mean_min=1, detection_dur_min_sec=0.4)
+    xs = [synth.synth_real(seed=900 + i, fs=4000, duration_s=60.0, f0=1000.0, sigma=300.0, rate_per_min=12,
+                           band_hz=100.0, snr_db=(15, 30), dur_s=(0.4, 2.0))[0] for i in range(5)]
+    lb = live.LiveBatch(context(0), len(xs), len(xs[0]), 4000, cfg)
+    for i, x in enumerate(xs):
+        lb.upload_file(i, x)
+    lb.run()
+    bdb = lb.band_db()
+    rows, counts = lb.meteors()
+    for i, x in enumerate(xs):
+        single = live.welch_band_db(x, 4000, cfg, sample_scale=1 / 32768)
+        np.testing.assert_array_equal(bdb[i], single)
+        m, _, _ = live.live_detect(single, 4000, cfg)
+        assert counts[i] == len(m)
+        assert [(r["time_start"], r["time_stop"], r["db_mean"]) for r in rows[i]] == \
+               [(a.time_start, a.time_stop, a.db_mean) for a in m]
+    assert counts.sum() > 0
