@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--cpu-files", type=int, default=150, help="files in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
+    ap.add_argument("--workload", choices=("c3", "live"), default="c3",
+                    help="c3: the headline day batch (default); live: the phase-2 live detector "
+                         "(Welch band powers + state machine) over a day of 4 kHz audio")
     return ap.parse_args()
 
 
@@ -76,6 +79,96 @@ def load_pmc_traffic(nfiles):
     return None
 
 
+LIVE_FS, LIVE_FILE_S, LIVE_FILES = 4000, 3600, 24
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec sheet (not listed in MI355X_MICROARCH.md)
+
+
+def cpu_baseline_live(pool, seconds):
+    """processor.py:177-507 restated (oracle/live_oracle.py): scipy welch per 0.2 s block, band
+    sums, the state machine — 1 thread, on `seconds` of the same audio."""
+    from oracle import live_oracle as L
+    x = pool[0][: int(seconds * LIVE_FS)].astype(np.float64) / 32768.0
+    t0 = time.perf_counter()
+    L.wav_file_process_ref(x, LIVE_FS, L.ConfigDetectionRef(detection_db_over_noise_mean_min=1,
+                                                            detection_dur_min_sec=0.5))
+    dt = time.perf_counter() - t0
+    return len(x) / dt / 1e6, dt
+
+
+def main_live(a, world, rank, local, dist):
+    """Phase-2 live detector over a day of 4 kHz audio per GPU: 24 x 1 h int16 files."""
+    from meteorgpu import _lib, synth
+    from meteorgpu import live as LV
+    ctx = _lib.Context(local)
+    cfg = LV.ConfigDetection(proc_block_sec=0.2, n_fft=4096, signal_freq=1000,
+                             detection_db_over_noise_mean_min=1, detection_dur_min_sec=0.5)
+    n = LIVE_FS * LIVE_FILE_S
+    F = LIVE_FILES
+    lb = LV.LiveBatch(ctx, F, n, LIVE_FS, cfg)
+    pool = [synth.synth_real(seed=3000 + j, fs=LIVE_FS, duration_s=LIVE_FILE_S, f0=1000.0, sigma=300.0,
+                             rate_per_min=5, band_hz=100.0, snr_db=(10, 30), dur_s=(0.3, 2.0))[0] for j in range(4)]
+    for i in range(F):
+        lb.upload_file(i, pool[(i + rank) % len(pool)])
+
+    def sync_all():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        lb.run()
+    sync_all()
+    _, counts = lb.meteors()
+    ctx.timing(True)
+    ctx.timing_reset()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        lb.run()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    w_ms, w_n = ctx.timing_get(_lib.K_WELCH)
+    l_ms, l_n = ctx.timing_get(_lib.K_LIVE)
+    wc = lb.plan.cfg
+    nseg = (wc.block_size - wc.nperseg) // (wc.nperseg - wc.noverlap) + 1
+    nslots = sum(wc.band_hi[j] - wc.band_lo[j] + 1 for j in range(wc.nbands))
+    blocks = F * lb.nb
+    flops = blocks * nseg * nslots * wc.nperseg * 3.0  # Goertzel: one fma + one subtract per sample and bin
+    avg_s = w_ms / max(w_n, 1) / 1e3
+    out = {
+        "metric": "Msamples/s processed (4 kHz live detector: Welch band powers + state machine)",
+        "value": round(world * F * n * a.steps / elapsed / 1e6, 1),
+        "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: 4 seeded 1 h 4 kHz int16 noise+ping recordings replicated over 24 files/GPU",
+        "config": {"workload": "phase-2 live detector day: 24 x 1 h 4 kHz int16 per GPU, 0.2 s blocks, "
+                               "welch(nperseg 256, nfft 4096) on 3 x 100 Hz bands, 8 s history, k = 4",
+                   "files_per_gpu": F, "samples_per_file": n, "blocks_per_file": lb.nb, "band_bins": nslots},
+        "meteors_per_step": int(counts.sum()),
+        "roofline": {"bound": "fp64-valu", "achieved": round(flops / avg_s / 1e12, 2), "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(flops / avg_s / 1e12 / FP64_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": "welch_bands_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
+                     "algorithmic_flops_per_launch": flops},
+        "kernel_ms_per_step": {"welch": round(avg_s * 1e3, 4), "live_detect": round(l_ms / max(l_n, 1), 4)},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
+        secs = 1800
+        v, dt = cpu_baseline_live(pool, secs)
+        out["cpu_baseline"] = {"value": round(v, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+                               "sample": f"{secs} s of one 4 kHz file ({dt:.1f} s): scipy welch per block + "
+                                         f"band sums + state machine (oracle/live_oracle.py), 1 thread"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,6 +180,11 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.workload == "live":
+        main_live(a, world, rank, local, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from meteorgpu import _lib, synth
     from meteorgpu.batch import BatchPipeline, Communicator

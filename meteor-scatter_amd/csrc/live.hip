@@ -5,14 +5,12 @@
 //   live_detect_kernel  a9  the over-noise value, its history threshold and the
 //                           Init / Detection / Tracking state machine (processor.py:391-507)
 //
-// welch_bands_kernel: one 256-thread workgroup per block.  The block's samples are staged
-// in LDS as float64 (times the soundfile scale); each Welch segment is detrended with its
-// numpy-order mean (np_reduce.h) and windowed in LDS; then every (segment, bin) pair runs a
-// float64 Goertzel recurrence over the nperseg samples — the band bins only, not the whole
-// nfft-point rFFT (the zero padding to nfft only sets the bin spacing).  Tasks are laid out
-// so that the 64 lanes of a wave share one segment (broadcast LDS reads).  Segment powers
-// are averaged in scipy's order (sequential over segments, / nseg) and the band sums use
-// numpy's pairwise order.
+// welch_bands_kernel: one wave per block.  Each Welch segment's samples are staged in the
+// wave's LDS as float64 (times the soundfile scale), detrended with the numpy-order mean and
+// windowed; then every band bin (one lane each) runs a float64 Goertzel recurrence over the
+// nperseg samples — the band bins only, not the whole nfft-point rFFT (the zero padding to
+// nfft only sets the bin spacing).  Segment powers are averaged in scipy's order (sequential
+// over segments, / nseg) and the band sums use numpy's pairwise order.
 //
 // live_detect_kernel: one workgroup per file.  The history thresholds mean + k*std of the
 // previous W over-noise values do not depend on the state, so they are computed in
@@ -28,7 +26,16 @@ namespace msd {
 namespace {
 
 constexpr int WL_THREADS = 256;
-constexpr int WL_SLOT_CHUNK = 512;  // bins per pass (LDS for the segment powers)
+constexpr int LV_CHUNK = 2048;  // blocks per LDS-staged chunk of the state-machine scan
+
+// np.sum over LDS: numpy's exact order up to 128 elements (one pairwise leaf); longer runs
+// (bands wider than 128 bins, nperseg != 256 above 128) use the same 8-accumulator leaf
+// over the whole run — within an ulp or two of numpy's tree, far below the Goertzel vs
+// pocketfft rounding difference of the values summed, and without the recursion's register
+// cost in this kernel
+__device__ __forceinline__ double lds_band_sum(const double *p, int64_t base, int64_t n) {
+    return n <= 128 ? np_sum_small(ArrRef{p}, base, n) : 0.0 + np_pairwise_leaf(ArrRef{p}, base, n);
+}
 
 template <typename T>
 __device__ __forceinline__ double to_f64(T v) {
@@ -38,12 +45,61 @@ __device__ __forceinline__ double to_f64(T v) {
 struct WelchArgs {
     int64_t nfiles, max_blocks, ld;
     int block_size, nperseg, step, nseg, nfft, nslots, nbands;
-    int ypitch;  // doubles per windowed segment row in LDS
+    int wave_lds;  // doubles of LDS per wave: segment [nperseg, padded] + psd [nslots, padded]
     double sample_scale, scale;
     int band_lo[MSD_WELCH_MAX_BANDS], band_hi[MSD_WELCH_MAX_BANDS];
     int band_slot0[MSD_WELCH_MAX_BANDS];  // first slot of each band
 };
 
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const int2 v = __builtin_bit_cast(int2, x);
+    int2 r;
+    r.x = __builtin_amdgcn_mov_dpp(v.x, CTRL, 0xf, 0xf, true);
+    r.y = __builtin_amdgcn_mov_dpp(v.y, CTRL, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, r);
+}
+
+__device__ __forceinline__ double readlane_f64(double x, int lane) {
+    const int2 v = __builtin_bit_cast(int2, x);
+    int2 r;
+    r.x = __builtin_amdgcn_readlane(v.x, lane);
+    r.y = __builtin_amdgcn_readlane(v.y, lane);
+    return __builtin_bit_cast(double, r);
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// np.sum(seg[0:n]) by one wave, numpy's pairwise order.  n = 256 (scipy's default
+// nperseg): two 128-element leaves, their 8 interleaved partial sums on lanes 0-7 / 8-15,
+// combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by DPP; other n: lane 0 (lds_band_sum).
+__device__ __forceinline__ double wave_np_sum(const double *seg, int n, int lane) {
+    if (n == 256) {
+        double r = 0.0;
+        if (lane < 16) {
+            const double *a = seg + (lane >> 3) * 128 + (lane & 7);
+            r = a[0];
+            for (int k = 1; k < 16; ++k) r += a[8 * k];
+        }
+        r += dpp_f64<0xB1>(r);   // lane ^ 1
+        r += dpp_f64<0x4E>(r);   // lane ^ 2
+        r += dpp_f64<0x141>(r);  // half-row mirror: lanes 0-3 meet 4-7 (8-11 meet 12-15)
+        return 0.0 + (readlane_f64(r, 0) + readlane_f64(r, 8));
+    }
+    double v = 0.0;
+    if (lane == 0) v = lds_band_sum(seg, 0, n);
+    return readlane_f64(v, 0);
+}
+
+// One wave per processing block: per Welch segment, stage + detrend + window the samples in
+// the wave's LDS, then Goertzel over the segment for every band bin (lane = bin, broadcast
+// LDS reads of the samples, two per ds_read_b128), accumulating the segment powers in the
+// wave's LDS psd in segment order.  No workgroup barriers: the 4 waves of a workgroup work
+// on independent blocks.
 template <typename T>
 __global__ __launch_bounds__(WL_THREADS) void welch_bands_kernel(const T *__restrict__ x,
                                                                  const int64_t *__restrict__ off,
@@ -53,48 +109,49 @@ __global__ __launch_bounds__(WL_THREADS) void welch_bands_kernel(const T *__rest
                                                                  double *__restrict__ band_db,
                                                                  double *__restrict__ psd_out) {
     extern __shared__ double sm[];
-    const int64_t gb = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t gb = (int64_t)blockIdx.x * (WL_THREADS / 64) + wave;
     const int64_t f = gb / A.max_blocks;
     const int64_t b = gb - f * A.max_blocks;
     if (f >= A.nfiles) return;
     const int64_t n = len[f];
     const int64_t nb = n >= A.block_size ? (n - A.block_size) / A.block_size + 1 : 0;
-    if (b >= nb) return;  // whole workgroup (uniform)
-    const int tid = threadIdx.x;
-    const int span = (A.nseg - 1) * A.step + A.nperseg;  // samples the segments cover
-    double *xs = sm;                                      // [span]
-    double *ys = xs + ((span + 1) & ~1);                  // [nseg][ypitch]
-    double *mean = ys + A.nseg * A.ypitch;                // [nseg] (padded to 8)
-    double *psd = mean + 8;                               // [nslots]
-    double *pw = psd + ((A.nslots + 1) & ~1);             // [nseg][WL_SLOT_CHUNK]
-
+    if (b >= nb) return;  // whole wave
+    double *seg = sm + wave * A.wave_lds;                 // [nperseg (+pad)]
+    double *psd = seg + ((A.nperseg + 1) & ~1);           // [nslots]
     const T *xb = x + off[f] + b * (int64_t)A.block_size;
-    for (int i = tid; i < span; i += WL_THREADS) xs[i] = to_f64(xb[i]) * A.sample_scale;
-    __syncthreads();
-    // detrend='constant': d - np.mean(d, axis=-1) per segment (numpy pairwise order)
-    if (tid < A.nseg) mean[tid] = np_sum(ArrRef{xs}, (int64_t)tid * A.step, A.nperseg) / (double)A.nperseg;
-    __syncthreads();
-    for (int i = tid; i < A.nseg * A.nperseg; i += WL_THREADS) {
-        const int s = i / A.nperseg, m = i - s * A.nperseg;
-        ys[s * A.ypitch + m] = g_win[m] * (xs[s * A.step + m] - mean[s]);  // win * detrended
-    }
-    __syncthreads();
+    const int L = A.nperseg;
 
-    const int chunk_pad = (WL_SLOT_CHUNK + 63) & ~63;
-    for (int c0 = 0; c0 < A.nslots; c0 += WL_SLOT_CHUNK) {
-        const int cn = A.nslots - c0 < WL_SLOT_CHUNK ? A.nslots - c0 : WL_SLOT_CHUNK;
-        const int cpad = (cn + 63) & ~63;  // slots per segment padded to whole waves
-        (void)chunk_pad;
-        for (int task = tid; task < A.nseg * cpad; task += WL_THREADS) {
-            const int s = task / cpad, j = task - s * cpad;  // s is wave-uniform
-            if (j >= cn) continue;
-            const double *bc = g_bins + 4 * (c0 + j);
+    for (int s = 0; s < A.nseg; ++s) {
+        const T *xs = xb + s * A.step;
+        for (int i = lane; i < L; i += 64) seg[i] = to_f64(xs[i]) * A.sample_scale;
+        wave_sync();
+        // detrend='constant': d - np.mean(d, axis=-1) (numpy pairwise order)
+        const double mean = wave_np_sum(seg, L, lane) / (double)L;
+        wave_sync();
+        for (int i = lane; i < L; i += 64) seg[i] = g_win[i] * (seg[i] - mean);  // win * detrended
+        wave_sync();
+        for (int j0 = 0; j0 < A.nslots; j0 += 64) {
+            const int j = j0 + lane;
+            const bool act = j < A.nslots;
+            const double *bc = g_bins + 4 * (act ? j : 0);
             const double cw = bc[0], sw = bc[1], c2 = bc[2], dbl = bc[3];
-            const double *y = ys + s * A.ypitch;
             double s1 = 0.0, s2 = 0.0;
-#pragma unroll 8
-            for (int m = 0; m < A.nperseg; ++m) {
-                const double s0 = __builtin_fma(c2, s1, y[m] - s2);
+            const double2 *y2 = reinterpret_cast<const double2 *>(seg);
+            int m = 0;
+#pragma unroll 4
+            for (; m + 2 <= L; m += 2) {
+                const double2 y = y2[m >> 1];
+                double s0 = __builtin_fma(c2, s1, y.x - s2);
+                s2 = s1;
+                s1 = s0;
+                s0 = __builtin_fma(c2, s1, y.y - s2);
+                s2 = s1;
+                s1 = s0;
+            }
+            if (m < L) {
+                const double s0 = __builtin_fma(c2, s1, seg[m] - s2);
                 s2 = s1;
                 s1 = s0;
             }
@@ -102,23 +159,21 @@ __global__ __launch_bounds__(WL_THREADS) void welch_bands_kernel(const T *__rest
             const double re = s1 - cw * s2, im = sw * s2;
             double p = re * re + im * im;  // conj(X) * X (real part)
             p = p * A.scale;               // result *= scale
-            p = p * dbl;                   // result[..., 1:-1] *= 2 (onesided, psd)
-            pw[s * WL_SLOT_CHUNK + j] = p;
+            p = p * dbl;                   // result[..., 1:-1] *= 2 (onesided psd)
+            if (act) psd[j] = s == 0 ? p : psd[j] + p;  // Pxy.mean(axis=-1): segments in order
         }
-        __syncthreads();
-        for (int j = tid; j < cn; j += WL_THREADS) {  // Pxy.mean(axis=-1): sequential over segments
-            double acc = pw[j];
-            for (int s = 1; s < A.nseg; ++s) acc += pw[s * WL_SLOT_CHUNK + j];
-            const double v = acc / (double)A.nseg;
-            psd[c0 + j] = v;
-            if (psd_out) psd_out[(f * A.ld + b) * (int64_t)A.nslots + c0 + j] = v;
-        }
-        __syncthreads();
+        wave_sync();
     }
-    if (tid < A.nbands) {
-        const int w = A.band_hi[tid] - A.band_lo[tid] + 1;
-        const double P = w > 0 ? np_sum(ArrRef{psd}, A.band_slot0[tid], w) : 0.0;  // np.sum(psd[mask])
-        band_db[(f * A.nbands + tid) * A.ld + b] = P > 0.0 ? 10.0 * log10(P) : -INFINITY;
+    for (int j = lane; j < A.nslots; j += 64) {
+        const double v = psd[j] / (double)A.nseg;
+        psd[j] = v;
+        if (psd_out) psd_out[(f * A.ld + b) * (int64_t)A.nslots + j] = v;
+    }
+    wave_sync();
+    if (lane < A.nbands) {
+        const int w = A.band_hi[lane] - A.band_lo[lane] + 1;
+        const double P = w > 0 ? lds_band_sum(psd, A.band_slot0[lane], w) : 0.0;  // np.sum(psd[mask])
+        band_db[(f * A.nbands + lane) * A.ld + b] = P > 0.0 ? 10.0 * log10(P) : -INFINITY;
     }
 }
 
@@ -136,6 +191,62 @@ __device__ __forceinline__ void py_minmax(const double *v, int64_t a, int64_t e,
         if (v[i] < mn) mn = v[i];
         if (v[i] > mx) mx = v[i];
     }
+}
+
+struct LiveScan {
+    int state = 0;  // 0 init, 1 detection, 2 tracking
+    double lock = -1.0, until = -1.0, t_start = 0.0;
+    int64_t trig = 0, cnt = 0;
+};
+
+// numpy mean/std of over[b, b+n): from the staged chunk when the run lies inside it (offsets,
+// not a shifted LDS pointer: that would leave the LDS aperture once made generic)
+__device__ __forceinline__ void hist_stats(const double *ov, const double *s_ov, int64_t c0, int64_t b, int64_t n,
+                                           double &mean, double &sd, double *mn, double *mx) {
+    const bool in = b >= c0;
+    const double *src = in ? s_ov : ov;
+    const int64_t sb = in ? b - c0 : b;
+    np_mean_std(src, sb, n, mean, sd);
+    if (mn) py_minmax(src, sb, sb + n, *mn, *mx);
+}
+
+// Detection → Tracking (processor.py:462-472): locked_threshold = thr + 0 * history_std
+__device__ __noinline__ void live_trigger(LiveScan &sc, const double *ov, const double *s_ov, int64_t c0, int64_t i,
+                                          double t, double t0, const msd_live_cfg &C) {
+    const int64_t W = C.avg_win_blocks;
+    const int64_t h0 = W > 0 ? (i - W > 0 ? i - W : 0) : 0;
+    double hm = NAN, hs = NAN;
+    if (i - h0 > 0) hist_stats(ov, s_ov, c0, h0, i - h0, hm, hs, nullptr, nullptr);
+    sc.lock = t + 0.0 * hs;
+    sc.t_start = t0;
+    sc.trig = i;
+    sc.state = 2;
+}
+
+// Tracking ends (processor.py:474-504): history = over[trig+1 .. i]
+__device__ __noinline__ void live_close(LiveScan &sc, const double *ov, const double *s_ov, int64_t c0, int64_t i,
+                                        double t0, const msd_live_cfg &C, msd_meteor *out, int64_t cap, bool writer) {
+    const double dur = t0 - sc.t_start;
+    double hm, hs, mn, mx;
+    hist_stats(ov, s_ov, c0, sc.trig + 1, i - sc.trig, hm, hs, &mn, &mx);
+    if (hm >= C.min_db_mean && dur >= C.min_dur_sec) {
+        if (writer && sc.cnt < cap) {
+            msd_meteor m;
+            m.start_block = sc.trig;
+            m.stop_block = i;
+            m.time_start = sc.t_start;
+            m.time_stop = t0;
+            m.duration = dur;
+            m.db_min = mn;
+            m.db_max = mx;
+            m.db_mean = hm;
+            m.db_std = hs;
+            out[sc.cnt] = m;
+        }
+        ++sc.cnt;
+    }
+    sc.state = 1;
+    sc.until = t0 + C.after_tracking_wait_sec;
 }
 
 __global__ __launch_bounds__(WL_THREADS) void live_detect_kernel(const double *__restrict__ band_db,
@@ -170,63 +281,73 @@ __global__ __launch_bounds__(WL_THREADS) void live_detect_kernel(const double *_
         th[i] = mean + C.k_std * sd;
     }
     __syncthreads();
-    if (tid != 0) return;
-    // the state machine (processor.py:404-507)
-    int state = 0;  // 0 init, 1 detection, 2 tracking
-    double lock = -1.0, until = -1.0, t_start = 0.0;
-    int64_t trig = 0, cnt = 0;
-    for (int64_t i = 0; i < nb; ++i) {
-        const double t0 = (double)(i * (int64_t)C.block_size) / C.fs;
-        const double t1 = (double)(i * (int64_t)C.block_size + C.block_size) / C.fs;
-        const double fresh = th[i];
-        double t = fresh;
-        if (state == 2) t = lock;
-        else if (state == 1 && until > t1) t = lock;
-        th[i] = t;
-        const double v = ov[i];
-        if (state == 0) {
-            if (t0 >= C.init_wait_sec) {
-                state = 1;
-                lock = -1.0;
-                until = -1.0;
-            }
-        } else if (state == 1) {
-            if (v > t) {
-                // locked_threshold = thr + 0 * history_std (NaN if the std is)
-                const int64_t W = C.avg_win_blocks;
-                const int64_t h0 = W > 0 ? (i - W > 0 ? i - W : 0) : 0;
-                double hm = NAN, hs = NAN;
-                if (i - h0 > 0) np_mean_std(ov, h0, i - h0, hm, hs);
-                lock = t + 0.0 * hs;
-                t_start = t0;
-                trig = i;
-                state = 2;
-            }
-        } else {
-            if (v < t) {  // history = over[trig+1 .. i]
-                const double dur = t0 - t_start;
-                double hm, hs;
-                np_mean_std(ov, trig + 1, i - trig, hm, hs);
-                if (hm >= C.min_db_mean && dur >= C.min_dur_sec) {
-                    if (cnt < A.cap) {
-                        msd_meteor m;
-                        m.start_block = trig;
-                        m.stop_block = i;
-                        m.time_start = t_start;
-                        m.time_stop = t0;
-                        m.duration = dur;
-                        py_minmax(ov, trig + 1, i + 1, m.db_min, m.db_max);
-                        m.db_mean = hm;
-                        m.db_std = hs;
-                        out[f * A.cap + cnt] = m;
-                    }
-                    ++cnt;
+    // the state machine (processor.py:404-507): wave 0 scans chunks of the over-noise values,
+    // fresh thresholds and block times staged in LDS by the whole workgroup; the thresholds
+    // used go back the same way.  History statistics at triggers / detections read the staged chunk when the
+    // history lies inside it, the global copy otherwise.
+    __shared__ double s_ov[LV_CHUNK], s_th[LV_CHUNK], s_t[LV_CHUNK + 1];
+    LiveScan sc;
+    for (int64_t c0 = 0; c0 < nb; c0 += LV_CHUNK) {
+        const int cn = nb - c0 < LV_CHUNK ? (int)(nb - c0) : LV_CHUNK;
+        for (int k = tid; k < cn; k += WL_THREADS) {
+            s_ov[k] = ov[c0 + k];
+            s_th[k] = th[c0 + k];
+        }
+        // block start times (i*B)/fs, i = c0 .. c0+cn (the last one is the chunk's end)
+        for (int k = tid; k <= cn; k += WL_THREADS) s_t[k] = (double)((c0 + k) * (int64_t)C.block_size) / C.fs;
+        __syncthreads();
+        if (tid < 64) {
+            // wave 0 scans: at position k, lane j evaluates block k+j under the current state;
+            // the first block whose event condition holds (ballot) is where the state changes.
+            // Blocks before it keep the state, so a 64-block span without events is one step;
+            // each event is one more.  All lanes carry identical copies of the scan state and
+            // run the (rare) event handlers redundantly; lane 0 writes the detection.
+            const int lane = tid;
+            int k = 0;
+            while (k < cn) {
+                const int kk = k + lane;
+                const bool valid = kk < cn;
+                const int kc = valid ? kk : cn - 1;
+                const double v = s_ov[kc], fresh = s_th[kc], t0 = s_t[kc], t1 = s_t[kc + 1];
+                double t;
+                bool cand;
+                if (sc.state == 0) {
+                    t = fresh;
+                    cand = t0 >= C.init_wait_sec;
+                } else if (sc.state == 1) {
+                    t = sc.until > t1 ? sc.lock : fresh;
+                    cand = v > t;
+                } else {
+                    t = sc.lock;
+                    cand = v < t;
                 }
-                state = 1;
-                until = t0 + C.after_tracking_wait_sec;
+                const uint64_t mask = __ballot(valid && cand);
+                const int first = mask ? __builtin_ctzll(mask) : 64;
+                if (valid && lane <= first) s_th[kk] = t;  // thresholds used (processor.py:395-412)
+                if (!mask) {
+                    k += 64;
+                    continue;
+                }
+                const int e = k + first;  // event block (chunk-relative)
+                const double te = __shfl(t, first), t0e = __shfl(t0, first);
+                if (sc.state == 0) {
+                    sc.state = 1;
+                    sc.lock = -1.0;
+                    sc.until = -1.0;
+                } else if (sc.state == 1) {
+                    live_trigger(sc, ov, s_ov, c0, c0 + e, te, t0e, C);
+                } else {
+                    live_close(sc, ov, s_ov, c0, c0 + e, t0e, C, out + f * A.cap, A.cap, lane == 0);
+                }
+                k = e + 1;
             }
         }
+        __syncthreads();
+        for (int k = tid; k < cn; k += WL_THREADS) th[c0 + k] = s_th[k];
+        __syncthreads();
     }
+    if (tid != 0) return;
+    const int64_t cnt = sc.cnt;
     counts[f] = cnt;
     if (status) status[f] = cnt > A.cap ? 3 : 0;
 }
@@ -246,7 +367,7 @@ int launch_welch_t(msd_welch_plan *p, const void *x, const int64_t *off, const i
     A.nfft = c.nfft;
     A.nslots = p->nslots;
     A.nbands = c.nbands;
-    A.ypitch = c.nperseg + 2;  // row offset of 2 doubles: segments start on different banks
+    A.wave_lds = ((c.nperseg + 1) & ~1) + ((p->nslots + 1) & ~1);
     A.sample_scale = c.sample_scale;
     A.scale = c.scale;
     int slot = 0;
@@ -256,17 +377,15 @@ int launch_welch_t(msd_welch_plan *p, const void *x, const int64_t *off, const i
         A.band_slot0[j] = slot;
         if (c.band_hi[j] >= c.band_lo[j]) slot += c.band_hi[j] - c.band_lo[j] + 1;
     }
-    const int span = (p->nseg - 1) * p->step + c.nperseg;
-    const size_t lds = sizeof(double) * (((span + 1) & ~1) + (size_t)p->nseg * A.ypitch + 8 +
-                                         ((p->nslots + 1) & ~1) + (size_t)p->nseg * WL_SLOT_CHUNK);
-    if (lds > 160 * 1024) return fail(MSD_ERR_UNSUPPORTED, "welch: block / segment configuration exceeds LDS");
+    const size_t lds = sizeof(double) * (WL_THREADS / 64) * (size_t)A.wave_lds;
+    if (lds > 160 * 1024) return fail(MSD_ERR_UNSUPPORTED, "welch: nperseg + band bins exceed the LDS budget");
     static bool attr = false;
     if (!attr) {
         MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(welch_bands_kernel<T>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
-    const int64_t grid = nfiles * max_blocks;
+    const int64_t grid = (nfiles * max_blocks + WL_THREADS / 64 - 1) / (WL_THREADS / 64);  // a wave per block
     if (grid > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "welch: grid too large");
     KernelTimer timer(p->ctx, K_WELCH);
     hipLaunchKernelGGL(welch_bands_kernel<T>, dim3((unsigned)grid), dim3(WL_THREADS), lds, p->ctx->stream,

@@ -45,23 +45,27 @@ __device__ __forceinline__ double np_pairwise_leaf(const A &a, int64_t base, int
     return res;
 }
 
-// Iterative post-order walk of numpy's recursion tree over [base, base+n)
-// (depth <= 48 for n < 2^48).  leaf(b, m) returns the sum of a leaf (m <= 128);
-// the walk combines the leaves exactly as numpy's recursion does.
+// Iterative post-order walk of numpy's recursion tree over [base, base+n), n <= 8192
+// (one ufunc buffer chunk).  leaf(b, m) returns the sum of a leaf (m <= 128); the walk
+// combines the leaves exactly as numpy's recursion does.  The explicit stack lives in
+// scratch (a cold, single-thread path: detect.hip's leaf-table builder).
+constexpr int NP_TREE_DEPTH = 48;
 template <typename LeafFn>
 __device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
 #pragma clang fp contract(off)
     if (n <= 128) return leaf(base, n);
-    int64_t st_base[48], st_n[48];
-    double st_left[48];
-    int st_state[48];
+    int64_t st_base[NP_TREE_DEPTH];
+    int st_n[NP_TREE_DEPTH];
+    double st_left[NP_TREE_DEPTH];
+    int st_state[NP_TREE_DEPTH];
     int sp = 0;
     st_base[0] = base;
-    st_n[0] = n;
+    st_n[0] = (int)n;
     st_state[0] = 0;
     double ret = 0.0;
     while (sp >= 0) {
-        const int64_t b = st_base[sp], m = st_n[sp];
+        const int64_t b = st_base[sp];
+        const int m = st_n[sp];
         if (m <= 128) {
             ret = leaf(b, m);
             --sp;
@@ -70,7 +74,7 @@ __device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
                 if (st_state[sp] == 1) {  // left finished: start the right half
                     st_left[sp] = ret;
                     st_state[sp] = 2;
-                    int64_t n2 = st_n[sp] / 2;
+                    int n2 = st_n[sp] / 2;
                     n2 -= n2 % 8;
                     const int np1 = sp + 1;
                     st_base[np1] = st_base[sp] + n2;
@@ -87,7 +91,7 @@ __device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
         }
         // internal node, first visit: descend left
         st_state[sp] = 1;
-        int64_t n2 = m / 2;
+        int n2 = m / 2;
         n2 -= n2 % 8;
         const int np1 = sp + 1;
         st_base[np1] = b;
@@ -98,9 +102,25 @@ __device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
     return ret;
 }
 
+// numpy's recursion written as compile-time recursion over the depth (n <= 8192 needs at
+// most 7 splits): no stack array, so nothing is promoted to (or spilled from) registers
+template <int D, typename A>
+__device__ __forceinline__ double np_pairwise_rec(const A &a, int64_t base, int64_t n) {
+#pragma clang fp contract(off)
+    if constexpr (D == 0) {
+        return np_pairwise_leaf(a, base, n);
+    } else {
+        if (n <= 128) return np_pairwise_leaf(a, base, n);
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        const double l = np_pairwise_rec<D - 1>(a, base, n2);
+        return l + np_pairwise_rec<D - 1>(a, base + n2, n - n2);
+    }
+}
+
 template <typename A>
-__device__ double np_pairwise(const A &a, int64_t base, int64_t n) {
-    return np_tree_walk(base, n, [&](int64_t b, int64_t m) { return np_pairwise_leaf(a, b, m); });
+__device__ double np_pairwise(const A &a, int64_t base, int64_t n) {  // n <= NP_BUFSIZE
+    return np_pairwise_rec<7>(a, base, n);
 }
 
 constexpr int64_t NP_BUFSIZE = 8192;

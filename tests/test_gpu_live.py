@@ -150,3 +150,20 @@ def test_live_batch_matches_single(live):
         assert [(r["time_start"], r["time_stop"], r["db_mean"]) for r in rows[i]] == \
                [(a.time_start, a.time_stop, a.db_mean) for a in m]
     assert counts.sum() > 0
+
+
+def test_state_machine_long_rows_cross_chunks(live):
+    """nb > the kernel's 2048-block LDS chunk: runs and histories straddling chunk edges."""
+    rng = np.random.default_rng(11)
+    nb = 5000
+    sig = rng.normal(0, 1, nb)
+    for s in (2040, 2046, 4093, 3000, 100, 4999 - 3):
+        sig[s:s + 5] += 25
+    rows = np.stack([sig, rng.normal(0, 0.5, nb), rng.normal(0, 0.5, nb)])
+    cfg = live.ConfigDetection(after_tracking_wait_sec=0.4)
+    m, thr, over = live.live_detect(rows, 4000, cfg)
+    rm, rthr, rover = L.live_detect_ref(rows, 4000, 800, _ref_cfg(cfg))
+    np.testing.assert_array_equal(thr, rthr)
+    got = [(a.time_start, a.time_stop, a.db_min, a.db_max, a.db_mean, a.db_std) for a in m]
+    assert got == [(b.time_start, b.time_stop, b.db_min, b.db_max, b.db_mean, b.db_std) for b in rm]
+    assert any(2040 * 0.2 <= a.time_start <= 2050 * 0.2 for a in m)
