@@ -88,6 +88,9 @@ int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches
 int msd_stft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float *window, double scale,
                          msd_stft_plan **out);
 void msd_stft_plan_destroy(msd_stft_plan *plan);
+/* detrend: 1 = 'constant' (scipy's default, the plan's initial setting), 0 = none
+ * (matplotlib.mlab.specgram's detrend_none, prime_detection.py:70) */
+int msd_stft_plan_set_detrend(msd_stft_plan *plan, int detrend);
 /* frames of an n-sample signal (0 if n < nperseg) */
 int64_t msd_stft_frames(const msd_stft_plan *plan, int64_t n);
 /* batch, device-resident: file f occupies x[off[f] .. off[f]+len[f]) (elements of dtype);
@@ -162,6 +165,13 @@ int msd_detect_dev(msd_ctx *ctx, const double *delta, const int64_t *nblocks, in
  * global mode: *thresholds receives the single threshold in thresholds[0]. */
 int msd_detect(msd_ctx *ctx, const double *delta, int64_t nb, const msd_det_cfg *cfg, msd_det *dets, int64_t cap,
                int64_t *count, double *thresholds, double *margin);
+
+/* ------------------------------------------- a10: legacy spectrogram noise floor
+ * prime_detection.py:65-91: band_power = np.sum(Pxx[noise_band]) sums the spectrogram over
+ * the band's bins AND all frames.  spec: device float32 [nfiles][K][ld] as msd_stft_psd_dev
+ * writes it; out[f] (device) = sum over k in [lo, hi], t < frames of spec, float64. */
+int msd_spec_band_sum_dev(msd_ctx *ctx, const float *spec, int64_t nfiles, int32_t K, int64_t frames, int64_t ld,
+                          int32_t lo, int32_t hi, double *out);
 
 /* ------------------------------------------------ a8: Welch band powers (phase 2)
  * Replaces, per processing block of dsp/src/live/backend/processor.py:177-206 and :349-369:

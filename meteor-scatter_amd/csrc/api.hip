@@ -324,6 +324,12 @@ int msd_stft_psd_dev(msd_stft_plan *p, const void *x, int dtype, const int64_t *
     return launch_stft(p, x, dtype, off, len, nfiles, max_frames, out, ld);
 }
 
+int msd_stft_plan_set_detrend(msd_stft_plan *p, int detrend) {
+    if (!p || (detrend != 0 && detrend != 1)) return fail(MSD_ERR_INVALID, "msd_stft_plan_set_detrend: bad args");
+    p->detrend = detrend;
+    return MSD_OK;
+}
+
 int msd_stft_psd(msd_stft_plan *p, const void *x, int dtype, int64_t n, float *out, int64_t *frames) {
     if (!p || !x || !out) return fail(MSD_ERR_INVALID, "msd_stft_psd: null");
     const size_t es = dtype_size(dtype);

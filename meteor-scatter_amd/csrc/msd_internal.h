@@ -48,6 +48,7 @@ struct msd_ctx {
 struct msd_stft_plan {
     msd_ctx *ctx = nullptr;
     int nperseg = 0, hop = 0, M = 0;  // M = nperseg/2 complex points
+    int detrend = 1;                   // 1 constant (scipy), 0 none (matplotlib mlab)
     double scale = 0;
     float *d_window = nullptr;   // [nperseg]
     float2 *d_tw = nullptr;      // [M]    exp(-2*pi*i*m/M)

@@ -178,7 +178,7 @@ struct StftGeom {
 template <int M, int NW, int TT, typename T>
 __global__ __launch_bounds__(NW * 64) void stft_psd_kernel(const T *__restrict__ x, const int64_t *__restrict__ off,
                                                            const int64_t *__restrict__ len, int64_t tiles_per_file,
-                                                           int hop, float scale, const float *__restrict__ g_win,
+                                                           int hop, float scale, int detrend, const float *__restrict__ g_win,
                                                            const float2 *__restrict__ g_tw,
                                                            const float2 *__restrict__ g_post, float *__restrict__ out,
                                                            int64_t ld) {
@@ -221,7 +221,8 @@ __global__ __launch_bounds__(NW * 64) void stft_psd_kernel(const T *__restrict__
 #pragma unroll
             for (int q = 0; q < SPL; ++q) ls += s[q];
             // integer samples: per-lane sums are exact in fp32, the wave sum in fp64
-            const float mean = static_cast<float>(wave_sum(static_cast<double>(ls)) / static_cast<double>(N));
+            float mean = static_cast<float>(wave_sum(static_cast<double>(ls)) / static_cast<double>(N));
+            if (!detrend) mean = 0.f;  // matplotlib's detrend_none
             const float *w = win + lane * SPL;
 #pragma unroll
             for (int q = 0; q < SPL / 2; ++q) {
@@ -276,7 +277,7 @@ int launch_t(msd_stft_plan *p, const void *x, const int64_t *off, const int64_t 
     if (blocks > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "stft: grid too large");
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NW * 64), G::LDS_BYTES, p->ctx->stream,
                        static_cast<const T *>(x), off, len, tiles, p->hop, static_cast<float>(p->scale),
-                       p->d_window, p->d_tw, p->d_post, out, ld);
+                       p->detrend, p->d_window, p->d_tw, p->d_post, out, ld);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }

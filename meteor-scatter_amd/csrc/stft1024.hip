@@ -197,7 +197,7 @@ __device__ __forceinline__ void load_pair(const T *__restrict__ x, const FileCur
 template <typename T, int MODE>  // MODE: 0 [K][T] out; experiments: 1 frame-major, 2 no store, 3 L2-resident store
 __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len,
-    int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float wscale,
+    int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float wscale, int detrend,
     const float *__restrict__ g_win, const float2 *__restrict__ g_tw, const float2 *__restrict__ g_post,
     float *__restrict__ out, int64_t ld) {
     using IO = PairIO<T>;
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                     s = row_sum_i(s);
                     const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
                                     __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
-                    mean[q] = (float)((double)tot * (1.0 / 1024.0));
+                    mean[q] = detrend ? (float)((double)tot * (1.0 / 1024.0)) : 0.f;
                 } else {
                     float s = 0.f;
 #pragma unroll
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                         return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), lane));
                     };
                     const float tot = (rl(s, 0) + rl(s, 16)) + (rl(s, 32) + rl(s, 48));
-                    mean[q] = tot * (1.0f / 1024.0f);
+                    mean[q] = detrend ? tot * (1.0f / 1024.0f) : 0.f;
                 }
             }
 #pragma unroll
@@ -449,7 +449,7 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
     const int64_t per = (ntiles + wgs - 1) / wgs;
     wgs = (ntiles + per - 1) / per;
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(F_NW * 64), F_LDS, p->ctx->stream, static_cast<const T *>(x),
-                       off, len, tiles_per_file, ntiles, per, p->hop, static_cast<float>(std::sqrt(p->scale * 0.5)),
+                       off, len, tiles_per_file, ntiles, per, p->hop, static_cast<float>(std::sqrt(p->scale * 0.5)), p->detrend,
                        p->d_window, p->d_tw, p->d_post, out, ld);
     MSD_HIP(hipGetLastError());
     return MSD_OK;

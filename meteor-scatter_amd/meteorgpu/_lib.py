@@ -132,6 +132,7 @@ _SIGS = [
     ("msd_timing_get", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     ("msd_stft_plan_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_double, C.POINTER(_P)]),
     ("msd_stft_plan_destroy", None, [_P]),
+    ("msd_stft_plan_set_detrend", C.c_int, [_P, C.c_int]),
     ("msd_stft_frames", C.c_int64, [_P, C.c_int64]),
     ("msd_stft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64]),
     ("msd_stft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
@@ -146,6 +147,7 @@ _SIGS = [
       C.POINTER(MsdHistCfg)]),
     ("msd_detect", C.c_int,
      [_P, _P, C.c_int64, C.POINTER(MsdDetCfg), _P, C.c_int64, C.POINTER(C.c_int64), _P, _P]),
+    ("msd_spec_band_sum_dev", C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
     ("msd_welch_plan_create", C.c_int, [_P, C.POINTER(MsdWelchCfg), _P, C.POINTER(_P)]),
     ("msd_welch_plan_destroy", None, [_P]),
     ("msd_welch_bands_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64, _P]),
@@ -317,6 +319,10 @@ class StftPlan:
 
     def frames(self, n: int) -> int:
         return int(self.ctx.lib.msd_stft_frames(self.h, int(n)))
+
+    def set_detrend(self, detrend: bool):
+        """True: scipy's 'constant' detrend (the default); False: none (matplotlib mlab)."""
+        check(self.ctx.lib.msd_stft_plan_set_detrend(self.h, 1 if detrend else 0))
 
     def run(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x)

@@ -1,0 +1,120 @@
+"""Legacy pipeline pieces: the spectrogram and noise floor of
+meteor_detect_class/prime_detection.py:65-91, on the GPU.
+
+``specgram`` mirrors ``matplotlib.mlab.specgram`` (what ``plt.specgram`` computes) for a
+real 1-D signal: symmetric Hann (``window_hanning``), no detrend, one-sided PSD with the
+DC / Nyquist rows undoubled, ``/Fs/sum(w**2)`` — on libmsdsp's STFT kernels (float32
+arithmetic; the reference computes in float64, agreement ~1e-6 relative, tested).
+``noise_floor`` adds the band power over the noise band's rows and all frames
+(``np.sum(Pxx[noise_band])``, a device reduction) and the reference's colour floor
+``vmin = 10*log10(band_power/bandwidth) / (40/23) + C_MS_SPEC_CUT_FACTOR``.
+
+Out of scope: the JPEG rendering and the ORB / DBSCAN burst clustering that follow in the
+reference (image processing, not this data path).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .dsp import context, hanning_sym
+
+C_MS_SPEC_CUT_FACTOR = 12  # prime_detection.py:22
+
+
+def _freqs_times(n: int, NFFT: int, Fs: float, noverlap: int):
+    """mlab._spectral_helper's frequency and time axes (onesided, even or odd pad_to = NFFT)."""
+    num = NFFT // 2 + 1 if NFFT % 2 == 0 else (NFFT + 1) // 2
+    freqs = np.fft.fftfreq(NFFT, 1 / Fs)[:num]
+    if not NFFT % 2:
+        freqs[-1] *= -1  # "get the last value correctly, it is negative otherwise"
+    t = np.arange(NFFT / 2, n - NFFT / 2 + 1, NFFT - noverlap) / Fs
+    return freqs, t
+
+
+class SpecgramPlan:
+    """mlab.specgram(x, NFFT, Fs, noverlap) for signals of one length, resident on the device."""
+
+    def __init__(self, n: int, NFFT: int = 256, Fs: float = 2, noverlap: int = 128, dtype=np.int16,
+                 device: int = 0):
+        if NFFT not in (256, 512, 1024, 2048):
+            raise NotImplementedError("NFFT must be 256, 512, 1024 or 2048 (the STFT kernels' sizes)")
+        if not 0 <= noverlap < NFFT:
+            raise ValueError("noverlap must be less than NFFT")
+        if n < NFFT:
+            raise NotImplementedError("signals shorter than NFFT (mlab zero-pads them) are not supported")
+        self.ctx = context(device)
+        self.n, self.NFFT, self.Fs, self.noverlap = int(n), int(NFFT), float(Fs), int(noverlap)
+        self.dtype = np.dtype(dtype)
+        w = hanning_sym(NFFT)                   # window_hanning(np.ones(NFFT)) = np.hanning(NFFT)
+        scale = 1.0 / (Fs * (w ** 2).sum())     # result /= Fs; result /= (window**2).sum()
+        self.plan = _lib.StftPlan(self.ctx, NFFT, NFFT - noverlap, w.astype(np.float32), scale)
+        self.plan.set_detrend(False)            # mlab default detrend_none
+        self.K = NFFT // 2 + 1
+        self.T = self.plan.frames(self.n)
+        self.ld = max(32, (self.T + 31) // 32 * 32)
+        self.freqs, self.t = _freqs_times(self.n, NFFT, Fs, noverlap)
+        es = self.dtype.itemsize
+        self.d_x = self.ctx.alloc((self.n + 7) // 8 * 8 * es)
+        self.d_off = self.ctx.alloc(8)
+        self.d_len = self.ctx.alloc(8)
+        self.d_off.upload(np.zeros(1, np.int64))
+        self.d_len.upload(np.array([self.n], np.int64))
+        self.d_spec = self.ctx.alloc(self.K * self.ld * 4)
+        self.d_sum = self.ctx.alloc(8)
+
+    def run(self, x: np.ndarray):
+        x = np.ascontiguousarray(x, dtype=self.dtype)
+        if x.shape != (self.n,):
+            raise ValueError("signal length differs from the plan's")
+        self.d_x.upload(x)
+        self.plan.run_dev(self.d_x, self.dtype, self.d_off, self.d_len, 1, self.T, self.d_spec, self.ld)
+
+    def spectrogram(self) -> np.ndarray:
+        out = np.empty((self.K, self.ld), np.float32)
+        self.d_spec.download(out)
+        return out[:, : self.T].astype(np.float64)
+
+    def band_power(self, lo_hz: float, hi_hz: float) -> tuple[float, int]:
+        """(np.sum(Pxx[(freqs >= lo) & (freqs <= hi)]), number of bins) on the device."""
+        idx = np.nonzero((self.freqs >= lo_hz) & (self.freqs <= hi_hz))[0]
+        if idx.size == 0:
+            return 0.0, 0
+        assert idx[-1] - idx[0] + 1 == idx.size
+        _lib.check(self.ctx.lib.msd_spec_band_sum_dev(self.ctx.h, self.d_spec.ptr, 1, self.K, self.T, self.ld,
+                                                      int(idx[0]), int(idx[-1]), self.d_sum.ptr))
+        s = np.empty(1, np.float64)
+        self.d_sum.download(s)
+        return float(s[0]), int(idx.size)
+
+
+def specgram(x, NFFT=None, Fs=None, noverlap=None, device: int = 0):
+    """matplotlib.mlab.specgram(x, NFFT, Fs, noverlap) defaults (window_hanning, detrend_none,
+    one-sided psd, scale_by_freq): returns (spec float64 [NFFT//2+1, T], freqs, t)."""
+    x = np.asarray(x)
+    if x.ndim != 1:
+        raise NotImplementedError("only 1-D real signals are implemented")
+    NFFT = 256 if NFFT is None else int(NFFT)
+    Fs = 2 if Fs is None else Fs
+    noverlap = 128 if noverlap is None else int(noverlap)
+    dt = x.dtype if x.dtype in (np.int16, np.uint8, np.float32) else np.float32
+    p = SpecgramPlan(len(x), NFFT, Fs, noverlap, dtype=dt, device=device)
+    p.run(x.astype(dt, copy=False))
+    return p.spectrogram(), p.freqs, p.t
+
+
+def noise_floor(x, fs, NFFT=2048, lower_freq=250, upper_freq=800, cut_factor=C_MS_SPEC_CUT_FACTOR, device: int = 0):
+    """prime_detection.py:65-91 without the figure: returns (Pxx, freqs, bins, vmin,
+    power_density_db_hz) for ``plt.specgram(x, Fs=fs, NFFT=NFFT, noverlap=NFFT // 2)``."""
+    x = np.asarray(x)
+    dt = x.dtype if x.dtype in (np.int16, np.uint8, np.float32) else np.float32
+    p = SpecgramPlan(len(x), NFFT, fs, NFFT // 2, dtype=dt, device=device)
+    p.run(x.astype(dt, copy=False))
+    band_power, nbins = p.band_power(lower_freq, upper_freq)
+    delta_f = fs / NFFT
+    bandwidth = nbins * delta_f
+    with np.errstate(divide="ignore", invalid="ignore"):
+        pddb = 10 * np.log10(band_power / bandwidth)
+    factor = 40 / 23
+    vmin = pddb / factor + cut_factor
+    return p.spectrogram(), p.freqs, p.t, float(vmin), float(pddb)

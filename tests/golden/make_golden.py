@@ -10,6 +10,9 @@ exactly as the reference makes them, on seeded synthetic inputs:
                  (mb_files, main.py:825-899) and a 48 kHz configuration
   spec_*.npz   : scipy.signal.spectrogram(x, fs, 'hann', nperseg=N, noverlap=N//2,
                  nfft=N, scaling='density', mode='psd') (main.py:132-133), float32
+  legacy_5k.npz: matplotlib.mlab.specgram(x, NFFT=2048, Fs=5000, noverlap=1024) as
+                 plt.specgram computes it, the 250-800 Hz band power over bins and frames and
+                 the colour floor vmin (meteor_detect_class/prime_detection.py:65-91)
   live_4k.npz  : per processing block, scipy.signal.welch(block, fs, nfft=n_fft) on the
                  soundfile float64 of PCM16 samples (x / 32768), the three inclusive band
                  masks and np.sum → dB (dsp/src/live/backend/processor.py:206, :349-369),
@@ -67,9 +70,24 @@ def live_golden():
                         psd_blocks=np.array([3, 77]), psd=np.array(psd2))
 
 
+def legacy_golden():
+    from matplotlib import mlab
+    fs, NFFT = 5000, 2048
+    x, _ = synth_real(seed=5151, fs=fs, duration_s=6.0, f0=1000.0, sigma=800.0, rate_per_min=20, band_hz=100.0,
+                      snr_db=(10, 25))
+    Pxx, freqs, t = mlab.specgram(x, NFFT=NFFT, Fs=fs, noverlap=NFFT // 2)    # prime_detection.py:70
+    nb = (freqs >= 250) & (freqs <= 800)
+    band_power = np.sum(Pxx[nb])
+    pddb = 10 * np.log10(band_power / (np.sum(nb) * (fs / NFFT)))
+    np.savez_compressed(os.path.join(HERE, "legacy_5k.npz"), x=x, fs=fs, NFFT=NFFT, Pxx=Pxx, freqs=freqs, t=t,
+                        band_power=band_power, pddb=pddb, vmin=pddb / (40 / 23) + 12)
+
+
 def main(names=()):
     if not names or "live" in names:
         live_golden()
+    if not names or "legacy" in names:
+        legacy_golden()
     if names and "core" not in names:
         return
     # 6 kHz, the reference's own configuration (main.py:827-833, 865-899)

@@ -1,0 +1,71 @@
+"""Legacy spectrogram noise floor (prime_detection.py:65-91).
+
+CPU: the oracle against the matplotlib golden (tests/golden/legacy_5k.npz).
+GPU: meteorgpu.legacy (libmsdsp STFT with detrend off + device band sum) against the golden
+and the oracle.  Bars: spectrogram within SPEC_TOL relative per frame (float32 kernels vs
+matplotlib's float64), band power within 1e-5 relative, vmin within VMIN_TOL dB."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import legacy_oracle as LO
+
+SPEC_TOL = 1e-5
+VMIN_TOL = 1e-4
+
+
+def _frame_rel(a, b):
+    num = np.linalg.norm(a - b, axis=0)
+    den = np.linalg.norm(b, axis=0)
+    return float(np.max(num / np.maximum(den, 1e-300)))
+
+
+def test_oracle_matches_golden(golden_dir):
+    g = np.load(os.path.join(golden_dir, "legacy_5k.npz"))
+    Pxx, freqs, t, vmin, pddb = LO.noise_floor_ref(g["x"], int(g["fs"]), int(g["NFFT"]))
+    np.testing.assert_array_equal(Pxx, g["Pxx"])
+    np.testing.assert_array_equal(freqs, g["freqs"])
+    np.testing.assert_array_equal(t, g["t"])
+    assert vmin == g["vmin"] and pddb == g["pddb"]
+
+
+@pytest.mark.gpu
+def test_noise_floor_golden(golden_dir):
+    from meteorgpu import legacy
+    g = np.load(os.path.join(golden_dir, "legacy_5k.npz"))
+    Pxx, freqs, t, vmin, pddb = legacy.noise_floor(g["x"], int(g["fs"]), int(g["NFFT"]))
+    assert Pxx.shape == g["Pxx"].shape
+    np.testing.assert_array_equal(freqs, g["freqs"])
+    np.testing.assert_array_equal(t, g["t"])
+    assert _frame_rel(Pxx, g["Pxx"]) < SPEC_TOL
+    assert abs(vmin - float(g["vmin"])) < VMIN_TOL
+    assert abs(pddb - float(g["pddb"])) < VMIN_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("NFFT,fs,dtype", [(2048, 5000, np.int16), (1024, 5000, np.int16), (256, 6000, np.int16),
+                                           (512, 5000, np.float32)])
+def test_specgram_vs_mlab(NFFT, fs, dtype):
+    from meteorgpu import legacy, synth
+    x, _ = synth.synth_real(seed=NFFT + fs, fs=fs, duration_s=8.0, f0=1000.0, sigma=700.0, rate_per_min=15)
+    if dtype == np.float32:
+        x = (x / 32768.0).astype(np.float32)
+    P, f, t = legacy.specgram(x, NFFT=NFFT, Fs=fs, noverlap=NFFT // 2)
+    rP, rf, rt = LO.specgram_ref(x, NFFT, fs, NFFT // 2)
+    assert P.shape == rP.shape
+    np.testing.assert_array_equal(f, rf)
+    np.testing.assert_array_equal(t, rt)
+    assert _frame_rel(P, rP) < SPEC_TOL
+
+
+@pytest.mark.gpu
+def test_noise_floor_30s_reference_shape():
+    """The reference's own configuration: 30 s at 5 kHz (C_SEG_LEN, C_SAMPLE_RATE), NFFT 2048."""
+    from meteorgpu import legacy, synth
+    x, _ = synth.synth_real(seed=31, fs=5000, duration_s=30.0, f0=1000.0, sigma=600.0, rate_per_min=10)
+    P, f, t, vmin, pddb = legacy.noise_floor(x, 5000)
+    rP, rf, rt, rvmin, rpddb = LO.noise_floor_ref(x, 5000)
+    assert P.shape == rP.shape == (1025, 145)
+    assert _frame_rel(P, rP) < SPEC_TOL
+    assert abs(vmin - rvmin) < VMIN_TOL
