@@ -118,3 +118,44 @@ def noise_floor(x, fs, NFFT=2048, lower_freq=250, upper_freq=800, cut_factor=C_M
     factor = 40 / 23
     vmin = pddb / factor + cut_factor
     return p.spectrogram(), p.freqs, p.t, float(vmin), float(pddb)
+
+
+# ------------------------------------------------------------------ §8(f) legacy drop-in shim
+def detect_and_cluster_bursts_audio(segment, fs, freq_band=(950.0, 1050.0), noise_band=(650.0, 750.0),
+                                    n_fft=1024, block_duration_sec=0.1, threshold_std_factor=4.0,
+                                    critical_min_dur_s=0.5, device: int = 0):
+    """Audio-fed stand-in for ``detect_and_cluster_bursts(image_path, ...)``
+    (meteor_detect_class/detector_and_classification.py:7-91) with its return shape
+    ``(bursts, unique_labels, burst_positions, critical_bursts, non_critical_bursts)``, so the
+    hourly loop of prime_detection.py:208-252 runs unchanged.  Bursts are the GPU block
+    detector's detections on the segment (adaptive threshold, main.py:450-522); a burst is
+    critical when it lasts >= 0.5 s, the duration rule of detector_and_classification.py:50
+    (``duration >= 5`` pixels ≈ 0.5 s).  The counts are not those of the reference's ORB /
+    DBSCAN image clustering (a different algorithm); only the interface and the hourly CSV
+    format are compatible."""
+    from .dsp import process_samples
+    x = np.asarray(segment)
+    if x.ndim == 2:
+        x = x[:, 0]  # prime_detection.py:70 uses iq_segment[:, 0]
+    res = process_samples(x, fs, block_duration_sec, freq_band, noise_band, n_fft, threshold_std_factor,
+                          flag_adaptive_threshold=True, device=device)
+    bursts = list(res.detections)
+    labels = set(range(len(bursts)))
+    positions = [(d.t_start, d.t_stop) for d in bursts]
+    critical = [i for i, d in enumerate(bursts) if d.dur_s >= critical_min_dur_s]
+    non_critical = [i for i, d in enumerate(bursts) if d.dur_s < critical_min_dur_s]
+    return bursts, labels, positions, critical, non_critical
+
+
+HOURLY_COLUMNS = ("Timestamp", "Anzahl", "Kritisch")  # prime_detection.py:138
+
+
+def append_hourly_row(file_name, start_time, n_critical: int, n_non_critical: int) -> None:
+    """prime_detection.py:229-245: append ``start_time;total;critical`` to the day's
+    ``;``-separated CSV (header ``Timestamp;Anzahl;Kritisch``, created if missing — :139-146)."""
+    import os
+    new = not os.path.exists(file_name)
+    with open(file_name, "a", newline="") as fh:
+        if new:
+            fh.write(";".join(HOURLY_COLUMNS) + "\n")
+        fh.write(f"{start_time.strftime('%Y-%m-%d %H:%M:%S')};{n_critical + n_non_critical};{n_critical}\n")

@@ -69,3 +69,38 @@ def test_noise_floor_30s_reference_shape():
     assert P.shape == rP.shape == (1025, 145)
     assert _frame_rel(P, rP) < SPEC_TOL
     assert abs(vmin - rvmin) < VMIN_TOL
+
+
+def test_hourly_csv_matches_pandas_flow(tmp_path):
+    """prime_detection.py:137-146 (create) and :229-245 (append) done with pandas as the
+    reference does, against meteorgpu.legacy.append_hourly_row."""
+    import datetime
+    import pandas as pd
+    from meteorgpu import legacy
+    ref = tmp_path / "ref.csv"
+    pd.DataFrame(columns=["Timestamp", "Anzahl", "Kritisch"]).to_csv(ref, sep=";", index=False)
+    rows = [(datetime.datetime(2025, 6, 1, 10, 0, 3), 3, 4), (datetime.datetime(2025, 6, 1, 10, 59, 51), 0, 0)]
+    for st, nc, nn in rows:
+        df2 = pd.read_csv(ref, sep=";")
+        df2 = pd.concat([df2, pd.DataFrame([{"Timestamp": st.strftime("%Y-%m-%d %H:%M:%S"),
+                                             "Anzahl": nc + nn, "Kritisch": nc}])], ignore_index=True)
+        df2.to_csv(ref, sep=";", index=False)
+    ours = tmp_path / "ours.csv"
+    for st, nc, nn in rows:
+        legacy.append_hourly_row(ours, st, nc, nn)
+    assert ours.read_bytes() == ref.read_bytes()
+
+
+@pytest.mark.gpu
+def test_burst_shim_classifies_by_duration():
+    from meteorgpu import legacy, synth
+    from oracle import dsp_oracle as O
+    x, _ = synth.synth_real(seed=13, fs=5000, duration_s=30.0, f0=1000.0, sigma=500.0, rate_per_min=6,
+                            band_hz=100.0, snr_db=(20, 35), dur_s=(0.2, 2.0))
+    bursts, labels, pos, crit, noncrit = legacy.detect_and_cluster_bursts_audio(x, 5000)
+    ref, *_ = O.proc_samples_ref(x, 5000, 0.1, (950.0, 1050.0), (650.0, 750.0), 1024, 4.0)
+    assert [(d.t_start, d.t_stop) for d in bursts] == [(r[0], r[1]) for r in ref]
+    assert len(bursts) > 0 and labels == set(range(len(bursts)))
+    assert sorted(crit + noncrit) == list(range(len(bursts)))
+    assert all(bursts[i].dur_s >= 0.5 for i in crit) and all(bursts[i].dur_s < 0.5 for i in noncrit)
+    assert len(crit) >= 1 and len(noncrit) >= 1
