@@ -44,6 +44,9 @@ extern "C" {
 #define MSD_I32 3
 #define MSD_F32 4
 #define MSD_F64 5
+/* complex (I/Q) samples, interleaved I, Q: one complex sample = 2 elements */
+#define MSD_CI16 6
+#define MSD_CF32 7
 
 typedef struct msd_ctx msd_ctx;
 typedef struct msd_stft_plan msd_stft_plan;
@@ -72,7 +75,7 @@ int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.
  * kernel id: 0 = STFT power, 1 = block delta, 2 = detector stats, 3 = detector scan,
- * 4 = Welch band powers, 5 = live detector. */
+ * 4 = Welch band powers, 5 = live detector, 6 = complex (I/Q) STFT. */
 int msd_timing_enable(msd_ctx *ctx, int enable);
 int msd_timing_reset(msd_ctx *ctx);
 int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
@@ -165,6 +168,25 @@ int msd_detect_dev(msd_ctx *ctx, const double *delta, const int64_t *nblocks, in
  * global mode: *thresholds receives the single threshold in thresholds[0]. */
 int msd_detect(msd_ctx *ctx, const double *delta, int64_t nb, const msd_det_cfg *cfg, msd_det *dets, int64_t cap,
                int64_t *count, double *thresholds, double *margin);
+
+/* --------------------------------------- C5: two-sided STFT of complex (I/Q) input
+ * scipy.signal.spectrogram(z, fs, 'hann', nperseg=N, noverlap=N-hop) for complex z (BASELINE
+ * config C5: 192 kHz I/Q, N = 4096, 75 % overlap): two-sided, bins in FFT order (0..N/2-1,
+ * -N/2..-1), |X|^2 * scale, constant detrend of the complex frame mean, complex64 arithmetic.
+ * window: N float32 (periodic Hann); scale = 1/(fs*sum(w^2)).  nperseg must be 4096.
+ * Output FRAME-major: out[(s*max_frames + t)*N + k] (scipy's Sxx[k][t] transposed; a
+ * frequency-major tile of 4096 rows would not fit in LDS); frames past a stream's end are 0.
+ * off/len: device int64 arrays in complex samples; dtype MSD_CI16 or MSD_CF32. */
+typedef struct msd_cstft_plan msd_cstft_plan;
+int msd_cstft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float *window, double scale,
+                          msd_cstft_plan **out);
+void msd_cstft_plan_destroy(msd_cstft_plan *plan);
+int msd_cstft_set_detrend(msd_cstft_plan *plan, int detrend);
+int64_t msd_cstft_frames(const msd_cstft_plan *plan, int64_t n);
+int msd_cstft_psd_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                      int64_t nstreams, int64_t max_frames, float *out);
+/* one stream, host buffers: n complex samples in, out float32 [T][N] */
+int msd_cstft_psd(msd_cstft_plan *plan, const void *x, int dtype, int64_t n, float *out, int64_t *frames);
 
 /* ------------------------------------------- a10: legacy spectrogram noise floor
  * prime_detection.py:65-91: band_power = np.sum(Pxx[noise_band]) sums the spectrogram over

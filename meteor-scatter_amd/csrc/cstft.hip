@@ -1,0 +1,319 @@
+// Two-sided power spectrogram of complex (I/Q) input — BASELINE config C5 (192 kHz I/Q,
+// 4096-point frames, 75 % overlap).  The quantity is scipy.signal.spectrogram(z, fs, 'hann',
+// nperseg=N, noverlap=N-hop) for complex z (return_onesided switches to two-sided, bins in
+// FFT order, |X|^2 / (fs * sum w^2), no doubling, complex64 arithmetic → float32 output).
+//
+// Mapping: one 256-thread workgroup transforms one frame at a time (persistent over a
+// contiguous range of frames).  N = 4096 = 16 x 16 x 16:
+//   pass 1  thread j holds z[j + 256 r] (r = 0..15, the coalesced load order): a 16-point
+//           DFT over r in registers, then the twiddle W4096^(j q) (held in registers across
+//           frames);
+//   LDS     y[q][j] → thread (q, j1) gets y[q][j1 + 16 j2];
+//   pass 2  16-point DFT over j2, twiddle W256^(j1 k2a) (LDS table);
+//   LDS     → thread t = q + 16 k2a gets the 16 values over j1;
+//   pass 3  16-point DFT over j1 → X[t + 256 k2b], k2b = 0..15.
+// The powers leave frame-major, out[frame][k] (FFT order): 256 threads store 1 KB of
+// consecutive bins per instruction, no output tile.  (A frequency-major [K][T] tile for
+// K = 4096 would need 512 KB of LDS per 128-B row segment; scipy's [K][T] is the transpose of
+// this layout.)  The window carries sqrt(scale), so |X|^2 is the density directly.
+#include <cmath>
+
+#include "msd_internal.h"
+
+namespace msd {
+namespace {
+
+constexpr int CS_T = 256;              // threads per workgroup
+constexpr int CS_N = 4096;             // frame length
+constexpr int CS_P = 272;              // LDS row pitch (float2) of the 16 x 256 transposes
+constexpr int CS_LDS_F2 = 16 * CS_P;   // float2 per frame buffer
+
+__device__ __forceinline__ float2 c_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 c_mul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 c_mi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
+
+__device__ __forceinline__ void dft4(float2 &a0, float2 &a1, float2 &a2, float2 &a3) {
+    const float2 t0 = c_add(a0, a2), t1 = c_sub(a0, a2), t2 = c_add(a1, a3), t3 = c_mi(c_sub(a1, a3));
+    a0 = c_add(t0, t2);
+    a1 = c_add(t1, t3);
+    a2 = c_sub(t0, t2);
+    a3 = c_sub(t1, t3);
+}
+
+// forward 16-point DFT, natural order in and out: n = n1 + 4 n2, k = k2 + 4 k1
+__device__ __forceinline__ void dft16(float2 *v) {
+    const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f, h = 0.70710678118654752440f;
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) dft4(v[n1], v[n1 + 4], v[n1 + 8], v[n1 + 12]);  // v[n1 + 4 k2]
+    // twiddles W16^(n1 k2)
+    v[5] = c_mul(v[5], make_float2(c1, -s1));    // n1 1, k2 1: W^1
+    v[9] = c_mul(v[9], make_float2(h, -h));      // n1 1, k2 2: W^2
+    v[13] = c_mul(v[13], make_float2(s1, -c1));  // n1 1, k2 3: W^3
+    v[6] = c_mul(v[6], make_float2(h, -h));      // n1 2, k2 1: W^2
+    v[10] = c_mi(v[10]);                         // n1 2, k2 2: W^4 = -i
+    v[14] = c_mul(v[14], make_float2(-h, -h));   // n1 2, k2 3: W^6
+    v[7] = c_mul(v[7], make_float2(s1, -c1));    // n1 3, k2 1: W^3
+    v[11] = c_mul(v[11], make_float2(-h, -h));   // n1 3, k2 2: W^6
+    v[15] = c_mul(v[15], make_float2(-c1, s1));  // n1 3, k2 3: W^9
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) dft4(v[4 * k2], v[4 * k2 + 1], v[4 * k2 + 2], v[4 * k2 + 3]);
+    // v[4 k2 + k1] holds X[k2 + 4 k1]: reorder to natural
+    float2 o[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2)
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1) o[k2 + 4 * k1] = v[4 * k2 + k1];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = o[i];
+}
+
+template <typename T>
+struct IQ;
+template <>
+struct IQ<int16_t> {  // interleaved int16 I, Q
+    using raw_t = uint32_t;
+    __device__ static raw_t load(const int16_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+    __device__ static int re_i(raw_t r) { return (int)(int16_t)(r & 0xffffu); }
+    __device__ static int im_i(raw_t r) { return (int)(int16_t)(r >> 16); }
+    __device__ static float2 f(raw_t r) { return make_float2((float)re_i(r), (float)im_i(r)); }
+};
+template <>
+struct IQ<float> {  // interleaved float32 I, Q (complex64)
+    using raw_t = float2;
+    __device__ static raw_t load(const float *p) { return *reinterpret_cast<const float2 *>(p); }
+    __device__ static float2 f(raw_t r) { return r; }
+};
+
+struct StreamCur {
+    int64_t s, t;    // stream, frame
+    int64_t nfr;     // frames in the stream
+    int64_t base;    // element offset (complex samples) of the stream
+};
+
+template <typename T>
+__global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x, const int64_t *__restrict__ off,
+                                                         const int64_t *__restrict__ len, int64_t nstreams,
+                                                         int64_t max_frames, int64_t total, int64_t per, int hop,
+                                                         int detrend, const float *__restrict__ g_win,
+                                                         const float2 *__restrict__ g_tw, float *__restrict__ out) {
+    using io = IQ<T>;
+    __shared__ float2 buf[CS_LDS_F2];
+    __shared__ float2 tw256[256];
+    __shared__ double red[2][CS_T / 64];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < 256; i += CS_T) tw256[i] = g_tw[16 * i];  // W256^i = W4096^(16 i)
+    // per-thread constants: window (x sqrt(scale)) and the pass-1 twiddles W4096^(j q)
+    float wr[16];
+    float2 tw1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        wr[r] = g_win[tid + 256 * r];
+        tw1[r] = g_tw[(tid * r) & (CS_N - 1)];
+    }
+    const int q2 = tid >> 4, j1 = tid & 15;   // pass-2 thread: (q, j1)
+    const int q3 = tid & 15, k2a = tid >> 4;  // pass-3 thread: t = q + 16 k2a
+    __syncthreads();
+
+    const int64_t g0 = (int64_t)blockIdx.x * per;
+    const int64_t g1 = g0 + per < total ? g0 + per : total;
+    if (g0 >= g1) return;
+    auto cur_at = [&](int64_t g) {
+        StreamCur c;
+        c.s = g / max_frames;
+        c.t = g - c.s * max_frames;
+        const int64_t n = len[c.s];
+        c.nfr = n >= CS_N ? (n - CS_N) / hop + 1 : 0;
+        c.base = off[c.s];
+        return c;
+    };
+    auto load = [&](const StreamCur &c, typename io::raw_t (&raw)[16]) {
+        if (c.t < c.nfr) {
+            const T *p = x + 2 * (c.base + c.t * (int64_t)hop);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) raw[r] = io::load(p + 2 * (tid + 256 * r));
+        }
+    };
+    typename io::raw_t raw[16];
+    StreamCur cur = cur_at(g0);
+    load(cur, raw);
+    for (int64_t g = g0; g < g1; ++g) {
+        const StreamCur nxt = g + 1 < g1 ? cur_at(g + 1) : cur;
+        const bool valid = cur.t < cur.nfr;  // uniform
+        float2 v[16];
+        // ---- detrend: the frame's complex mean (scipy 'constant'), workgroup reduction in fp64
+        double sr = 0.0, si = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            v[r] = io::f(raw[r]);
+            sr += (double)v[r].x;
+            si += (double)v[r].y;
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            sr += __shfl_xor(sr, o, 64);
+            si += __shfl_xor(si, o, 64);
+        }
+        if (lane == 0) {
+            red[0][wave] = sr;
+            red[1][wave] = si;
+        }
+        if (g + 1 < g1) load(nxt, raw);  // prefetch the next frame (raw is consumed)
+        __syncthreads();
+        float mr = 0.f, mi = 0.f;
+        if (detrend) {
+            mr = (float)((red[0][0] + red[0][1] + red[0][2] + red[0][3]) * (1.0 / CS_N));
+            mi = (float)((red[1][0] + red[1][1] + red[1][2] + red[1][3]) * (1.0 / CS_N));
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = make_float2((v[r].x - mr) * wr[r], (v[r].y - mi) * wr[r]);
+        // ---- pass 1: DFT over r, twiddle W4096^(j q), y[q][j]
+        dft16(v);
+#pragma unroll
+        for (int q = 1; q < 16; ++q) v[q] = c_mul(v[q], tw1[q]);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) buf[q * CS_P + tid] = v[q];
+        __syncthreads();
+        // ---- pass 2: thread (q, j1): DFT over j2 of y[q][j1 + 16 j2], twiddle W256^(j1 k2a)
+#pragma unroll
+        for (int j2 = 0; j2 < 16; ++j2) v[j2] = buf[q2 * CS_P + j1 + 16 * j2];
+        dft16(v);
+#pragma unroll
+        for (int k = 1; k < 16; ++k) v[k] = c_mul(v[k], tw256[(j1 * k) & 255]);
+        __syncthreads();  // everyone has read pass 1's layout
+#pragma unroll
+        for (int k = 0; k < 16; ++k) buf[q2 * CS_P + 16 * k + j1] = v[k];  // u[q][k2a][j1]
+        __syncthreads();
+        // ---- pass 3: thread t = q + 16 k2a: DFT over j1 → X[t + 256 k2b]
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = buf[q3 * CS_P + 16 * k2a + j];
+        dft16(v);
+        {  // frames past a stream's end (shorter streams in a batch) are written as zeros
+            float *of = out + (cur.s * max_frames + cur.t) * (int64_t)CS_N;
+#pragma unroll
+            for (int k2b = 0; k2b < 16; ++k2b)
+                of[tid + 256 * k2b] = valid ? v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y : 0.f;
+        }
+        __syncthreads();  // buf and red are reused by the next frame
+        cur = nxt;
+    }
+}
+
+}  // namespace
+}  // namespace msd
+
+struct msd_cstft_plan {
+    msd_ctx *ctx = nullptr;
+    int nperseg = 0, hop = 0, detrend = 1;
+    float *d_win = nullptr;   // window x sqrt(scale)
+    float2 *d_tw = nullptr;   // W4096^m, m = 0..4095
+};
+
+using namespace msd;
+
+extern "C" {
+
+int msd_cstft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float *window, double scale,
+                          msd_cstft_plan **out) {
+    if (!ctx || !window || !out) return fail(MSD_ERR_INVALID, "msd_cstft_plan_create: null");
+    *out = nullptr;
+    if (nperseg != CS_N) return fail(MSD_ERR_UNSUPPORTED, "cstft: nperseg must be 4096");
+    if (hop <= 0 || hop > nperseg) return fail(MSD_ERR_INVALID, "cstft: need 0 < hop <= nperseg");
+    if (!(scale > 0)) return fail(MSD_ERR_INVALID, "cstft: scale must be > 0");
+    DeviceGuard g(ctx->device);
+    auto *p = new msd_cstft_plan();
+    p->ctx = ctx;
+    p->nperseg = nperseg;
+    p->hop = hop;
+    std::vector<float> w(nperseg);
+    const double rs = std::sqrt(scale);
+    for (int i = 0; i < nperseg; ++i) w[i] = (float)((double)window[i] * rs);
+    std::vector<float2> tw(CS_N);
+    for (int m = 0; m < CS_N; ++m) {
+        const double a = -2.0 * M_PI * (double)m / (double)CS_N;
+        tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    hipError_t e = hipMalloc(&p->d_win, sizeof(float) * nperseg);
+    if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(float2) * CS_N);
+    if (e == hipSuccess) e = hipMemcpy(p->d_win, w.data(), sizeof(float) * nperseg, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(float2) * CS_N, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        msd_cstft_plan_destroy(p);
+        return hip_fail(e, "msd_cstft_plan_create");
+    }
+    *out = p;
+    return MSD_OK;
+}
+
+void msd_cstft_plan_destroy(msd_cstft_plan *p) {
+    if (!p) return;
+    DeviceGuard g(p->ctx->device);
+    (void)hipStreamSynchronize(p->ctx->stream);
+    if (p->d_win) (void)hipFree(p->d_win);
+    if (p->d_tw) (void)hipFree(p->d_tw);
+    delete p;
+}
+
+int msd_cstft_set_detrend(msd_cstft_plan *p, int detrend) {
+    if (!p || (detrend != 0 && detrend != 1)) return fail(MSD_ERR_INVALID, "msd_cstft_set_detrend: bad args");
+    p->detrend = detrend;
+    return MSD_OK;
+}
+
+int64_t msd_cstft_frames(const msd_cstft_plan *p, int64_t n) {
+    if (!p || n < p->nperseg) return 0;
+    return (n - p->nperseg) / p->hop + 1;
+}
+
+int msd_cstft_psd_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                      int64_t nstreams, int64_t max_frames, float *out) {
+    if (!p || (nstreams > 0 && (!x || !off || !len || !out))) return fail(MSD_ERR_INVALID, "msd_cstft_psd_dev: null");
+    if (dtype != MSD_CI16 && dtype != MSD_CF32) return fail(MSD_ERR_UNSUPPORTED, "cstft: dtype must be CI16 or CF32");
+    if (nstreams == 0 || max_frames == 0) return MSD_OK;
+    DeviceGuard g(p->ctx->device);
+    const int64_t total = nstreams * max_frames;
+    int64_t wgs = (int64_t)p->ctx->num_cu * 3;  // LDS (36 KB) and registers allow 3 per CU
+    if (wgs > total) wgs = total;
+    const int64_t per = (total + wgs - 1) / wgs;
+    wgs = (total + per - 1) / per;
+    KernelTimer timer(p->ctx, K_CSTFT);
+    if (dtype == MSD_CI16)
+        hipLaunchKernelGGL(cstft4096_kernel<int16_t>, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream,
+                           static_cast<const int16_t *>(x), off, len, nstreams, max_frames, total, per, p->hop,
+                           p->detrend, p->d_win, p->d_tw, out);
+    else
+        hipLaunchKernelGGL(cstft4096_kernel<float>, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream,
+                           static_cast<const float *>(x), off, len, nstreams, max_frames, total, per, p->hop,
+                           p->detrend, p->d_win, p->d_tw, out);
+    MSD_HIP(hipGetLastError());
+    return MSD_OK;
+}
+
+int msd_cstft_psd(msd_cstft_plan *p, const void *x, int dtype, int64_t n, float *out, int64_t *frames) {
+    if (!p || (!x && n) || !out) return fail(MSD_ERR_INVALID, "msd_cstft_psd: null");
+    const size_t es = dtype == MSD_CI16 ? 4 : dtype == MSD_CF32 ? 8 : 0;
+    if (!es) return fail(MSD_ERR_UNSUPPORTED, "cstft: dtype must be CI16 or CF32");
+    const int64_t T = msd_cstft_frames(p, n);
+    if (frames) *frames = T;
+    if (T == 0) return MSD_OK;
+    msd_ctx *ctx = p->ctx;
+    DeviceGuard g(ctx->device);
+    void *dx, *dmeta, *dout;
+    int rc;
+    if ((rc = ctx_scratch(ctx, 0, ((size_t)n * es + 255) / 256 * 256, &dx))) return rc;
+    if ((rc = ctx_scratch(ctx, 1, 64, &dmeta))) return rc;
+    if ((rc = ctx_scratch(ctx, 2, sizeof(float) * CS_N * (size_t)T, &dout))) return rc;
+    int64_t meta[2] = {0, n};
+    MSD_HIP(hipMemcpyAsync(dx, x, (size_t)n * es, hipMemcpyHostToDevice, ctx->stream));
+    MSD_HIP(hipMemcpyAsync(dmeta, meta, sizeof(meta), hipMemcpyHostToDevice, ctx->stream));
+    const int64_t *doff = static_cast<const int64_t *>(dmeta);
+    rc = msd_cstft_psd_dev(p, dx, dtype, doff, doff + 1, 1, T, static_cast<float *>(dout));
+    if (rc) return rc;
+    MSD_HIP(hipMemcpyAsync(out, dout, sizeof(float) * CS_N * (size_t)T, hipMemcpyDeviceToHost, ctx->stream));
+    MSD_HIP(hipStreamSynchronize(ctx->stream));
+    return MSD_OK;
+}
+
+}  // extern "C"

@@ -21,7 +21,7 @@ int hip_fail(hipError_t e, const char *what);
         if (e_ != hipSuccess) return hip_fail(e_, #call); \
     } while (0)
 
-enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_WELCH = 4, K_LIVE = 5, K_COUNT = 6 };
+enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_WELCH = 4, K_LIVE = 5, K_CSTFT = 6, K_COUNT = 7 };
 
 struct EventPair {
     hipEvent_t a, b;

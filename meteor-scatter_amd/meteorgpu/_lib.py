@@ -25,6 +25,7 @@ MSD_ERR_INDEX = -6
 MSD_ERR_RCCL = -7
 
 MSD_U8, MSD_I16, MSD_I32, MSD_F32, MSD_F64 = 1, 2, 3, 4, 5
+MSD_CI16, MSD_CF32 = 6, 7  # interleaved I/Q
 DTYPE_CODES = {
     np.dtype(np.uint8): MSD_U8,
     np.dtype(np.int16): MSD_I16,
@@ -33,7 +34,7 @@ DTYPE_CODES = {
     np.dtype(np.float64): MSD_F64,
 }
 
-K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE = 0, 1, 2, 3, 4, 5
+K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE, K_CSTFT = 0, 1, 2, 3, 4, 5, 6
 OPT_GENERIC_STFT = 1
 COMM_ID_BYTES = 128
 
@@ -147,6 +148,12 @@ _SIGS = [
       C.POINTER(MsdHistCfg)]),
     ("msd_detect", C.c_int,
      [_P, _P, C.c_int64, C.POINTER(MsdDetCfg), _P, C.c_int64, C.POINTER(C.c_int64), _P, _P]),
+    ("msd_cstft_plan_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_double, C.POINTER(_P)]),
+    ("msd_cstft_plan_destroy", None, [_P]),
+    ("msd_cstft_set_detrend", C.c_int, [_P, C.c_int]),
+    ("msd_cstft_frames", C.c_int64, [_P, C.c_int64]),
+    ("msd_cstft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P]),
+    ("msd_cstft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
     ("msd_spec_band_sum_dev", C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
     ("msd_welch_plan_create", C.c_int, [_P, C.POINTER(MsdWelchCfg), _P, C.POINTER(_P)]),
     ("msd_welch_plan_destroy", None, [_P]),
@@ -461,3 +468,46 @@ def live_detect(ctx: Context, band_db: np.ndarray, cfg: MsdLiveCfg, cap: int | N
     check(ctx.lib.msd_live_detect(ctx.h, ptr(b), int(nb), C.byref(cfg), ptr(out), int(cap), C.byref(count),
                                   ptr(thr), ptr(over)))
     return out[: count.value], thr[:nb], over[:nb]
+
+
+class CStftPlan:
+    """Two-sided power spectrogram of complex (I/Q) samples (include/msdsp.h, config C5)."""
+
+    def __init__(self, ctx: Context, nperseg: int, hop: int, window: np.ndarray, scale: float):
+        self.ctx = ctx
+        w = np.ascontiguousarray(window, dtype=np.float32)
+        if w.shape != (nperseg,):
+            raise ValueError("window length must equal nperseg")
+        h = C.c_void_p()
+        check(ctx.lib.msd_cstft_plan_create(ctx.h, int(nperseg), int(hop), ptr(w), float(scale), C.byref(h)))
+        self.h = h
+        self.nperseg, self.hop = int(nperseg), int(hop)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.msd_cstft_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def frames(self, n: int) -> int:
+        return int(self.ctx.lib.msd_cstft_frames(self.h, int(n)))
+
+    def run(self, iq: np.ndarray, dtype_code_iq: int) -> np.ndarray:
+        """iq: interleaved I/Q (int16 or float32), 2*n elements → float32 [T][nperseg] (frame-major)."""
+        iq = np.ascontiguousarray(iq)
+        n = iq.shape[0] // 2
+        T = self.frames(n)
+        out = np.empty((T, self.nperseg), np.float32)
+        t = C.c_int64(0)
+        check(self.ctx.lib.msd_cstft_psd(self.h, ptr(iq), int(dtype_code_iq), int(n), ptr(out), C.byref(t)))
+        return out
+
+    def run_dev(self, x: DeviceBuffer, dtype_code_iq: int, off: DeviceBuffer, length: DeviceBuffer, nstreams: int,
+                max_frames: int, out: DeviceBuffer):
+        check(self.ctx.lib.msd_cstft_psd_dev(self.h, x.ptr, int(dtype_code_iq), off.ptr, length.ptr, int(nstreams),
+                                             int(max_frames), out.ptr))

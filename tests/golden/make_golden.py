@@ -13,6 +13,8 @@ exactly as the reference makes them, on seeded synthetic inputs:
   legacy_5k.npz: matplotlib.mlab.specgram(x, NFFT=2048, Fs=5000, noverlap=1024) as
                  plt.specgram computes it, the 250-800 Hz band power over bins and frames and
                  the colour floor vmin (meteor_detect_class/prime_detection.py:65-91)
+  iq_192k_4096.npz: scipy.signal.spectrogram(I + 1j*Q, 192000, 'hann', 4096, noverlap 3072)
+                 (two-sided, config C5 shape), stored as float32
   live_4k.npz  : per processing block, scipy.signal.welch(block, fs, nfft=n_fft) on the
                  soundfile float64 of PCM16 samples (x / 32768), the three inclusive band
                  masks and np.sum → dB (dsp/src/live/backend/processor.py:206, :349-369),
@@ -83,7 +85,24 @@ def legacy_golden():
                         band_power=band_power, pddb=pddb, vmin=pddb / (40 / 23) + 12)
 
 
+def iq_golden():
+    from scipy.signal import spectrogram
+    fs, N = 192000, 4096
+    rng = np.random.default_rng(192)
+    n = 8192
+    t = np.arange(n) / fs
+    z = 3000 * np.exp(2j * np.pi * 1000.0 * t) + 700 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+    i = np.clip(np.round(z.real), -32768, 32767).astype(np.int16)
+    q = np.clip(np.round(z.imag), -32768, 32767).astype(np.int16)
+    f, tt, S = spectrogram(i.astype(np.float64) + 1j * q.astype(np.float64), fs, window="hann", nperseg=N,
+                           noverlap=3 * N // 4)
+    np.savez_compressed(os.path.join(HERE, "iq_192k_4096.npz"), i=i, q=q, fs=fs, nperseg=N, noverlap=3 * N // 4,
+                        f=f, t=tt, S=S.astype(np.float32))
+
+
 def main(names=()):
+    if not names or "iq" in names:
+        iq_golden()
     if not names or "live" in names:
         live_golden()
     if not names or "legacy" in names:

@@ -1,0 +1,70 @@
+"""Complex (I/Q) spectrogram, BASELINE config C5 shape (192 kHz, N = 4096, 75 % overlap).
+
+CPU: the oracle against the scipy golden.  GPU: meteorgpu.iq (cstft4096_kernel through the
+C-ABI) against the golden and the oracle, int16 and float32 I/Q, within SPEC_TOL relative per
+frame (float32 kernel vs scipy's float64 for complex128 input)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import iq_oracle as Q
+
+SPEC_TOL = 1e-5
+
+
+def _frame_rel(a, b):
+    return float(np.max(np.linalg.norm(a - b, axis=0) / np.maximum(np.linalg.norm(b, axis=0), 1e-300)))
+
+
+def test_oracle_matches_golden(golden_dir):
+    g = np.load(os.path.join(golden_dir, "iq_192k_4096.npz"))
+    f, t, S = Q.spectrogram_iq_ref(g["i"], g["q"], int(g["fs"]), int(g["nperseg"]), int(g["noverlap"]))
+    np.testing.assert_array_equal(f, g["f"])
+    np.testing.assert_array_equal(t, g["t"])
+    np.testing.assert_array_equal(S.astype(np.float32), g["S"])
+
+
+@pytest.mark.gpu
+def test_golden():
+    from meteorgpu import iq
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "iq_192k_4096.npz"))
+    f, t, S = iq.spectrogram_iq(g["i"], g["q"], int(g["fs"]), int(g["nperseg"]), int(g["noverlap"]))
+    np.testing.assert_array_equal(f, g["f"])
+    np.testing.assert_array_equal(t, g["t"])
+    assert S.shape == g["S"].shape
+    assert _frame_rel(S, g["S"].astype(np.float64)) < SPEC_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["int16", "float32"])
+@pytest.mark.parametrize("n", [4096, 4096 + 1023, 65536 + 77])
+def test_vs_scipy(kind, n):
+    from meteorgpu import iq
+    rng = np.random.default_rng(n)
+    tt = np.arange(n) / 192000
+    z = 5000 * np.exp(2j * np.pi * (-2500.0) * tt) + 900 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+    if kind == "int16":
+        i, q = np.round(z.real).astype(np.int16), np.round(z.imag).astype(np.int16)
+    else:
+        i, q = (z.real / 32768).astype(np.float32), (z.imag / 32768).astype(np.float32)
+    f, t, S = iq.spectrogram_iq(i, q, 192000, 4096, 3072)
+    rf, rt, rS = Q.spectrogram_iq_ref(i, q, 192000, 4096, 3072)
+    assert S.shape == rS.shape
+    assert _frame_rel(S, rS) < SPEC_TOL
+
+
+@pytest.mark.gpu
+def test_batch_matches_single():
+    from meteorgpu import iq
+    from meteorgpu.dsp import context
+    rng = np.random.default_rng(3)
+    n = 40000
+    streams = [rng.integers(-4000, 4000, 2 * n).astype(np.int16) for _ in range(3)]
+    b = iq.IQBatch(context(0), 3, n, 192000)
+    for s, x in enumerate(streams):
+        b.upload(s, x)
+    b.run()
+    for s, x in enumerate(streams):
+        _, _, S = iq.spectrogram_iq(x[0::2], x[1::2], 192000, 4096, 3072)
+        np.testing.assert_array_equal(b.frames(s, 0, b.T), S.T)
