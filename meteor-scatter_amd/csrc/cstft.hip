@@ -25,8 +25,13 @@ namespace {
 
 constexpr int CS_T = 256;              // threads per workgroup
 constexpr int CS_N = 4096;             // frame length
-constexpr int CS_P = 272;              // LDS row pitch (float2) of the 16 x 256 transposes
-constexpr int CS_LDS_F2 = 16 * CS_P;   // float2 per frame buffer
+// LDS layouts (float2 index) of the two transposes, chosen for the gfx950 bank model:
+//   A (pass 1 → 2): y[q][c] at q*272 + c — the row pitch 272 ≡ 16 (mod 32) puts the two q rows
+//     a half-wave reads into disjoint bank halves;
+//   B (pass 2 → 3): u[q][c] at c*17 + q — column-major with an odd pitch: the pass-3 reads
+//     (16 q values x 2 columns per half-wave) hit 64 distinct banks.
+constexpr int CS_P = 272;
+constexpr int CS_LDS_F2 = 16 * CS_P;   // float2 per frame buffer (= 256 * 17)
 
 __device__ __forceinline__ float2 c_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -79,12 +84,18 @@ struct IQ<int16_t> {  // interleaved int16 I, Q
     __device__ static int re_i(raw_t r) { return (int)(int16_t)(r & 0xffffu); }
     __device__ static int im_i(raw_t r) { return (int)(int16_t)(r >> 16); }
     __device__ static float2 f(raw_t r) { return make_float2((float)re_i(r), (float)im_i(r)); }
+    using acc_t = int;
+    __device__ static int acc_re(raw_t r) { return re_i(r); }
+    __device__ static int acc_im(raw_t r) { return im_i(r); }
 };
 template <>
 struct IQ<float> {  // interleaved float32 I, Q (complex64)
     using raw_t = float2;
     __device__ static raw_t load(const float *p) { return *reinterpret_cast<const float2 *>(p); }
     __device__ static float2 f(raw_t r) { return r; }
+    using acc_t = float;
+    __device__ static float acc_re(raw_t r) { return r.x; }
+    __device__ static float acc_im(raw_t r) { return r.y; }
 };
 
 struct StreamCur {
@@ -144,21 +155,23 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
         const StreamCur nxt = g + 1 < g1 ? cur_at(g + 1) : cur;
         const bool valid = cur.t < cur.nfr;  // uniform
         float2 v[16];
-        // ---- detrend: the frame's complex mean (scipy 'constant'), workgroup reduction in fp64
-        double sr = 0.0, si = 0.0;
+        // ---- detrend: the frame's complex mean (scipy 'constant'): exact integer sums for
+        // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; wave DPP-free xor shuffles,
+        // then one LDS slot per wave
+        typename io::acc_t sr = 0, si = 0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             v[r] = io::f(raw[r]);
-            sr += (double)v[r].x;
-            si += (double)v[r].y;
+            sr += io::acc_re(raw[r]);
+            si += io::acc_im(raw[r]);
         }
         for (int o = 32; o >= 1; o >>= 1) {
             sr += __shfl_xor(sr, o, 64);
             si += __shfl_xor(si, o, 64);
         }
         if (lane == 0) {
-            red[0][wave] = sr;
-            red[1][wave] = si;
+            red[0][wave] = (double)sr;
+            red[1][wave] = (double)si;
         }
         if (g + 1 < g1) load(nxt, raw);  // prefetch the next frame (raw is consumed)
         __syncthreads();
@@ -184,11 +197,11 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
         for (int k = 1; k < 16; ++k) v[k] = c_mul(v[k], tw256[(j1 * k) & 255]);
         __syncthreads();  // everyone has read pass 1's layout
 #pragma unroll
-        for (int k = 0; k < 16; ++k) buf[q2 * CS_P + 16 * k + j1] = v[k];  // u[q][k2a][j1]
+        for (int k = 0; k < 16; ++k) buf[(16 * k + j1) * 17 + q2] = v[k];  // u[q][k2a][j1], column-major
         __syncthreads();
         // ---- pass 3: thread t = q + 16 k2a: DFT over j1 → X[t + 256 k2b]
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = buf[q3 * CS_P + 16 * k2a + j];
+        for (int j = 0; j < 16; ++j) v[j] = buf[(16 * k2a + j) * 17 + q3];
         dft16(v);
         {  // frames past a stream's end (shorter streams in a batch) are written as zeros
             float *of = out + (cur.s * max_frames + cur.t) * (int64_t)CS_N;
