@@ -331,3 +331,26 @@ def test_stft_fast_path_matches_generic_kernel(dt):
     finally:
         ctx.set_option(_lib.OPT_GENERIC_STFT, 0)
     assert _frame_err(fast, gen) <= 2e-6
+
+
+def test_rccl_communicator_single_rank_allreduce():
+    """The N>1 exchange step on the one-GPU box: an RCCL communicator of one rank sums a
+    device histogram in place (identity), through msd_comm_* (dlopen'd librccl)."""
+    from meteorgpu import _lib
+    from meteorgpu.batch import Communicator
+    from meteorgpu.dsp import context
+    ctx = context(0)
+    uid = Communicator.unique_id()
+    assert len(uid) == _lib.COMM_ID_BYTES
+    comm = Communicator(ctx, 1, uid, 0)
+    try:
+        h = np.arange(24, dtype=np.int64) * 7 - 3
+        buf = ctx.alloc(h.nbytes)
+        buf.upload(h)
+        comm.allreduce_i64(buf, h.size)
+        ctx.synchronize()
+        out = np.empty_like(h)
+        buf.download(out)
+        np.testing.assert_array_equal(out, h)
+    finally:
+        comm.close()
