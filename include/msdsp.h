@@ -265,6 +265,32 @@ int msd_live_detect_dev(msd_ctx *ctx, const double *band_db, const int64_t *nblo
 int msd_live_detect(msd_ctx *ctx, const double *band_db /* [3][nb] */, int64_t nb, const msd_live_cfg *cfg,
                     msd_meteor *out, int64_t cap, int64_t *count, double *thresholds, double *over);
 
+/* ------------------------------------------- a1 / §8(f)1: WAV ingest and uploads
+ * scipy.io.wavfile.read semantics for the reference's files (dsp/src/main.py:249): RIFF
+ * little-endian; PCM 8 → u8, 16 → i16, 24 → i32 (sample in the top 3 bytes), 32 → i32;
+ * IEEE float 32 / 64; WAVE_FORMAT_EXTENSIBLE.  msd_wav_read decodes frames
+ * [frame0, frame0+nframes) of one channel (channel >= 0) or all (channel = -1, interleaved)
+ * with pread straight into dst (host memory; pinned memory from msd_host_alloc lets the
+ * upload run asynchronously).  Thread-safe (no shared state). */
+typedef struct {
+    int32_t rate, channels, bits, format; /* format: 1 PCM, 3 IEEE float */
+    int32_t dtype;                        /* MSD_* of the decoded samples */
+    int32_t reserved;
+    int64_t frames;                       /* frames (samples per channel) */
+    int64_t data_offset, data_bytes;
+} msd_wav_info;
+int msd_wav_probe(const char *path, msd_wav_info *info);
+int msd_wav_read(const char *path, int32_t channel, int64_t frame0, int64_t nframes, void *dst, int64_t dst_bytes,
+                 msd_wav_info *info);
+int msd_host_alloc(msd_ctx *ctx, size_t bytes, void **ptr); /* pinned (page-locked) */
+int msd_host_free(msd_ctx *ctx, void *ptr);
+/* upload on the context's copy stream (overlaps the compute stream) */
+int msd_memcpy_h2d_async(msd_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* direction 0: work enqueued on the compute stream from now on waits for the uploads enqueued
+ * so far; 1: uploads enqueued from now on wait for the compute enqueued so far */
+int msd_fence(msd_ctx *ctx, int direction);
+int msd_copy_synchronize(msd_ctx *ctx);
+
 /* ------------------------------------------ multi-GPU: per-hour count reduction
  * RCCL (loaded at run time from librccl.so.1), one communicator per (process, GPU). */
 #define MSD_COMM_ID_BYTES 128

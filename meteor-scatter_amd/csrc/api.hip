@@ -157,6 +157,11 @@ void msd_destroy(msd_ctx *ctx) {
     for (auto e : ctx->pool) hipEventDestroy(e);
     for (int i = 0; i < 4; ++i)
         if (ctx->scratch[i]) hipFree(ctx->scratch[i]);
+    if (ctx->copy_stream) {
+        hipStreamSynchronize(ctx->copy_stream);
+        hipStreamDestroy(ctx->copy_stream);
+    }
+    if (ctx->fence_ev) hipEventDestroy(ctx->fence_ev);
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -34,6 +34,8 @@ struct msd_ctx {
     int device = 0;
     int num_cu = 256;  // compute units (persistent-grid sizing)
     hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;  // host → HBM uploads (msd_memcpy_h2d_async), created on first use
+    hipEvent_t fence_ev = nullptr;      // cross-stream ordering (msd_fence)
     bool timing = false;
     bool force_generic = false;  // MSD_OPT_GENERIC_STFT
     std::vector<msd::EventPair> pending;  // recorded, not yet folded into totals

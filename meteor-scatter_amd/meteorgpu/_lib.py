@@ -113,6 +113,20 @@ METEOR_DTYPE = np.dtype([("start_block", np.int64), ("stop_block", np.int64), ("
                          ("db_max", np.float64), ("db_mean", np.float64), ("db_std", np.float64)])
 
 
+class MsdWavInfo(C.Structure):
+    _fields_ = [
+        ("rate", C.c_int32),
+        ("channels", C.c_int32),
+        ("bits", C.c_int32),
+        ("format", C.c_int32),
+        ("dtype", C.c_int32),
+        ("reserved", C.c_int32),
+        ("frames", C.c_int64),
+        ("data_offset", C.c_int64),
+        ("data_bytes", C.c_int64),
+    ]
+
+
 # (name, restype, argtypes) — every symbol of include/msdsp.h
 _P = C.c_void_p
 _SIGS = [
@@ -163,6 +177,13 @@ _SIGS = [
      [_P, _P, _P, C.c_int64, C.c_int64, C.POINTER(MsdLiveCfg), _P, C.c_int64, _P, _P, _P, _P]),
     ("msd_live_detect", C.c_int,
      [_P, _P, C.c_int64, C.POINTER(MsdLiveCfg), _P, C.c_int64, C.POINTER(C.c_int64), _P, _P]),
+    ("msd_wav_probe", C.c_int, [C.c_char_p, C.POINTER(MsdWavInfo)]),
+    ("msd_wav_read", C.c_int, [C.c_char_p, C.c_int32, C.c_int64, C.c_int64, _P, C.c_int64, C.POINTER(MsdWavInfo)]),
+    ("msd_host_alloc", C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
+    ("msd_host_free", C.c_int, [_P, _P]),
+    ("msd_memcpy_h2d_async", C.c_int, [_P, _P, _P, C.c_size_t]),
+    ("msd_fence", C.c_int, [_P, C.c_int]),
+    ("msd_copy_synchronize", C.c_int, [_P]),
     ("msd_comm_get_unique_id", C.c_int, [_P]),
     ("msd_comm_init", C.c_int, [_P, C.c_int, _P, C.c_int, C.POINTER(_P)]),
     ("msd_comm_destroy", None, [_P]),

@@ -97,14 +97,19 @@ class BatchPipeline:
         self.hist.base_us = int(base_us)
 
     # ------------------------------------------------------------------ the step
-    def run(self):
-        """Enqueue one pass over the batch (no host synchronisation)."""
+    def run(self, x: _lib.DeviceBuffer | None = None, start_us: _lib.DeviceBuffer | None = None,
+            clear_hist: bool = True):
+        """Enqueue one pass over the batch (no host synchronisation).  ``x`` / ``start_us``:
+        alternative device buffers of the same layout as ``d_x`` / ``d_start_us`` (double-buffered
+        ingest); ``clear_hist=False`` accumulates the hour histogram across batches."""
         lib, h = self.ctx.lib, self.ctx.h
-        _lib.check(lib.msd_memset_dev(h, self.d_hist.ptr, 0, self.d_hist.nbytes))
+        x = self.d_x if x is None else x
+        self.hist.file_start_us = (self.d_start_us if start_us is None else start_us).ptr
+        if clear_hist:
+            _lib.check(lib.msd_memset_dev(h, self.d_hist.ptr, 0, self.d_hist.nbytes))
         if self.with_spectrogram:
-            self.stft.run_dev(self.d_x, self.dtype, self.d_off, self.d_len, self.nfiles, self.T, self.d_spec,
-                              self.ld_t)
-        self.blocks.run_dev(self.d_x, self.dtype, self.d_off, self.d_len, self.nfiles, self.nb, None, None,
+            self.stft.run_dev(x, self.dtype, self.d_off, self.d_len, self.nfiles, self.T, self.d_spec, self.ld_t)
+        self.blocks.run_dev(x, self.dtype, self.d_off, self.d_len, self.nfiles, self.nb, None, None,
                             self.d_delta, self.ld_b)
         _lib.check(lib.msd_detect_dev(h, self.d_delta.ptr, self.d_nb.ptr, self.nfiles, self.ld_b, self.cfg,
                                       self.d_dets.ptr, self.cap, self.d_counts.ptr, self.d_thr.ptr,
