@@ -354,3 +354,72 @@ def test_rccl_communicator_single_rank_allreduce():
         np.testing.assert_array_equal(out, h)
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("nperseg", [1024, 256])
+def test_ragged_batch_through_the_c_abi(nperseg):
+    """msd_stft_psd_dev / msd_block_delta_dev / msd_detect_dev on a ragged batch: files of
+    different lengths, one shorter than a frame and a block, one empty, in one launch each —
+    every file equals its single-file result (and the oracle); padding columns are zero."""
+    ctx = dsp.context(0)
+    fs = 48000
+    lens = [fs * 7 + 313, 0, 700, fs * 3, fs * 11 + 5]
+    xs = [synth.synth_real(seed=40 + i, fs=fs, duration_s=max(m, 1) / fs, f0=1000.0, rate_per_min=20,
+                           snr_db=(25.0, 40.0))[0][:m] for i, m in enumerate(lens)]
+    F = len(xs)
+    offs = np.cumsum([0] + [(m + 7) // 8 * 8 for m in lens[:-1]]).astype(np.int64)
+    total = int(offs[-1] + lens[-1] + 8)
+    host = np.zeros(total, np.int16)
+    for o, x in zip(offs, xs):
+        host[o:o + len(x)] = x
+    d_x = ctx.alloc(host.nbytes)
+    d_x.upload(host)
+    d_off, d_len = ctx.alloc(F * 8), ctx.alloc(F * 8)
+    d_off.upload(offs)
+    d_len.upload(np.array(lens, np.int64))
+    w = dsp.hann_periodic(nperseg).astype(np.complex64)
+    scale = float(np.real(1.0 / (fs * (w * w).sum())))
+    plan = _lib.StftPlan(ctx, nperseg, nperseg // 2, w.real.astype(np.float32), scale)
+    K = nperseg // 2 + 1
+    T = [plan.frames(m) for m in lens]
+    ld = max(32, (max(T) + 31) // 32 * 32)
+    d_spec = ctx.alloc(F * K * ld * 4)
+    plan.run_dev(d_x, np.int16, d_off, d_len, F, max(T), d_spec, ld)
+    spec = np.empty((F, K, ld), np.float32)
+    d_spec.download(spec)
+    for i in range(F):
+        if T[i]:
+            _, _, S = dsp.spectrogram(xs[i], fs=fs, nperseg=nperseg, noverlap=nperseg // 2)
+            np.testing.assert_array_equal(spec[i, :, :T[i]], S)
+        assert not spec[i, :, T[i]:].any()
+    # block delta + adaptive detector over the same ragged batch
+    B = int(fs * 0.2)
+    nb = [m // B for m in lens]
+    ldb = max(1, max(nb))
+    blk = _lib.BlockPlan(ctx, B, 1024, dsp.hanning_sym(B)[:1024], dsp.band_bins(1024, fs, (950, 1050)),
+                         dsp.band_bins(1024, fs, (2950, 3050)))
+    d_delta = ctx.alloc(F * ldb * 8)
+    blk.run_dev(d_x, np.int16, d_off, d_len, F, ldb, None, None, d_delta, ldb)
+    delta = np.empty((F, ldb), np.float64)
+    d_delta.download(delta)
+    cfg = _lib.det_cfg(True, 4.0, 600, 15, 100, 50)
+    d_nb = ctx.alloc(F * 8)
+    d_nb.upload(np.array(nb, np.int64))
+    cap = ldb // 2 + 2
+    d_dets, d_cnt, d_thr = ctx.alloc(F * cap * _lib.DET_DTYPE.itemsize), ctx.alloc(F * 8), ctx.alloc(F * ldb * 8)
+    d_mg, d_st = ctx.alloc(F * 8), ctx.alloc(F * 4)
+    _lib.check(ctx.lib.msd_detect_dev(ctx.h, d_delta.ptr, d_nb.ptr, F, ldb, cfg, d_dets.ptr, cap, d_cnt.ptr,
+                                      d_thr.ptr, d_mg.ptr, d_st.ptr, None))
+    cnt = np.empty(F, np.int64)
+    d_cnt.download(cnt)
+    dets = np.empty((F, cap), _lib.DET_DTYPE)
+    d_dets.download(dets)
+    for i in range(F):
+        if nb[i] == 0:
+            assert cnt[i] == 0
+            continue
+        _, _, d, _ = dsp.block_powers(xs[i], fs, 0.2, (950, 1050), (2950, 3050), 512)
+        np.testing.assert_array_equal(delta[i, :nb[i]], d)
+        rdets, _ = O.get_detections_adaptive_ref(d, 4.0, 0.2)
+        assert [(int(a["start"]), int(a["stop"]), float(a["db"])) for a in dets[i, :cnt[i]]] == \
+               [(int(round(r[0] / 0.2)), int(round(r[1] / 0.2)), r[3]) for r in rdets]
