@@ -147,29 +147,49 @@ __global__ __launch_bounds__(DT_THREADS) void detect_kernel(const double *__rest
             if (cfg.adaptive) c_thr[i] = tf[c0 + i];
         }
         __syncthreads();
-        if (tid == 0) {
-            if (cfg.adaptive) {
-                for (int64_t j = 0; j < cn; ++j) {
-                    const int64_t i = c0 + j;
-                    if (i < cfg.fixed_init_blocks) cur_thr = thr0;
-                    else if (i > freeze_until) cur_thr = c_thr[j];
-                    c_thr[j] = cur_thr;  // the threshold actually used (thresholds list)
-                    const double dv = c_delta[j];
-                    const double mg = fabs(dv - cur_thr);
-                    if (mg < min_margin) min_margin = mg;
-                    if (dv > cur_thr) {
-                        if (ndet == 0 || i > last_stop + 1) {
-                            if (ndet > 0 && ndet - 1 < P.cap) df[ndet - 1].stop = last_stop + 1;
-                            ++ndet;
-                            if (ndet - 1 < P.cap) df[ndet - 1].start = i;
-                        }
-                        last_stop = i;
-                        int64_t fu = i + cfg.freeze_after_blocks;
-                        const int64_t fs = i - cfg.freeze_before_blocks > 0 ? i - cfg.freeze_before_blocks : 0;
-                        freeze_until = fu > fs ? fu : fs;
-                    }
+        if (cfg.adaptive && tid < 64) {
+            // wave 0: at position k lane l evaluates block k+l under the current state (the
+            // threshold is thr0 before the fixed-init end, the fresh one after freeze_until,
+            // the held one inside a freeze); the first block above its threshold (ballot) is
+            // the only place the state changes, so a span without one is a single step
+            const int lane = tid;
+            int64_t k = 0;
+            while (k < cn) {
+                const int64_t j = k + lane;
+                const bool valid = j < cn;
+                const int64_t jc = valid ? j : cn - 1;
+                const int64_t i = c0 + jc;
+                const double t = i < cfg.fixed_init_blocks ? thr0 : (i > freeze_until ? c_thr[jc] : cur_thr);
+                const double dv = c_delta[jc];
+                const uint64_t mask = __ballot(valid && dv > t);
+                const int first = mask ? __builtin_ctzll(mask) : 64;
+                const bool take = valid && lane <= first;
+                if (take) c_thr[j] = t;  // the threshold actually used (thresholds list)
+                double mg = take ? fabs(dv - t) : __builtin_inf();
+                for (int o = 32; o >= 1; o >>= 1) mg = fmin(mg, __shfl_xor(mg, o, 64));
+                if (mg < min_margin) min_margin = mg;
+                if (!mask) {  // no event in this span: cur_thr follows the last block's threshold
+                    const int last = (int)((cn - k < 64 ? cn - k : 64) - 1);
+                    cur_thr = __shfl(t, last);
+                    k += 64;
+                    continue;
                 }
-            } else {
+                const int64_t e = c0 + k + first;  // event block
+                cur_thr = __shfl(t, first);
+                if (ndet == 0 || e > last_stop + 1) {
+                    if (lane == 0 && ndet > 0 && ndet - 1 < P.cap) df[ndet - 1].stop = last_stop + 1;
+                    ++ndet;
+                    if (lane == 0 && ndet - 1 < P.cap) df[ndet - 1].start = e;
+                }
+                last_stop = e;
+                const int64_t fu = e + cfg.freeze_after_blocks;
+                const int64_t fs = e - cfg.freeze_before_blocks > 0 ? e - cfg.freeze_before_blocks : 0;
+                freeze_until = fu > fs ? fu : fs;
+                k += first + 1;
+            }
+        }
+        if (!cfg.adaptive && tid == 0) {
+            {
                 for (int64_t j = 0; j < cn; ++j) {
                     const int64_t i = c0 + j;
                     const double dv = c_delta[j];
