@@ -113,9 +113,16 @@ __global__ __launch_bounds__(DT_THREADS) void detect_kernel(const double *__rest
     const double gstd = sqrt(s2 / (double)nb);
     const double thr0 = gmean + cfg.k_std * gstd;
 
-    // ---- 2. fresh adaptive thresholds (main.py:475-480), all blocks in parallel ----
+    // ---- 2. fresh adaptive thresholds (main.py:475-480), all blocks in parallel; a file that
+    // fits one LDS chunk (a 60 s file: 300 blocks) has its windows read from LDS ----
     double *tf = thr + f * P.ld;
+    const bool whole = nb <= DT_CHUNK;
     if (cfg.adaptive) {
+        if (whole) {
+            for (int64_t i = tid; i < nb; i += DT_THREADS) c_delta[i] = d[i];
+            __syncthreads();
+        }
+        const double *src = whole ? c_delta : d;
         const int64_t W = cfg.window_blocks;
         for (int64_t i = tid; i < nb; i += DT_THREADS) {
             if (i < cfg.fixed_init_blocks) {
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(DT_THREADS) void detect_kernel(const double *__rest
                 const int64_t ws = i - W > 0 ? i - W : 0;
                 const int64_t wn = i - ws;
                 double m, s;
-                np_mean_std(d, ws, wn, m, s);
+                np_mean_std(src, ws, wn, m, s);
                 tf[i] = m + cfg.k_std * s;
             }
         }
