@@ -228,6 +228,9 @@ int msd_welch_bands_dev(msd_welch_plan *plan, const void *x, int dtype, const in
                         int64_t nfiles, int64_t max_blocks, double *band_db, int64_t ld, double *psd);
 /* single signal, host buffers: band_db [nbands][nb] */
 int msd_welch_bands(msd_welch_plan *plan, const void *x, int dtype, int64_t n, double *band_db, int64_t *blocks);
+/* single signal, host buffers: the per-block PSD of the band bins, psd [nb][nslots] (one band
+ * 0..nfft/2 and block_size = n gives scipy.signal.welch(x, fs, ...)'s whole PSD) */
+int msd_welch_psd(msd_welch_plan *plan, const void *x, int dtype, int64_t n, double *psd, int64_t *blocks);
 
 /* --------------------------------------------- a9: live detector state machine
  * Replaces processor.py:391-507 (states aggregates.py:4-24) over per-block band dB

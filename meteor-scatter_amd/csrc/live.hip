@@ -111,7 +111,7 @@ __global__ __launch_bounds__(WL_THREADS) void welch_bands_kernel(const T *__rest
     extern __shared__ double sm[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int64_t gb = (int64_t)blockIdx.x * (WL_THREADS / 64) + wave;
+    const int64_t gb = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;  // 1-4 waves per workgroup
     const int64_t f = gb / A.max_blocks;
     const int64_t b = gb - f * A.max_blocks;
     if (f >= A.nfiles) return;
@@ -377,18 +377,22 @@ int launch_welch_t(msd_welch_plan *p, const void *x, const int64_t *off, const i
         A.band_slot0[j] = slot;
         if (c.band_hi[j] >= c.band_lo[j]) slot += c.band_hi[j] - c.band_lo[j] + 1;
     }
-    const size_t lds = sizeof(double) * (WL_THREADS / 64) * (size_t)A.wave_lds;
-    if (lds > 160 * 1024) return fail(MSD_ERR_UNSUPPORTED, "welch: nperseg + band bins exceed the LDS budget");
+    // waves per workgroup: 4 unless one wave's segment + PSD buffer needs more of the LDS
+    // (e.g. nperseg 4096 with a full 2049-bin PSD: 3)
+    const size_t wave_bytes = sizeof(double) * (size_t)A.wave_lds;
+    const int nw = (int)std::min<size_t>(WL_THREADS / 64, (160 * 1024) / wave_bytes);
+    if (nw < 1) return fail(MSD_ERR_UNSUPPORTED, "welch: nperseg + band bins exceed the LDS budget");
+    const size_t lds = wave_bytes * nw;
     static bool attr = false;
     if (!attr) {
         MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(welch_bands_kernel<T>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
-    const int64_t grid = (nfiles * max_blocks + WL_THREADS / 64 - 1) / (WL_THREADS / 64);  // a wave per block
+    const int64_t grid = (nfiles * max_blocks + nw - 1) / nw;  // a wave per block
     if (grid > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "welch: grid too large");
     KernelTimer timer(p->ctx, K_WELCH);
-    hipLaunchKernelGGL(welch_bands_kernel<T>, dim3((unsigned)grid), dim3(WL_THREADS), lds, p->ctx->stream,
+    hipLaunchKernelGGL(welch_bands_kernel<T>, dim3((unsigned)grid), dim3(64 * nw), lds, p->ctx->stream,
                        static_cast<const T *>(x), off, len, A, p->d_window, p->d_bins, band_db, psd);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
@@ -515,6 +519,36 @@ int msd_welch_bands(msd_welch_plan *p, const void *x, int dtype, int64_t n, doub
     rc = launch_welch(p, dx, dtype, doff, doff + 1, 1, nb, static_cast<double *>(dout), nb, nullptr);
     if (rc) return rc;
     MSD_HIP(hipMemcpyAsync(band_db, dout, sizeof(double) * nbands * nb, hipMemcpyDeviceToHost, ctx->stream));
+    MSD_HIP(hipStreamSynchronize(ctx->stream));
+    return MSD_OK;
+}
+
+int msd_welch_psd(msd_welch_plan *p, const void *x, int dtype, int64_t n, double *psd, int64_t *blocks) {
+    if (!p || (!x && n) || !psd) return fail(MSD_ERR_INVALID, "msd_welch_psd: null");
+    const size_t es = dtype_size(dtype);
+    if (!es) return fail(MSD_ERR_INVALID, "msd_welch_psd: unknown dtype");
+    const int64_t B = p->cfg.block_size;
+    const int64_t nb = n >= B ? (n - B) / B + 1 : 0;
+    if (blocks) *blocks = nb;
+    if (nb == 0) return MSD_OK;
+    msd_ctx *ctx = p->ctx;
+    DeviceGuard g(ctx->device);
+    void *dx, *dmeta, *dout;
+    int rc;
+    const int nbands = p->cfg.nbands;
+    const size_t band_bytes = sizeof(double) * nbands * nb, psd_bytes = sizeof(double) * (size_t)p->nslots * nb;
+    if ((rc = ctx_scratch(ctx, 0, ((size_t)n * es + 255) / 256 * 256, &dx))) return rc;
+    if ((rc = ctx_scratch(ctx, 1, 64, &dmeta))) return rc;
+    if ((rc = ctx_scratch(ctx, 2, band_bytes + psd_bytes, &dout))) return rc;
+    int64_t meta[2] = {0, n};
+    MSD_HIP(hipMemcpyAsync(dx, x, (size_t)n * es, hipMemcpyHostToDevice, ctx->stream));
+    MSD_HIP(hipMemcpyAsync(dmeta, meta, sizeof(meta), hipMemcpyHostToDevice, ctx->stream));
+    const int64_t *doff = static_cast<const int64_t *>(dmeta);
+    double *dband = static_cast<double *>(dout);
+    double *dpsd = reinterpret_cast<double *>(static_cast<char *>(dout) + band_bytes);
+    rc = launch_welch(p, dx, dtype, doff, doff + 1, 1, nb, dband, nb, dpsd);
+    if (rc) return rc;
+    MSD_HIP(hipMemcpyAsync(psd, dpsd, psd_bytes, hipMemcpyDeviceToHost, ctx->stream));
     MSD_HIP(hipStreamSynchronize(ctx->stream));
     return MSD_OK;
 }

@@ -173,6 +173,7 @@ _SIGS = [
     ("msd_welch_plan_destroy", None, [_P]),
     ("msd_welch_bands_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64, _P]),
     ("msd_welch_bands", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
+    ("msd_welch_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
     ("msd_live_detect_dev", C.c_int,
      [_P, _P, _P, C.c_int64, C.c_int64, C.POINTER(MsdLiveCfg), _P, C.c_int64, _P, _P, _P, _P]),
     ("msd_live_detect", C.c_int,
@@ -466,6 +467,16 @@ class WelchPlan:
         got = C.c_int64(0)
         check(self.ctx.lib.msd_welch_bands(self.h, ptr(x), dtype_code(x.dtype), int(x.shape[0]), ptr(out),
                                            C.byref(got)))
+        return out
+
+    def psd(self, x: np.ndarray, nslots: int) -> np.ndarray:
+        """[nb][nslots] per-block PSD of the band bins (host buffers)."""
+        x = np.ascontiguousarray(x)
+        nb = self.blocks(x.shape[0])
+        out = np.empty((nb, nslots), np.float64)
+        got = C.c_int64(0)
+        check(self.ctx.lib.msd_welch_psd(self.h, ptr(x), dtype_code(x.dtype), int(x.shape[0]), ptr(out),
+                                         C.byref(got)))
         return out
 
     def run_dev(self, x: DeviceBuffer, dtype, off: DeviceBuffer, length: DeviceBuffer, nfiles: int,

@@ -10,9 +10,10 @@ work runs on the GPU through libmsdsp (no CPU fallback).  Lower-level pieces:
 * ``write_csv`` / ``write_audacity_labels`` — main.py:640-658 / 630-638
 * ``count_per_hour`` — main.py:687-696 (Counter over utc_start hours)
 
-Deliberately not implemented: the matplotlib / plotly figures (debug_plot_*,
-the per-detection spectrogram export) — SURVEY §8(f) row 4; asking for them
-raises ``NotImplementedError`` rather than silently skipping.
+The per-detection spectrogram + PSD export (``disable_show_and_write=False``,
+main.py:721-806) draws GPU arrays with matplotlib (``figures.py``).  Not implemented:
+the whole-file debug figures (``debug_plot_*``); asking for them raises
+``NotImplementedError`` rather than silently skipping.
 """
 from __future__ import annotations
 
@@ -285,16 +286,18 @@ def proc_wav_file(file_path,
     if outfile_path is not None:
         assert os.path.exists(os.path.dirname(outfile_path)), \
             f"Output directory does not exist: {os.path.dirname(outfile_path)}"
+        now = datetime.datetime.now()  # main.py:235-237: a fresh timestamped export directory
+        outfile_path = f"{outfile_path}/{now.strftime('%Y%m%d_%H%M%S')}/"
+        os.makedirs(outfile_path, exist_ok=False)
     if out_audacity_lbl_file is not None:
         assert os.path.exists(os.path.dirname(out_audacity_lbl_file)), \
             f"Output directory does not exist: {os.path.dirname(out_audacity_lbl_file)}"
     if out_csv_file is not None:
         assert os.path.exists(os.path.dirname(out_csv_file)), \
             f"Output directory does not exist: {os.path.dirname(out_csv_file)}"
-    if debug_plot_whole or debug_plot_config or debug_plot_output or debug_plot_output_interactive \
-            or not disable_show_and_write:
-        raise NotImplementedError("plots / per-detection figure export are not part of the GPU drop-in; "
-                                  "pass disable_show_and_write=True and leave debug_plot_* False")
+    if debug_plot_whole or debug_plot_config or debug_plot_output or debug_plot_output_interactive:
+        raise NotImplementedError("the debug_plot_* figures are not part of the GPU drop-in "
+                                  "(the per-detection export, disable_show_and_write=False, is)")
 
     wav_sample_rate, wav_data = wav.read(file_path)
 
@@ -334,6 +337,9 @@ def proc_wav_file(file_path,
     if out_csv_file is not None:
         write_csv(res.detections, out_csv_file)
         say("Wrote Items", len(res.detections), "to CSV file:", out_csv_file)
+    if not disable_show_and_write:  # main.py:721-806: per-detection spectrogram + PSD figures
+        from .figures import export_detections
+        export_detections(res.detections, wav_data, wav_sample_rate, freq_band, outfile_path, device=device)
     return res
 
 

@@ -288,3 +288,32 @@ class LiveBatch:
         out = np.empty((self.nfiles, self.ld), np.float64)
         self.d_thr.download(out)
         return out[:, : self.nb]
+
+
+def welch_psd(x, fs, nperseg=256, noverlap=None, nfft=None, sample_scale: float = 1.0, device: int = 0):
+    """scipy.signal.welch(x, fs, window='hann', nperseg, noverlap, nfft, scaling='density') over a
+    whole 1-D signal on the GPU (float64 arithmetic): returns (f, Pxx[nfft//2 + 1]).  As scipy
+    does, nperseg is capped at len(x)."""
+    x = np.ascontiguousarray(x)
+    n = x.shape[0]
+    if n == 0:
+        return np.empty(0), np.empty(0)
+    nperseg = min(int(nperseg), n)
+    noverlap = nperseg // 2 if noverlap is None else int(noverlap)
+    nfft = nperseg if nfft is None else int(nfft)
+    if nfft < nperseg:
+        raise ValueError("nfft must be greater than or equal to nperseg.")
+    win = hann_periodic(nperseg)
+    wc = win.astype(np.complex128)
+    c = _lib.MsdWelchCfg()
+    c.block_size, c.nperseg, c.noverlap, c.nfft = n, nperseg, noverlap, nfft
+    c.sample_scale = float(sample_scale)
+    c.scale = float(np.real(1.0 / (fs * (wc * wc).sum())))
+    c.nbands = 1
+    c.band_lo[0], c.band_hi[0] = 0, nfft // 2
+    plan = _lib.WelchPlan(context(device), c, win)
+    try:
+        P = plan.psd(x if x.dtype != np.uint8 else x.astype(np.int16) - 128, nfft // 2 + 1)[0]
+    finally:
+        plan.close()
+    return np.fft.rfftfreq(nfft, 1 / fs), P

@@ -167,3 +167,36 @@ def test_state_machine_long_rows_cross_chunks(live):
     got = [(a.time_start, a.time_stop, a.db_min, a.db_max, a.db_mean, a.db_std) for a in m]
     assert got == [(b.time_start, b.time_stop, b.db_min, b.db_max, b.db_mean, b.db_std) for b in rm]
     assert any(2040 * 0.2 <= a.time_start <= 2050 * 0.2 for a in m)
+
+
+@pytest.mark.parametrize("n,nperseg", [(48000, 4096), (3000, 4096), (20000, 256)])
+def test_welch_psd_whole_signal_vs_scipy(live, n, nperseg):
+    """live.welch_psd = scipy.signal.welch(x, fs, 'hann', nperseg, nperseg//2, nfft) over a whole
+    float64 signal (the figure export's PSD panel, main.py:88-90); nperseg capped at len(x)."""
+    import warnings
+    from scipy.signal import welch
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n) * 0.1 + 0.5 * np.sin(2 * np.pi * 1000 * np.arange(n) / 6000)
+    f, P = live.welch_psd(x, 6000, nperseg=nperseg, noverlap=nperseg // 2, nfft=nperseg)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        rf, rP = welch(x, 6000, window="hann", nperseg=nperseg, noverlap=nperseg // 2, nfft=nperseg)
+    np.testing.assert_array_equal(f, rf)
+    assert np.linalg.norm(P - rP) <= 1e-9 * np.linalg.norm(rP)
+
+
+def test_proc_wav_file_exports_detection_figures(tmp_path):
+    """disable_show_and_write=False (main.py:721-806): one spec_and_psd PNG per detection in a
+    fresh timestamped directory under outfile_path."""
+    from meteorgpu import dsp, synth, wav
+    x, _ = synth.synth_real(seed=5, fs=6000, duration_s=60.0, f0=1003.0, rate_per_min=10, band_hz=20.0,
+                            snr_db=(20, 35))
+    p = tmp_path / "a.wav"
+    wav.write(p, 6000, x)
+    out = tmp_path / "spec_export"
+    out.mkdir()
+    res = dsp.proc_wav_file(str(p), 0.2, (993, 1013), (690, 710), 512, 4, outfile_path=str(out) + "/x",
+                            disable_show_and_write=False, verbose=False)
+    pngs = sorted(out.glob("x/*/spec_and_psd_*.png"))
+    assert len(res.detections) > 0 and len(pngs) == len(res.detections)
+    assert all(q.stat().st_size > 10000 for q in pngs)
