@@ -194,7 +194,7 @@ __device__ __forceinline__ void load_pair(const T *__restrict__ x, const FileCur
     }
 }
 
-template <typename T, int MODE>  // MODE: 0 [K][T] out; experiments: 1 frame-major, 2 no store, 3 L2-resident store
+template <typename T, int WIDE>  // WIDE: 64-bit output offsets (files of 2^21 frames and more)
 __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len,
     int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float wscale, int detrend,
@@ -251,29 +251,22 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     // transform and the prefetched samples waited for at the top of the loop are never younger
     // than a tile's stores.
     auto write_out = [&](const FileCur &wc) {
-        if constexpr (MODE == 2) {
-        } else if constexpr (MODE == 1) {  // experiment: frame-major tile, 65.7 KB contiguous
-            float *of = out + ((wc.f * tiles_per_file + wc.ti) * (int64_t)F_TT) * F_K;
-            for (int o = tid; o < F_TT * F_K; o += F_NW * 64) {
-                const int c = o / F_K, k = o - c * F_K;
-                of[o] = tile[k * F_PITCH + c];
-            }
-        } else {
-            // scalar base + 32-bit lane offsets (k*ld*4 < 2^32 for ld < 2^21); 8 lanes x 16 B
-            // per row: two 8-B LDS reads (pitch 34 keeps rows 8-B aligned) → one 16-B store
-            char *of = MODE == 3 ? reinterpret_cast<char *>(out + blockIdx.x * F_TT)  // experiment: L2-resident
-                                 : reinterpret_cast<char *>(out + wc.f * (int64_t)F_K * ld + wc.ti * F_TT);
-            const int qq = tid & 7;
-            const uint32_t ldb = (uint32_t)ld * 4u;
+        // scalar base + lane offsets, 8 lanes x 16 B per row: two 8-B LDS reads (pitch 34 keeps
+        // rows 8-B aligned) → one 16-B store.  WIDE = 0: 32-bit offsets (K*ld*4 < 2^32, i.e.
+        // ld < 2^21 frames); WIDE = 1: 64-bit (longer files)
+        char *of = reinterpret_cast<char *>(out + wc.f * (int64_t)F_K * ld + wc.ti * F_TT);
+        const int qq = tid & 7;
 #pragma unroll
-            for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 8) {
-                const int k = k0 + (tid >> 3);
-                if (k < F_K) {
-                    const float2 a = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq]);
-                    const float2 b = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq + 2]);
-                    *reinterpret_cast<float4 *>(of + ((uint32_t)k * ldb + 16u * (uint32_t)qq)) =
-                        make_float4(a.x, a.y, b.x, b.y);
-                }
+        for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 8) {
+            const int k = k0 + (tid >> 3);
+            if (k < F_K) {
+                const float2 a = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq]);
+                const float2 b = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq + 2]);
+                const float4 v = make_float4(a.x, a.y, b.x, b.y);
+                if constexpr (WIDE)
+                    *reinterpret_cast<float4 *>(of + ((int64_t)k * ld * 4 + 16 * qq)) = v;
+                else
+                    *reinterpret_cast<float4 *>(of + ((uint32_t)k * ((uint32_t)ld * 4u) + 16u * (uint32_t)qq)) = v;
             }
         }
     };
@@ -429,14 +422,13 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 template <typename T>
 int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int64_t *len, int64_t nfiles, float *out,
                   int64_t ld) {
-    static const int mode = getenv("MSD_EXP_TMAJOR") ? 1 : getenv("MSD_EXP_NOSTORE") ? 2 : getenv("MSD_EXP_L2STORE") ? 3 : 0;
-    auto kern = mode == 1   ? stft1024_kernel<T, 1>
-                : mode == 2 ? stft1024_kernel<T, 2>
-                : mode == 3 ? stft1024_kernel<T, 3>
-                            : stft1024_kernel<T, 0>;
+    const bool wide = (uint64_t)F_K * (uint64_t)ld * 4u >= (1ull << 32);
+    auto kern = wide ? stft1024_kernel<T, 1> : stft1024_kernel<T, 0>;
     static bool attr_set = false;
     if (!attr_set) {
-        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(stft1024_kernel<T, 0>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
+        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(stft1024_kernel<T, 1>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
         attr_set = true;
     }

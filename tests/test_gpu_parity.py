@@ -423,3 +423,32 @@ def test_ragged_batch_through_the_c_abi(nperseg):
         rdets, _ = O.get_detections_adaptive_ref(d, 4.0, 0.2)
         assert [(int(a["start"]), int(a["stop"]), float(a["db"])) for a in dets[i, :cnt[i]]] == \
                [(int(round(r[0] / 0.2)), int(round(r[1] / 0.2)), r[3]) for r in rdets]
+
+
+def test_stft_fast_path_wide_row_stride():
+    """Rows of 2^21 frames and more (a > 6 h 48 kHz file): the N = 1024 kernel switches to 64-bit
+    output offsets.  Exercised with a short signal and a padded row stride ld >= 2^21."""
+    ctx = dsp.context(0)
+    fs = 48000
+    x, _ = synth.synth_real(seed=9, fs=fs, duration_s=3.0, f0=1000.0)
+    w = dsp.hann_periodic(1024).astype(np.complex64)
+    scale = float(np.real(1.0 / (fs * (w * w).sum())))
+    plan = _lib.StftPlan(ctx, 1024, 512, w.real.astype(np.float32), scale)
+    T = plan.frames(len(x))
+    ld = (1 << 21) + 32
+    d_x = ctx.alloc(x.nbytes)
+    d_x.upload(x)
+    d_off, d_len = ctx.alloc(8), ctx.alloc(8)
+    d_off.upload(np.zeros(1, np.int64))
+    d_len.upload(np.array([len(x)], np.int64))
+    d_spec = ctx.alloc(513 * ld * 4)
+    plan.run_dev(d_x, np.int16, d_off, d_len, 1, T, d_spec, ld)
+    _, _, S = dsp.spectrogram(x, fs=fs, nperseg=1024, noverlap=512)
+    row = np.empty(T + 32, np.float32)
+    for k in (0, 1, 255, 511, 512):
+        d_spec.download(row, byte_offset=k * ld * 4)
+        np.testing.assert_array_equal(row[:T], S[k])
+        assert not row[T:].any()
+    tail = np.empty(64, np.float32)
+    d_spec.download(tail, byte_offset=(512 * ld + ld - 64) * 4)
+    assert not tail.any()
