@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--files", type=int, default=1440, help="one-minute files per GPU")
     ap.add_argument("--cpu-files", type=int, default=150, help="files in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=16, help="processes of the multi-core CPU baseline "
+                    "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
     ap.add_argument("--workload", choices=("c3", "live", "c5", "files"), default="c3",
                     help="c3: the headline day batch (default); live: the phase-2 live detector "
@@ -65,6 +67,43 @@ def cpu_baseline(pool, nfiles):
         O.proc_samples_ref(x, FS, 0.2, BAND, NOISE, 512, 4)
     dt = time.perf_counter() - t0
     return nfiles * FS * SECONDS / dt / 1e6, dt
+
+
+_MP_POOL = None
+
+
+def _mp_one(i):
+    from oracle import dsp_oracle as O
+    x = _MP_POOL[i % len(_MP_POOL)]
+    O.spectrogram_ref(x, FS, NPERSEG)
+    O.proc_samples_ref(x, FS, 0.2, BAND, NOISE, 512, 4)
+    return 0
+
+
+def cpu_baseline_mp(pool, nfiles, procs):
+    """The same CPU path over `nfiles` files on `procs` worker processes.
+    Forked before the GPU is touched (bench.py calls it first), one file per task."""
+    import multiprocessing as mp
+    global _MP_POOL
+    _MP_POOL = pool
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as workers:
+        workers.map(_mp_one, range(min(procs, nfiles)))  # warm the workers (imports)
+        t0 = time.perf_counter()
+        workers.map(_mp_one, range(nfiles), chunksize=1)
+        dt = time.perf_counter() - t0
+    return nfiles * FS * SECONDS / dt / 1e6, dt
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_pmc_traffic(nfiles):
@@ -323,12 +362,20 @@ def main():
     from meteorgpu import _lib, synth
     from meteorgpu.batch import BatchPipeline, Communicator
 
+    pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
+    mp_base = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
+        # before any GPU call: the workers are forked from this process
+        mp_files = a.cpu_files * a.cpu_procs // 4
+        v, dt = cpu_baseline_mp(pool, mp_files, a.cpu_procs)
+        mp_base = {"value": round(v, 2), "unit": "Msamples/s", "cores": a.cpu_procs, "kind": "port",
+                   "sample": f"{mp_files} of the 60 s 48 kHz files on {a.cpu_procs} processes ({dt:.1f} s), "
+                             f"same path as cpu_baseline; CPU: {cpu_model()}"}
     ctx = _lib.Context(local)
     n = FS * SECONDS
     F = a.files
     bp = BatchPipeline(ctx, F, n, FS, nperseg=NPERSEG, noverlap=NOVERLAP, freq_band=BAND, noise_band=NOISE,
                        with_spectrogram=not a.no_spectrogram)
-    pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
     for i in range(F):
         bp.upload_file(i, pool[(i + rank) % POOL])
     # rank r holds day r: file i starts at minute i of 2025-06-(1+r) 00:00 UTC
@@ -444,6 +491,8 @@ def main():
             "sample": f"{a.cpu_files} of the 60 s 48 kHz files ({dt:.1f} s): scipy.signal.spectrogram "
                       f"1024/512 + main.py block loop + adaptive detector (oracle/), 1 thread",
         }
+    if mp_base is not None:
+        out["cpu_baseline_multicore"] = mp_base
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
