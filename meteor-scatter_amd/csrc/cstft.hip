@@ -209,7 +209,8 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
             for (int k2b = 0; k2b < 16; ++k2b)
                 of[tid + 256 * k2b] = valid ? v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y : 0.f;
         }
-        __syncthreads();  // buf and red are reused by the next frame
+        // no barrier here: the next frame writes buf / red only after its first barrier, which
+        // every wave reaches after its pass-3 reads of this frame
         cur = nxt;
     }
 }
