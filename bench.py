@@ -200,7 +200,7 @@ def main_live(a, world, rank, local, dist):
                      "algorithmic_flops_per_launch": flops},
         "kernel_ms_per_step": {"welch": round(avg_s * 1e3, 4), "live_detect": round(l_ms / max(l_n, 1), 4)},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
+    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0:
         secs = 1800
         v, dt = cpu_baseline_live(pool, secs)
         out["cpu_baseline"] = {"value": round(v, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
@@ -281,7 +281,7 @@ def main_c5(a, world, rank, local, dist):
                      "kernel": "cstft4096_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
+    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0:
         from oracle import iq_oracle as Q
         m = C5_FS * 60  # one minute of the stream
         z = pool[0]
@@ -348,7 +348,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # MSD_BENCH_FORCE_DIST=1 takes the N>1 path (nccl process group + RCCL communicator) at
+    # world size 1, so the distributed code runs on a one-GPU box too
+    use_dist = world > 1 or os.environ.get("MSD_BENCH_FORCE_DIST", "0") not in ("", "0")
+    if use_dist:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -364,7 +367,7 @@ def main():
 
     pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
     mp_base = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
+    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
         # before any GPU call: the workers are forked from this process
         mp_files = a.cpu_files * a.cpu_procs // 4
         v, dt = cpu_baseline_mp(pool, mp_files, a.cpu_procs)
@@ -385,7 +388,7 @@ def main():
     bp.set_start_times(np.array([us(day0 + datetime.timedelta(minutes=i)) for i in range(F)], np.int64),
                        us(day0))
     comm = None
-    if world > 1:
+    if dist is not None:
         obj = [Communicator.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = Communicator(ctx, world, obj[0], rank)
@@ -428,7 +431,7 @@ def main():
     else:
         total_dets = int(counts.sum())
     hist = bp.hour_counts()
-    assert int(hist.sum()) == total_dets * (1 if world == 1 else 1), "hour histogram != detections"
+    assert int(hist.sum()) == total_dets, "hour histogram != detections"
     stft_ms, stft_launches = ctx.timing_get(_lib.K_STFT)
     blk_ms, blk_launches = ctx.timing_get(_lib.K_BLOCK)
     det_ms, det_launches = ctx.timing_get(_lib.K_DSCAN)
@@ -481,7 +484,7 @@ def main():
         "block_delta": round(blk_ms / max(blk_launches, 1), 4),
         "detect": round(det_ms / max(det_launches, 1), 4),
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
+    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0:
         v, dt = cpu_baseline(pool, a.cpu_files)
         out["cpu_baseline"] = {
             "value": round(v, 2),
