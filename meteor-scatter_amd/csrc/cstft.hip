@@ -17,6 +17,7 @@
 // K = 4096 would need 512 KB of LDS per 128-B row segment; scipy's [K][T] is the transpose of
 // this layout.)  The window carries sqrt(scale), so |X|^2 is the density directly.
 #include <cmath>
+#include <type_traits>
 
 #include "msd_internal.h"
 
@@ -98,13 +99,11 @@ struct IQ<float> {  // interleaved float32 I, Q (complex64)
     __device__ static float acc_im(raw_t r) { return r.y; }
 };
 
-struct StreamCur {
-    int64_t s, t;    // stream, frame
-    int64_t nfr;     // frames in the stream
-    int64_t base;    // element offset (complex samples) of the stream
-};
-
-template <typename T>
+// SH = hop / 256 when the hop is a multiple of 256 below N (C5: hop 1024 → 4), else 0.
+// Thread j holds z[j + 256 r]; the next frame of the same stream needs z[j + 256 (r + SH)],
+// so with SH > 0 it keeps raw[SH..15] (shifted down) and loads only raw[16-SH..15]: each
+// sample is loaded once per workgroup instead of N / hop times.
+template <typename T, int SH>
 __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x, const int64_t *__restrict__ off,
                                                          const int64_t *__restrict__ len, int64_t nstreams,
                                                          int64_t max_frames, int64_t total, int64_t per, int hop,
@@ -131,87 +130,106 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
 
     const int64_t g0 = (int64_t)blockIdx.x * per;
     const int64_t g1 = g0 + per < total ? g0 + per : total;
-    if (g0 >= g1) return;
-    auto cur_at = [&](int64_t g) {
-        StreamCur c;
-        c.s = g / max_frames;
-        c.t = g - c.s * max_frames;
-        const int64_t n = len[c.s];
-        c.nfr = n >= CS_N ? (n - CS_N) / hop + 1 : 0;
-        c.base = off[c.s];
-        return c;
-    };
-    auto load = [&](const StreamCur &c, typename io::raw_t (&raw)[16]) {
-        if (c.t < c.nfr) {
-            const T *p = x + 2 * (c.base + c.t * (int64_t)hop);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) raw[r] = io::load(p + 2 * (tid + 256 * r));
-        }
-    };
     typename io::raw_t raw[16];
-    StreamCur cur = cur_at(g0);
-    load(cur, raw);
-    for (int64_t g = g0; g < g1; ++g) {
-        const StreamCur nxt = g + 1 < g1 ? cur_at(g + 1) : cur;
-        const bool valid = cur.t < cur.nfr;  // uniform
-        float2 v[16];
-        // ---- detrend: the frame's complex mean (scipy 'constant'): exact integer sums for
-        // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; wave DPP-free xor shuffles,
-        // then one LDS slot per wave
-        typename io::acc_t sr = 0, si = 0;
+    // load rows [R0, 16) of frame t of the stream at element offset `base`
+    auto load_rows = [&](int64_t base, int64_t t, auto r0c) {
+        constexpr int R0 = decltype(r0c)::value;
+        const T *p = x + 2 * (base + t * (int64_t)hop);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            v[r] = io::f(raw[r]);
-            sr += io::acc_re(raw[r]);
-            si += io::acc_im(raw[r]);
+        for (int r = R0; r < 16; ++r) raw[r] = io::load(p + 2 * (tid + 256 * r));
+    };
+    // The workgroup's frames, split at stream boundaries: per segment, the frames of the stream
+    // [ga, gv) and then the frames past its end [gv, gb), written as zeros.  Within [ga, gv) the
+    // prefetch of frame t + 1 is unconditional (clamped to the last frame at the end), so the
+    // register rows never pass through data-dependent copies.
+    for (int64_t ga = g0; ga < g1;) {
+        const int64_t s = ga / max_frames;
+        const int64_t gb = (s + 1) * max_frames < g1 ? (s + 1) * max_frames : g1;
+        const int64_t n = len[s];
+        const int64_t nfr = n >= CS_N ? (n - CS_N) / hop + 1 : 0;
+        const int64_t ge = s * max_frames + nfr;  // end of the stream's frames
+        const int64_t gv = ge < ga ? ga : ge > gb ? gb : ge;
+        const int64_t base = off[s];
+        float *of = out + ga * (int64_t)CS_N;
+        // one frame: consumes raw (frame g), prefetches frame g + 1 into raw, writes `of`
+        auto frame = [&](int64_t g, float *of) __attribute__((always_inline)) {
+            float2 v[16];
+            // ---- detrend: the frame's complex mean (scipy 'constant'): exact integer sums for
+            // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; wave xor shuffles, then one
+            // LDS slot per wave
+            typename io::acc_t sr = 0, si = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                v[r] = io::f(raw[r]);
+                sr += io::acc_re(raw[r]);
+                si += io::acc_im(raw[r]);
+            }
+            for (int o = 32; o >= 1; o >>= 1) {
+                sr += __shfl_xor(sr, o, 64);
+                si += __shfl_xor(si, o, 64);
+            }
+            if (lane == 0) {
+                red[0][wave] = (double)sr;
+                red[1][wave] = (double)si;
+            }
+            {  // prefetch frame t + 1 (raw is consumed); the segment's last frame reloads itself
+                const int64_t tn = (g + 1 < gv ? g + 1 : g) - s * max_frames;
+                if constexpr (SH > 0) {  // (after the segment's last frame raw is dead)
+#pragma unroll
+                    for (int r = 0; r < 16 - SH; ++r) raw[r] = raw[r + SH];
+                    load_rows(base, tn, std::integral_constant<int, (SH > 0 ? 16 - SH : 0)>{});
+                } else {
+                    load_rows(base, tn, std::integral_constant<int, 0>{});
+                }
+            }
+            lds_barrier();
+            float mr = 0.f, mi = 0.f;
+            if (detrend) {
+                mr = (float)((red[0][0] + red[0][1] + red[0][2] + red[0][3]) * (1.0 / CS_N));
+                mi = (float)((red[1][0] + red[1][1] + red[1][2] + red[1][3]) * (1.0 / CS_N));
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = make_float2((v[r].x - mr) * wr[r], (v[r].y - mi) * wr[r]);
+            // ---- pass 1: DFT over r, twiddle W4096^(j q), y[q][j]
+            dft16(v);
+#pragma unroll
+            for (int q = 1; q < 16; ++q) v[q] = c_mul(v[q], tw1[q]);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) buf[q * CS_P + tid] = v[q];
+            lds_barrier();
+            // ---- pass 2: thread (q, j1): DFT over j2 of y[q][j1 + 16 j2], twiddle W256^(j1 k2a)
+#pragma unroll
+            for (int j2 = 0; j2 < 16; ++j2) v[j2] = buf[q2 * CS_P + j1 + 16 * j2];
+            dft16(v);
+#pragma unroll
+            for (int k = 1; k < 16; ++k) v[k] = c_mul(v[k], tw256[(j1 * k) & 255]);
+            lds_barrier();  // everyone has read pass 1's layout
+#pragma unroll
+            for (int k = 0; k < 16; ++k) buf[(16 * k + j1) * 17 + q2] = v[k];  // u[q][k2a][j1], column-major
+            lds_barrier();
+            // ---- pass 3: thread t = q + 16 k2a: DFT over j1 → X[t + 256 k2b]
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = buf[(16 * k2a + j) * 17 + q3];
+            dft16(v);
+#pragma unroll
+            for (int k2b = 0; k2b < 16; ++k2b) of[tid + 256 * k2b] = v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y;
+            // no barrier at the end: the next frame writes buf / red only after its first
+            // barrier, which every wave reaches after its pass-3 reads of this frame
+        };
+        // The first frame is peeled off the loop: both ways into the loop then end with the
+        // prefetch loads followed by this frame's 16 stores, so the compiler's wait for the
+        // prefetched rows is vmcnt(16) — it never waits for the stores (gfx9 counts loads and
+        // stores in one vmcnt; a loop entered straight after a load would wait vmcnt(0)).
+        if (ga < gv) {
+            load_rows(base, ga - s * max_frames, std::integral_constant<int, 0>{});
+            frame(ga, of);
+            of += CS_N;
+            for (int64_t g = ga + 1; g < gv; ++g, of += CS_N) frame(g, of);
         }
-        for (int o = 32; o >= 1; o >>= 1) {
-            sr += __shfl_xor(sr, o, 64);
-            si += __shfl_xor(si, o, 64);
-        }
-        if (lane == 0) {
-            red[0][wave] = (double)sr;
-            red[1][wave] = (double)si;
-        }
-        if (g + 1 < g1) load(nxt, raw);  // prefetch the next frame (raw is consumed)
-        __syncthreads();
-        float mr = 0.f, mi = 0.f;
-        if (detrend) {
-            mr = (float)((red[0][0] + red[0][1] + red[0][2] + red[0][3]) * (1.0 / CS_N));
-            mi = (float)((red[1][0] + red[1][1] + red[1][2] + red[1][3]) * (1.0 / CS_N));
-        }
+        for (int64_t g = gv; g < gb; ++g, of += CS_N)  // frames past a shorter stream's end
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = make_float2((v[r].x - mr) * wr[r], (v[r].y - mi) * wr[r]);
-        // ---- pass 1: DFT over r, twiddle W4096^(j q), y[q][j]
-        dft16(v);
-#pragma unroll
-        for (int q = 1; q < 16; ++q) v[q] = c_mul(v[q], tw1[q]);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) buf[q * CS_P + tid] = v[q];
-        __syncthreads();
-        // ---- pass 2: thread (q, j1): DFT over j2 of y[q][j1 + 16 j2], twiddle W256^(j1 k2a)
-#pragma unroll
-        for (int j2 = 0; j2 < 16; ++j2) v[j2] = buf[q2 * CS_P + j1 + 16 * j2];
-        dft16(v);
-#pragma unroll
-        for (int k = 1; k < 16; ++k) v[k] = c_mul(v[k], tw256[(j1 * k) & 255]);
-        __syncthreads();  // everyone has read pass 1's layout
-#pragma unroll
-        for (int k = 0; k < 16; ++k) buf[(16 * k + j1) * 17 + q2] = v[k];  // u[q][k2a][j1], column-major
-        __syncthreads();
-        // ---- pass 3: thread t = q + 16 k2a: DFT over j1 → X[t + 256 k2b]
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = buf[(16 * k2a + j) * 17 + q3];
-        dft16(v);
-        {  // frames past a stream's end (shorter streams in a batch) are written as zeros
-            float *of = out + (cur.s * max_frames + cur.t) * (int64_t)CS_N;
-#pragma unroll
-            for (int k2b = 0; k2b < 16; ++k2b)
-                of[tid + 256 * k2b] = valid ? v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y : 0.f;
-        }
-        // no barrier here: the next frame writes buf / red only after its first barrier, which
-        // every wave reaches after its pass-3 reads of this frame
-        cur = nxt;
+            for (int k2b = 0; k2b < 16; ++k2b) of[tid + 256 * k2b] = 0.f;
+        ga = gb;
     }
 }
 
@@ -293,14 +311,22 @@ int msd_cstft_psd_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t
     const int64_t per = (total + wgs - 1) / wgs;
     wgs = (total + per - 1) / per;
     KernelTimer timer(p->ctx, K_CSTFT);
-    if (dtype == MSD_CI16)
-        hipLaunchKernelGGL(cstft4096_kernel<int16_t>, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream,
-                           static_cast<const int16_t *>(x), off, len, nstreams, max_frames, total, per, p->hop,
-                           p->detrend, p->d_win, p->d_tw, out);
-    else
-        hipLaunchKernelGGL(cstft4096_kernel<float>, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream,
-                           static_cast<const float *>(x), off, len, nstreams, max_frames, total, per, p->hop,
-                           p->detrend, p->d_win, p->d_tw, out);
+    auto launch = [&](auto kern, const auto *xp) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
+                           max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out);
+    };
+    const int sh = p->hop % 256 == 0 ? p->hop / 256 : 0;
+    if (dtype == MSD_CI16) {
+        const auto *xp = static_cast<const int16_t *>(x);
+        if (sh == 4) launch(cstft4096_kernel<int16_t, 4>, xp);       // 75 % overlap (C5)
+        else if (sh == 8) launch(cstft4096_kernel<int16_t, 8>, xp);  // 50 %
+        else launch(cstft4096_kernel<int16_t, 0>, xp);
+    } else {
+        const auto *xp = static_cast<const float *>(x);
+        if (sh == 4) launch(cstft4096_kernel<float, 4>, xp);
+        else if (sh == 8) launch(cstft4096_kernel<float, 8>, xp);
+        else launch(cstft4096_kernel<float, 0>, xp);
+    }
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }

@@ -83,6 +83,11 @@ struct msd_welch_plan {
 
 namespace msd {
 
+// workgroup barrier that orders LDS only: waits for this wave's LDS accesses, not for its
+// global loads (prefetches) or stores still in flight.  __syncthreads() on gfx9 also waits
+// vmcnt(0), which drains every outstanding prefetch and store at each barrier.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // makes `dev` current for the scope
 struct DeviceGuard {
     int prev = -1;

@@ -103,10 +103,6 @@ __constant__ int8_t k_pass3_lane[64] = {0,  32, 1,  63, 3,  61, 5,  59, 6,  58, 
                                         2,  62, 4,  60, 8,  56, 9,  55, 10, 54, 11, 53, 17, 47, 19, 45,
                                         20, 44, 21, 43, 22, 42, 23, 41, 24, 40, 29, 35, 30, 34, 31, 33};
 
-// workgroup barrier that orders LDS only: waits for this wave's LDS accesses, not for
-// its global stores (the tile write-out) or loads (the prefetch) still in flight
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

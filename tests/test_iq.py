@@ -68,3 +68,42 @@ def test_batch_matches_single():
     for s, x in enumerate(streams):
         _, _, S = iq.spectrogram_iq(x[0::2], x[1::2], 192000, 4096, 3072)
         np.testing.assert_array_equal(b.frames(s, 0, b.T), S.T)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["int16", "float32"])
+@pytest.mark.parametrize("noverlap", [3072, 2048, 3000])
+def test_batch_ragged_persistent(kind, noverlap):
+    """Enough frames that every workgroup runs several consecutive frames (the register shift
+    for hops that are multiples of 256: 3072 → hop 1024, 2048 → hop 2048; 3000 → hop 1096
+    reloads), streams of different lengths in one launch (frames past a stream's end are 0)."""
+    from meteorgpu import iq
+    from meteorgpu.dsp import context
+    rng = np.random.default_rng(noverlap)
+    n = 1_000_000
+    lens = [n, n - 300_001, 4095]  # the last stream has no frame
+    dt = np.int16 if kind == "int16" else np.float32
+    b = iq.IQBatch(context(0), 3, n, 192000, 4096, noverlap, dtype=dt)
+    streams = []
+    for s in range(3):
+        tt = np.arange(n) / 192000
+        z = 4000 * np.exp(2j * np.pi * (1000.0 * (s + 1)) * tt) + 700 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+        if kind == "int16":
+            i, q = np.round(z.real).astype(np.int16), np.round(z.imag).astype(np.int16)
+        else:
+            i, q = (z.real / 32768).astype(np.float32), (z.imag / 32768).astype(np.float32)
+        x = np.empty(2 * n, dt)
+        x[0::2], x[1::2] = i, q
+        b.upload(s, x)
+        streams.append((i[: lens[s]], q[: lens[s]]))
+    b.d_len.upload(np.array(lens, np.int64))
+    b.run()
+    hop = 4096 - noverlap
+    for s, (i, q) in enumerate(streams):
+        got = b.frames(s, 0, b.T)
+        nf = (lens[s] - 4096) // hop + 1 if lens[s] >= 4096 else 0
+        assert not got[nf:].any()
+        if nf:
+            _, _, rS = Q.spectrogram_iq_ref(i, q, 192000, 4096, noverlap)
+            assert rS.shape[1] == nf
+            assert _frame_rel(got[:nf].T.astype(np.float64), rS) < SPEC_TOL
