@@ -86,6 +86,7 @@ struct IQ<int16_t> {  // interleaved int16 I, Q
     __device__ static int im_i(raw_t r) { return (int)(int16_t)(r >> 16); }
     __device__ static float2 f(raw_t r) { return make_float2((float)re_i(r), (float)im_i(r)); }
     using acc_t = int;
+    __device__ static int wave_sum(int v) { return wave_sum_i(v); }
     __device__ static int acc_re(raw_t r) { return re_i(r); }
     __device__ static int acc_im(raw_t r) { return im_i(r); }
 };
@@ -95,6 +96,7 @@ struct IQ<float> {  // interleaved float32 I, Q (complex64)
     __device__ static raw_t load(const float *p) { return *reinterpret_cast<const float2 *>(p); }
     __device__ static float2 f(raw_t r) { return r; }
     using acc_t = float;
+    __device__ static float wave_sum(float v) { return wave_sum_f(v); }
     __device__ static float acc_re(raw_t r) { return r.x; }
     __device__ static float acc_im(raw_t r) { return r.y; }
 };
@@ -155,8 +157,8 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
         auto frame = [&](int64_t g, float *of) __attribute__((always_inline)) {
             float2 v[16];
             // ---- detrend: the frame's complex mean (scipy 'constant'): exact integer sums for
-            // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; wave xor shuffles, then one
-            // LDS slot per wave
+            // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; per wave, then one LDS slot
+            // per wave
             typename io::acc_t sr = 0, si = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -164,10 +166,8 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
                 sr += io::acc_re(raw[r]);
                 si += io::acc_im(raw[r]);
             }
-            for (int o = 32; o >= 1; o >>= 1) {
-                sr += __shfl_xor(sr, o, 64);
-                si += __shfl_xor(si, o, 64);
-            }
+            sr = io::wave_sum(sr);  // DPP row sums + readlane: no LDS round trips
+            si = io::wave_sum(si);
             if (lane == 0) {
                 red[0][wave] = (double)sr;
                 red[1][wave] = (double)si;

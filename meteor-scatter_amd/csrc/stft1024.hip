@@ -109,27 +109,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// DPP: v + v[lane ^ 1], v[lane ^ 2], mirrored half rows, mirrored rows → each lane
-// holds the sum of its row of 16
-__device__ __forceinline__ int row_sum_i(int v) {
-    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
-    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
-    v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true);  // row_half_mirror
-    v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true);  // row_mirror
-    return v;
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xf, 0xf, true));
-}
-__device__ __forceinline__ float row_sum_f(float v) {
-    v += dpp_f<0xB1>(v);
-    v += dpp_f<0x4E>(v);
-    v += dpp_f<0x141>(v);
-    v += dpp_f<0x140>(v);
-    return v;
-}
-
 template <typename T>
 struct PairIO;
 template <>
