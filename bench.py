@@ -106,14 +106,15 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def load_pmc_traffic(nfiles):
-    """HBM bytes per STFT launch from the committed rocprofv3 PMC summary (profiles/), if it
-    was collected for this workload; FETCH_SIZE doubled per the gfx950 rule."""
-    p = os.path.join(ROOT, "profiles", "stft_pmc.json")
+def load_pmc_traffic(name, **match):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
+    profiles/<name>_pmc.json, if it was collected for this workload (the `match` keys agree);
+    FETCH_SIZE doubled per the gfx950 rule."""
+    p = os.path.join(ROOT, "profiles", f"{name}_pmc.json")
     try:
         with open(p) as fh:
             d = json.load(fh)
-        if d.get("files") == nfiles and d.get("nperseg") == NPERSEG:
+        if all(d.get(k) == v for k, v in match.items()):
             return float(d["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         pass
@@ -277,7 +278,8 @@ def main_c5(a, world, rank, local, dist):
                    "samples_per_gpu": samples, "frames_per_gpu": b.T, "bins": C5_N,
                    "parallelism": f"time shards over {world} GPU(s), 1 process per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": load_pmc_traffic("cstft", frames=b.T, nperseg=C5_N),
                      "kernel": "cstft4096_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
     }
@@ -474,7 +476,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_pmc_traffic(F),
+            "traffic": load_pmc_traffic("stft", files=F, nperseg=NPERSEG),
             "kernel": "stft1024_kernel<int16>",
             "kernel_ms": round(avg_s * 1e3, 4),
             "algorithmic_bytes_per_launch": alg_bytes,

@@ -1,6 +1,7 @@
 #!/bin/bash
-# One round's measurements on the GPU box: the default bench line, a rocprofv3 kernel-trace
-# summary of a short bench, and the PMC passes (tools/pmc_stft.sh).  Usage: tools/profile_round.sh TAG
+# One round's measurements on the GPU box: the default bench line, rocprofv3 kernel-trace
+# summaries of short runs of every workload, and the PMC passes over the headline STFT
+# (tools/pmc_stft.sh).  Usage: tools/profile_round.sh TAG
 set -u
 TAG=${1:-r1}
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -10,4 +11,9 @@ timeout -k 10 400 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.er
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- \
     python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/kt.log" 2>&1 || exit 1
-bash "$ROOT/tools/pmc_stft.sh" "$TAG"
+for wl in live c5; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_$wl" -o kt -- \
+      python3 "$ROOT/bench.py" --workload $wl --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/kt_$wl.log" 2>&1 || exit 1
+done
+bash "$ROOT/tools/pmc_stft.sh" "$TAG" || exit 1
+REGEX=cstft bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline
