@@ -75,7 +75,8 @@ int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.
  * kernel id: 0 = STFT power, 1 = block delta, 2 = detector stats, 3 = detector scan,
- * 4 = Welch band powers, 5 = live detector, 6 = complex (I/Q) STFT. */
+ * 4 = Welch band powers, 5 = live detector, 6 = complex (I/Q) STFT, 7 = I/Q band delta,
+ * 8 = stream fresh thresholds, 9 = stream scan. */
 int msd_timing_enable(msd_ctx *ctx, int enable);
 int msd_timing_reset(msd_ctx *ctx);
 int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
@@ -187,6 +188,68 @@ int msd_cstft_psd_dev(msd_cstft_plan *plan, const void *x, int dtype, const int6
                       int64_t nstreams, int64_t max_frames, float *out);
 /* one stream, host buffers: n complex samples in, out float32 [T][N] */
 int msd_cstft_psd(msd_cstft_plan *plan, const void *x, int dtype, int64_t n, float *out, int64_t *frames);
+
+/* -------------------------------- C5: band / noise dB per frame of the I/Q spectrogram
+ * The per-block band energies of dsp/src/main.py:380-393 taken per STFT frame of the two-sided
+ * spectrogram (the frame is the detector's block, block_sec = hop/fs):
+ *   E = sum(Sxx[mask, t]) + 1e-12;  dB = 10*log10(E);  delta = band_dB - noise_dB
+ * with the masks of fftfreq(N, 1/fs) selected as (f >= lo) & (f <= hi).  Bands are inclusive
+ * SIGNED bin ranges [lo, hi] in -N/2 .. N/2-1 (contiguous in frequency; bin b < 0 is column
+ * b + N of the frame-major row); hi < lo = empty band (E = 1e-12).  spec: device float32
+ * [s][max_frames][N] as msd_cstft_psd_dev writes it; frames: device int64 [nstreams];
+ * outputs float64 [s*ld + t] (band_db / noise_db may be NULL).  Sums are float64. */
+int msd_iq_band_delta_dev(msd_ctx *ctx, const float *spec, int64_t nstreams, int64_t max_frames,
+                          const int64_t *frames, int32_t nperseg, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
+                          int32_t noise_hi, double *band_db, double *noise_db, double *delta, int64_t ld);
+
+/* -------------------------- C5: the detector over one long stream, time-sharded over ranks
+ * get_detections_adaptive() (dsp/src/main.py:450-522) and get_detections() (:396-448) over
+ * the delta of ONE stream of n_total frames of which this rank holds [frame0, frame0+n_local).
+ * Bit-exact with the reference's numpy arithmetic (pairwise sums in 8192-element chunks,
+ * mean + k*std rounded as numpy, no FMA).  The whole-stream mean/std, the W-frame look-back
+ * of the adaptive threshold and the freeze/run state at the shard edges are the only things
+ * that cross ranks; the host moves them (meteorgpu/stream.py):
+ *   1. halos: the tail halo holds the min(W, frame0) frames before frame0, the head halo
+ *      the min(head_frames, n_total - frame0 - n_local) frames after the shard;
+ *   2. msd_stream_chunk_sums: the pairwise sums of the 8192-frame chunks (of delta, or of
+ *      (delta - mean)^2) that START in the shard; in chunk order, s = 0.0; s += c gives
+ *      numpy's add.reduce over the whole stream;
+ *   3. msd_stream_fresh: every frame's mean + k*std(delta[max(0, i-W):i]) (state-free);
+ *   4. msd_stream_scan: the freeze/run scan of the shard from the state entering frame0,
+ *      in parallel segments iterated to a fixed point; returns the state after the shard
+ *      (rank r+1 enters with rank r's end state: repeat until no entry state changes);
+ *   5. msd_stream_runs / msd_stream_db: the shard's runs [start, stop) (start = -1: a run
+ *      continued from the previous shard) and their dB means.
+ * cfg->adaptive = 0 gives the global detector (every frame uses thr0; the end quirk of
+ * main.py:414-415 and the assert of :437 are the host's, on the last shard). */
+typedef struct msd_stream_plan msd_stream_plan;
+typedef struct {
+    int64_t freeze_until; /* freeze_until_idx (main.py:455), -1 initially             */
+    int64_t last_stop;    /* last frame of the last run, -2 if there is none           */
+    double thr;           /* the `threshold` variable after the previous frame         */
+    int64_t reserved;
+} msd_stream_state;
+int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total, int64_t frame0, int64_t n_local,
+                           int64_t seg_len, int64_t cap_per_seg, int64_t head_frames, msd_stream_plan **out);
+void msd_stream_plan_destroy(msd_stream_plan *plan);
+/* device pointers into the plan: the shard's delta (n_local, written by the caller, e.g. by
+ * msd_iq_band_delta_dev), the tail halo (n_tail = min(W, frame0)), the head halo, and the
+ * thresholds actually used per frame (after msd_stream_scan).  Any may be NULL. */
+int msd_stream_buffers(msd_stream_plan *plan, double **delta, double **tail, int64_t *n_tail, double **head,
+                       int64_t *n_head, double **thresholds);
+/* use_mean = 0: sums of delta; 1: sums of (delta - mean)^2.  Synchronous; sums -> host
+ * (cap >= chunks), *first_chunk = global index of the first chunk. */
+int msd_stream_chunk_sums(msd_stream_plan *plan, int32_t use_mean, double mean, double *sums, int64_t cap,
+                          int64_t *nchunks, int64_t *first_chunk);
+int msd_stream_fresh(msd_stream_plan *plan); /* async; needs the tail halo */
+/* thr0 = mean + k*std of the whole stream.  reset = 1: every segment restarts from the clean
+ * state (first call); 0: only the entry state changed.  Synchronous; *rounds = scan launches. */
+int msd_stream_scan(msd_stream_plan *plan, double thr0, const msd_stream_state *entry, int32_t reset,
+                    msd_stream_state *exit_state, int32_t *rounds);
+/* the shard's runs in order, host out; stop is exclusive; margin = min |delta - thr| */
+int msd_stream_runs(msd_stream_plan *plan, msd_det *runs, int64_t cap, int64_t *count, double *margin);
+/* dets[j].db = np.mean(delta[start:stop]) for global [start, stop) inside the halos + shard */
+int msd_stream_db(msd_stream_plan *plan, msd_det *dets, int64_t n);
 
 /* ------------------------------------------- a10: legacy spectrogram noise floor
  * prime_detection.py:65-91: band_power = np.sum(Pxx[noise_band]) sums the spectrogram over
@@ -302,6 +365,9 @@ int msd_comm_init(msd_ctx *ctx, int nranks, const char *id, int rank, msd_comm *
 void msd_comm_destroy(msd_comm *comm);
 /* in-place sum of n int64 on the device, on the context stream */
 int msd_comm_allreduce_i64(msd_comm *comm, int64_t *dbuf, int64_t n);
+/* recv[r*bytes .. (r+1)*bytes) = rank r's send (device buffers, context stream) — the C5
+ * stream detector's halo / chunk-sum / shard-state exchange */
+int msd_comm_allgather(msd_comm *comm, const void *dsend, void *drecv, size_t bytes);
 
 #ifdef __cplusplus
 }

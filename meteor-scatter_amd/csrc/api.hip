@@ -68,6 +68,7 @@ struct Rccl {
     ncclResult_t (*commInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*allReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
+    ncclResult_t (*allGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
     const char *(*getErrorString)(ncclResult_t) = nullptr;
     bool ok = false;
@@ -86,9 +87,10 @@ static Rccl *rccl() {
         r.getUniqueId = reinterpret_cast<decltype(r.getUniqueId)>(dlsym(r.h, "ncclGetUniqueId"));
         r.commInitRank = reinterpret_cast<decltype(r.commInitRank)>(dlsym(r.h, "ncclCommInitRank"));
         r.allReduce = reinterpret_cast<decltype(r.allReduce)>(dlsym(r.h, "ncclAllReduce"));
+        r.allGather = reinterpret_cast<decltype(r.allGather)>(dlsym(r.h, "ncclAllGather"));
         r.commDestroy = reinterpret_cast<decltype(r.commDestroy)>(dlsym(r.h, "ncclCommDestroy"));
         r.getErrorString = reinterpret_cast<decltype(r.getErrorString)>(dlsym(r.h, "ncclGetErrorString"));
-        r.ok = r.getUniqueId && r.commInitRank && r.allReduce && r.commDestroy;
+        r.ok = r.getUniqueId && r.commInitRank && r.allReduce && r.allGather && r.commDestroy;
     });
     return r.ok ? &r : nullptr;
 }
@@ -603,6 +605,17 @@ int msd_comm_allreduce_i64(msd_comm *c, int64_t *dbuf, int64_t n) {
     DeviceGuard g(c->ctx->device);
     ncclResult_t e = r->allReduce(dbuf, dbuf, (size_t)n, ncclInt64, ncclSum, c->comm, c->ctx->stream);
     if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
+    return MSD_OK;
+}
+
+int msd_comm_allgather(msd_comm *c, const void *dsend, void *drecv, size_t bytes) {
+    if (!c || ((!dsend || !drecv) && bytes)) return fail(MSD_ERR_INVALID, "msd_comm_allgather: null");
+    if (bytes == 0) return MSD_OK;
+    Rccl *r = rccl();
+    if (!r) return fail(MSD_ERR_RCCL, "librccl.so.1 not loadable");
+    DeviceGuard g(c->ctx->device);
+    ncclResult_t e = r->allGather(dsend, drecv, bytes, ncclChar, c->comm, c->ctx->stream);
+    if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllGather");
     return MSD_OK;
 }
 

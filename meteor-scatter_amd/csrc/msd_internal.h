@@ -21,7 +21,8 @@ int hip_fail(hipError_t e, const char *what);
         if (e_ != hipSuccess) return hip_fail(e_, #call); \
     } while (0)
 
-enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_WELCH = 4, K_LIVE = 5, K_CSTFT = 6, K_COUNT = 7 };
+enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_WELCH = 4, K_LIVE = 5, K_CSTFT = 6, K_IQDELTA = 7, K_FRESH = 8, K_SSCAN = 9,
+               K_COUNT = 10 };
 
 struct EventPair {
     hipEvent_t a, b;

@@ -1,0 +1,867 @@
+// C5: the reference's threshold detectors over ONE long stream (a 24 h I/Q recording whose STFT
+// frames are the detector's blocks), time-sharded over ranks.  get_detections_adaptive()
+// dsp/src/main.py:450-522 and get_detections() :396-448, float64, numpy-exact.
+//
+// Per rank (one shard of the stream's frames), all on the context stream:
+//   iq_band_delta_kernel   frame-major spectrogram [T][N] -> band / noise dB, delta (main.py:380-393)
+//   chunk_sums_kernel      numpy's add.reduce over the whole stream is s = 0.0; s += pairwise(chunk)
+//                          for 8192-element chunks in order: each wave sums one chunk that starts
+//                          in the shard (64 lanes x one 128-element leaf, butterfly = numpy's
+//                          balanced tree); the host adds the chunk sums of all ranks in order
+//   fresh_kernel           mean + k*std(delta[i-W:i]) for every frame i >= W.  The pairwise tree of
+//                          a W-element window has the same shape for every i, so the host turns it
+//                          into a program (leaf / add / chunk-end ops) that every lane runs on its
+//                          own 8 consecutive frames: one LDS element feeds 8 frames' accumulators
+//                          (register blocking), the leaves stream through double-buffered LDS
+//   fresh_short_kernel     frames i < W (windows delta[0:i], a different tree per frame)
+//   scan_kernel            the freeze/run state machine, one wave per segment: lane j evaluates
+//                          frame pos+j; with the freeze state fixed the decisions of 64 frames are
+//                          two ballots (fresh threshold / held threshold), and only the frames
+//                          where the freeze state changes are walked in scalar code
+//   propagate_kernel       segment s+1 re-enters with segment s's exit state; repeated to a
+//                          fixed point (normally 2 rounds: speculative clean start, then fix-up)
+//   runs_kernel, db_kernel the shard's runs (merged over segment edges) and np.mean dB of each
+// FP contraction is off: numpy rounds every add / multiply separately.
+#include "msd_internal.h"
+#include "np_reduce.h"
+
+#include <cmath>
+#include <cstring>
+#include <type_traits>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+struct msd_stream_plan {
+    msd_ctx *ctx = nullptr;
+    msd_det_cfg cfg{};
+    int64_t n_total = 0, frame0 = 0, n_local = 0;
+    int64_t n_tail = 0, n_head = 0, head_cap = 0;
+    int64_t seg_len = 0, nseg = 0, cap = 0;
+    double *d_x = nullptr;      // [n_tail | n_local | head_cap] delta of the stream around the shard
+    double *d_fresh = nullptr;  // [n_local]
+    double *d_thr = nullptr;    // [n_local] thresholds used (scan output)
+    void *d_state = nullptr;    // in[nseg], out[nseg] states
+    int32_t *d_active = nullptr;  // [nseg] + changed counter + overflow flag
+    msd_det *d_runs = nullptr;  // [nseg][cap]
+    int32_t *d_nruns = nullptr; // [nseg]
+    double *d_margin = nullptr; // [nseg]
+    msd_det *d_out = nullptr;   // compacted runs [nseg*cap]
+    int64_t *d_count = nullptr;
+    int64_t *d_pos = nullptr;   // [nseg] runs emitted before each segment
+    double *d_chunks = nullptr; // chunk sums
+    int2 *d_prog = nullptr;     // fresh-threshold program for windows of exactly W frames
+    int nprog = 0;
+    double thr0 = 0;
+    bool scanned = false;
+};
+
+namespace msd {
+namespace {
+
+constexpr int64_t CHUNK = NP_BUFSIZE;  // numpy's reduction buffer (8192 elements)
+
+struct SState {  // msd_stream_state
+    int64_t fz, last_stop;
+    double thr;
+    int64_t reserved;
+};
+
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+    return __builtin_bit_cast(double, __shfl_xor(__builtin_bit_cast(long long, v), m, 64));
+}
+
+// ------------------------------------------------------------------ band delta per frame
+__global__ __launch_bounds__(256) void iq_band_delta_kernel(const float *__restrict__ spec, int64_t nstreams,
+                                                            int64_t max_frames, const int64_t *__restrict__ frames,
+                                                            int N, int blo, int bhi, int nlo, int nhi,
+                                                            double *__restrict__ band_db,
+                                                            double *__restrict__ noise_db,
+                                                            double *__restrict__ delta, int64_t ld) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    for (int64_t g = wave; g < nstreams * max_frames; g += nwaves) {
+        const int64_t s = g / max_frames, t = g - s * max_frames;
+        if (t >= frames[s]) continue;
+        const float *row = spec + (s * max_frames + t) * (int64_t)N;
+        double e[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int lo = b ? nlo : blo, hi = b ? nhi : bhi;
+            double acc = 0.0;
+            for (int k = lo + lane; k <= hi; k += 64) acc += (double)row[k < 0 ? k + N : k];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) acc += shfl_xor_d(acc, o);
+            e[b] = acc;
+        }
+        if (lane == 0) {
+            const double bd = 10.0 * log10(e[0] + 1e-12), nd = 10.0 * log10(e[1] + 1e-12);
+            if (band_db) band_db[s * ld + t] = bd;
+            if (noise_db) noise_db[s * ld + t] = nd;
+            delta[s * ld + t] = bd - nd;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ chunk sums
+// x: the stream around the shard (x[j] = frame x0 + j); chunk c covers frames [8192c, min(8192(c+1),
+// n_total)).  One wave per chunk that starts in the shard.
+template <bool SQ>
+__global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restrict__ x, int64_t x0,
+                                                         int64_t first_chunk, int64_t nchunks, int64_t n_total,
+                                                         double mean, double *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nchunks) return;
+    const int64_t g = (first_chunk + c) * CHUNK;
+    const int64_t m = n_total - g < CHUNK ? n_total - g : CHUNK;
+    const double *p = x + (g - x0);
+    if (m == CHUNK) {  // 64 leaves of 128; numpy's tree over them is balanced: a butterfly
+        double r;
+        if constexpr (SQ)
+            r = np_pairwise_leaf(SqDevRef{p, mean}, (int64_t)lane * 128, 128);
+        else
+            r = np_pairwise_leaf(ArrRef{p}, (int64_t)lane * 128, 128);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) r = r + shfl_xor_d(r, o);
+        if (lane == 0) out[c] = r;
+    } else if (lane == 0) {  // the stream's last, short chunk
+        out[c] = SQ ? np_pairwise(SqDevRef{p, mean}, 0, m) : np_pairwise(ArrRef{p}, 0, m);
+    }
+}
+
+// ------------------------------------------------------------------ fresh thresholds
+// program ops (int2 {op, arg}): LEAF {len | off << 8 in .y? } -> see build_program
+enum { OP_LEAF = 0, OP_ADD = 1, OP_CHUNK = 2 };
+
+constexpr int FR_THREADS = 256;
+constexpr int FR_F = 8;                          // frames per lane
+constexpr int FR_FRAMES = FR_THREADS * FR_F;     // 2048 frames per workgroup
+constexpr int FR_STAGE = FR_FRAMES + 128;        // staged elements per leaf (leaf <= 128)
+constexpr int FR_PADDED = FR_STAGE + FR_STAGE / 4;  // 2 pad doubles per 8: conflict-free b128 reads
+constexpr int FR_LOADS = (FR_STAGE + FR_THREADS - 1) / FR_THREADS;
+constexpr int FR_DEPTH = 10;
+
+__device__ __forceinline__ int padded(int q) { return q + 2 * (q >> 3); }
+
+struct FreshParams {
+    int64_t n_local, frame0, n_tail, x_len, W, F0;
+    double k;
+    int nprog;
+    int64_t wg0;  // first workgroup (blocks below it only hold frames with short windows)
+};
+
+// one pass of the program over this lane's 8 frames: out[f] = numpy np.sum of the window of frame f
+// (SQ: of (x - mean[f])^2)
+template <bool SQ>
+__device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t xbase, int64_t x_len,
+                                           const int2 *__restrict__ prog, int nprog, double *stage,
+                                           const double (&mean)[FR_F], double (&out)[FR_F]) {
+    const int tid = threadIdx.x;
+    double stk[FR_F][FR_DEPTH];
+    int sp = 0;
+    double acc[FR_F];
+#pragma unroll
+    for (int f = 0; f < FR_F; ++f) acc[f] = 0.0;
+
+    // prefetch registers for the next leaf's stage
+    double pre[FR_LOADS];
+    auto fetch = [&](int off) {
+#pragma unroll
+        for (int j = 0; j < FR_LOADS; ++j) {
+            const int q = tid + j * FR_THREADS;
+            int64_t idx = xbase + off + q;
+            idx = idx < 0 ? 0 : (idx >= x_len ? x_len - 1 : idx);
+            pre[j] = q < FR_STAGE ? x[idx] : 0.0;
+        }
+    };
+    auto commit = [&](double *buf) {
+#pragma unroll
+        for (int j = 0; j < FR_LOADS; ++j) {
+            const int q = tid + j * FR_THREADS;
+            if (q < FR_STAGE) buf[padded(q)] = pre[j];
+        }
+    };
+    int nextleaf = 0;
+    while (nextleaf < nprog && prog[nextleaf].x != OP_LEAF) ++nextleaf;
+    int buf = 0;
+    if (nextleaf < nprog) {
+        fetch(prog[nextleaf].y >> 8);
+        commit(stage);
+    }
+    __syncthreads();
+    for (int pc = 0; pc < nprog; ++pc) {
+        const int2 op = prog[pc];
+        if (op.x == OP_ADD) {
+#pragma unroll
+            for (int f = 0; f < FR_F; ++f) stk[f][sp - 2] = stk[f][sp - 2] + stk[f][sp - 1];
+            --sp;
+            continue;
+        }
+        if (op.x == OP_CHUNK) {
+#pragma unroll
+            for (int f = 0; f < FR_F; ++f) acc[f] = acc[f] + stk[f][sp - 1];
+            --sp;
+            continue;
+        }
+        // LEAF: prefetch the following leaf while this one is summed
+        const int len = op.y & 255;
+        int nl = pc + 1;
+        while (nl < nprog && prog[nl].x != OP_LEAF) ++nl;
+        if (nl < nprog) fetch(prog[nl].y >> 8);
+        const double *st = stage + buf * FR_PADDED;
+        const int l8 = tid * 8;  // this lane's first element (frame f reads st[l8 + f + m])
+        auto elem = [&](int q) -> double { return st[padded(l8 + q)]; };
+        double res[FR_F];
+        if (len >= 8) {
+            const int lim = len - (len & 7);
+            const int G = lim >> 3;  // groups 0..G (G+1 groups: frame f spans q in [f, f+lim))
+            double r[FR_F][8];
+#pragma unroll
+            for (int f = 0; f < FR_F; ++f)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) r[f][k] = -0.0;
+            auto group = [&](int g, auto first, auto last) {
+                const double2 *vp = reinterpret_cast<const double2 *>(st + padded(l8 + 8 * g));
+                double v[8];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const double2 t = vp[h];
+                    v[2 * h] = t.x;
+                    v[2 * h + 1] = t.y;
+                }
+#pragma unroll
+                for (int f = 0; f < FR_F; ++f) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if constexpr (decltype(first)::value) {
+                            if (k < f) continue;
+                        }
+                        if constexpr (decltype(last)::value) {
+                            if (k >= f) continue;
+                        }
+                        if constexpr (SQ) {
+                            const double d = v[k] - mean[f];
+                            r[f][(k - f) & 7] += d * d;
+                        } else {
+                            r[f][(k - f) & 7] += v[k];
+                        }
+                    }
+                }
+            };
+            using T_ = std::integral_constant<bool, true>;
+            using F_ = std::integral_constant<bool, false>;
+            group(0, T_{}, F_{});
+            for (int g = 1; g < G; ++g) group(g, F_{}, F_{});
+            group(G, F_{}, T_{});
+#pragma unroll
+            for (int f = 0; f < FR_F; ++f) res[f] = ((r[f][0] + r[f][1]) + (r[f][2] + r[f][3])) +
+                                                     ((r[f][4] + r[f][5]) + (r[f][6] + r[f][7]));
+            for (int t = lim; t < len; ++t) {
+#pragma unroll
+                for (int f = 0; f < FR_F; ++f) {
+                    const double v = elem(f + t);
+                    if constexpr (SQ) {
+                        const double d = v - mean[f];
+                        res[f] += d * d;
+                    } else {
+                        res[f] += v;
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int f = 0; f < FR_F; ++f) res[f] = -0.0;
+            for (int t = 0; t < len; ++t) {
+#pragma unroll
+                for (int f = 0; f < FR_F; ++f) {
+                    const double v = elem(f + t);
+                    if constexpr (SQ) {
+                        const double d = v - mean[f];
+                        res[f] += d * d;
+                    } else {
+                        res[f] += v;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < FR_F; ++f) stk[f][sp] = res[f];
+        ++sp;
+        if (nl < nprog) {
+            commit(stage + (buf ^ 1) * FR_PADDED);
+            buf ^= 1;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int f = 0; f < FR_F; ++f) out[f] = acc[f];
+}
+
+__global__ __launch_bounds__(FR_THREADS) void fresh_kernel(const double *__restrict__ x, FreshParams P,
+                                                           const int2 *__restrict__ prog,
+                                                           double *__restrict__ fresh) {
+    __shared__ __attribute__((aligned(16))) double stage[2 * FR_PADDED];
+    const int64_t wg = P.wg0 + blockIdx.x;
+    const int64_t j0 = wg * FR_FRAMES + threadIdx.x * FR_F;  // this lane's first local frame
+    // element m of the window of local frame j sits at x[n_tail + j - W + m]
+    const int64_t xbase = P.n_tail + wg * FR_FRAMES - P.W;
+    double mean[FR_F], s[FR_F];
+#pragma unroll
+    for (int f = 0; f < FR_F; ++f) mean[f] = 0.0;
+    fresh_pass<false>(x, xbase, P.x_len, prog, P.nprog, stage, mean, s);
+#pragma unroll
+    for (int f = 0; f < FR_F; ++f) mean[f] = s[f] / (double)P.W;
+    fresh_pass<true>(x, xbase, P.x_len, prog, P.nprog, stage, mean, s);
+#pragma unroll
+    for (int f = 0; f < FR_F; ++f) {
+        const int64_t j = j0 + f;
+        const int64_t i = P.frame0 + j;
+        if (j < P.n_local && i >= P.W && i >= P.F0) {
+            const double sd = sqrt(s[f] / (double)P.W);
+            fresh[j] = mean[f] + P.k * sd;
+        }
+    }
+}
+
+// frames with i < W: window delta[0:i] (only the shard that holds the stream's first W frames)
+__global__ __launch_bounds__(256) void fresh_short_kernel(const double *__restrict__ x, FreshParams P,
+                                                          int64_t jend, double *__restrict__ fresh) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= jend) return;
+    const int64_t i = P.frame0 + j;
+    if (i < P.F0) return;
+    double m, sd;
+    np_mean_std(x, P.n_tail + j - i, i, m, sd);  // x index of global frame 0 = n_tail - frame0
+    fresh[j] = m + P.k * sd;
+}
+
+// ------------------------------------------------------------------ scan
+struct ScanParams {
+    int64_t n_local, frame0, seg_len, nseg, cap, F0, Fa;
+    double thr0;
+    int32_t write_thr;
+};
+
+__device__ __forceinline__ uint64_t bits_from(int p) { return p >= 64 ? 0ull : (~0ull << p); }
+__device__ __forceinline__ uint64_t bits_upto(int e) { return e >= 63 ? ~0ull : ((1ull << (e + 1)) - 1ull); }
+
+__global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ delta, const double *__restrict__ fresh,
+                                                  ScanParams P, const SState *__restrict__ in_state,
+                                                  SState *__restrict__ out_state, const int32_t *__restrict__ active,
+                                                  msd_det *__restrict__ runs, int32_t *__restrict__ nruns,
+                                                  double *__restrict__ seg_margin, double *__restrict__ thr_used,
+                                                  int32_t *__restrict__ overflow) {
+    const int64_t s = blockIdx.x;
+    if (!active[s]) return;
+    const int lane = threadIdx.x;
+    const int64_t a = s * P.seg_len;
+    const int64_t b = a + P.seg_len < P.n_local ? a + P.seg_len : P.n_local;
+    const SState in = in_state[s];
+    int64_t fz = in.fz, last_stop = in.last_stop;
+    double thr_cur = in.thr;
+    const double thr0 = P.thr0;
+    msd_det *rs = runs + s * P.cap;
+    int64_t nr = 0, cur_start = 0;
+    bool have = false;
+    double min_margin = __builtin_inf();
+
+    for (int64_t k = a; k < b; k += 64) {
+        const int nvalid = (int)(b - k < 64 ? b - k : 64);
+        const bool valid = lane < nvalid;
+        const int64_t j = valid ? k + lane : k;
+        const int64_t gi = P.frame0 + j;  // global frame of this lane
+        const int64_t pos = P.frame0 + k;
+        const double dv = delta[j];
+        const bool init = gi < P.F0;
+        const double t_unf = init ? thr0 : fresh[j];
+        const uint64_t A_unf = __ballot(valid && dv > t_unf);
+        double t_fin = t_unf;
+        uint64_t D = 0;
+        int p = 0;
+        while (p < nvalid) {
+            const int64_t i = pos + p;
+            if (fz >= i) {  // frozen from p on: threshold held (thr0 before the fixed-init end)
+                const int e = (int)(fz - pos < nvalid - 1 ? fz - pos : nvalid - 1);
+                const double held = i < P.F0 ? thr0 : thr_cur;
+                const double t_h = init ? thr0 : held;
+                const uint64_t rng = bits_from(p) & bits_upto(e);
+                const uint64_t m = __ballot(valid && dv > t_h) & rng;
+                if ((rng >> lane) & 1ull) t_fin = t_h;
+                thr_cur = (pos + e) < P.F0 ? thr0 : held;
+                if (m) {
+                    const int last = 63 - __builtin_clzll(m);
+                    D |= m;
+                    fz = pos + last + P.Fa;
+                }
+                p = e + 1;
+            } else {  // unfrozen: fresh (or fixed) thresholds until the first detection
+                const uint64_t m = A_unf & bits_from(p);
+                if (!m) {
+                    thr_cur = __shfl(t_unf, nvalid - 1);
+                    p = nvalid;
+                    break;
+                }
+                const int u = __builtin_ctzll(m);
+                D |= 1ull << u;
+                thr_cur = __shfl(t_unf, u);
+                fz = pos + u + P.Fa;
+                p = u + 1;
+            }
+        }
+        if (valid) {
+            const double mg = fabs(dv - t_fin);
+            if (mg < min_margin) min_margin = mg;
+            if (P.write_thr) thr_used[j] = t_fin;
+        }
+        // runs: maximal groups of consecutive detected frames (a new run iff i > last_stop + 1)
+        while (D) {
+            const int g0 = __builtin_ctzll(D);
+            const uint64_t rest = ~(D >> g0);
+            const int glen = rest ? __builtin_ctzll(rest) : 64 - g0;
+            const int64_t ib = pos + g0, ie = ib + glen - 1;
+            if (last_stop == ib - 1) {
+                if (!have) {  // continues the previous segment's run
+                    have = true;
+                    cur_start = -1;
+                }
+            } else {
+                if (have) {
+                    if (lane == 0 && nr < P.cap) {
+                        rs[nr].start = cur_start;
+                        rs[nr].stop = last_stop + 1;
+                    }
+                    ++nr;
+                }
+                have = true;
+                cur_start = ib;
+            }
+            last_stop = ie;
+            D &= (glen + g0 >= 64) ? 0ull : (~0ull << (g0 + glen));
+        }
+    }
+    if (have) {
+        if (lane == 0 && nr < P.cap) {
+            rs[nr].start = cur_start;
+            rs[nr].stop = last_stop + 1;
+        }
+        ++nr;
+    }
+    for (int o = 32; o >= 1; o >>= 1) min_margin = fmin(min_margin, __shfl_xor(min_margin, o, 64));
+    if (lane == 0) {
+        nruns[s] = (int32_t)(nr < P.cap ? nr : P.cap);
+        if (nr > P.cap) atomicOr(overflow, 1);
+        seg_margin[s] = min_margin;
+        SState o;
+        o.fz = fz;
+        o.last_stop = last_stop;
+        o.thr = thr_cur;
+        o.reserved = 0;
+        out_state[s] = o;
+    }
+}
+
+// normalised equality of two states entering frame a (see msd_stream_state)
+__device__ __forceinline__ bool same_state(const SState &x, const SState &y, int64_t a, int64_t F0) {
+    const bool fx = x.fz >= a, fy = y.fz >= a;
+    if (fx != fy) return false;
+    if (fx) {
+        if (x.fz != y.fz) return false;
+        if (a >= F0 && __builtin_bit_cast(long long, x.thr) != __builtin_bit_cast(long long, y.thr)) return false;
+    }
+    return (x.last_stop == a - 1) == (y.last_stop == a - 1);
+}
+
+__global__ void propagate_kernel(SState *__restrict__ in_state, const SState *__restrict__ out_state,
+                                 int32_t *__restrict__ active, int64_t nseg, int64_t seg_len, int64_t frame0,
+                                 int64_t F0, int32_t *__restrict__ changed) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    if (s == 0) {
+        active[0] = 0;
+        return;
+    }
+    const SState nw = out_state[s - 1];
+    if (same_state(nw, in_state[s], frame0 + s * seg_len, F0)) {
+        active[s] = 0;
+    } else {
+        in_state[s] = nw;
+        active[s] = 1;
+        atomicAdd(changed, 1);
+    }
+}
+
+// compaction: runs of segment s go to out[pos_s ..]; a continued first run of s >= 1 extends the
+// last run of s-1 (or the run that one continues) instead.  One workgroup.
+__global__ __launch_bounds__(1024) void runs_kernel(const msd_det *__restrict__ runs,
+                                                    const int32_t *__restrict__ nruns, int64_t nseg, int64_t cap,
+                                                    msd_det *__restrict__ out, int64_t *__restrict__ count,
+                                                    int64_t *__restrict__ seg_pos) {
+    __shared__ int64_t s_base;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < nseg; c0 += 1024) {
+        const int64_t s = c0 + tid;
+        int64_t e = 0;
+        bool cont = false;
+        if (s < nseg) {
+            const int64_t n = nruns[s];
+            cont = s > 0 && n > 0 && runs[s * cap].start < 0;
+            e = n - (cont ? 1 : 0);
+        }
+        // block-wide inclusive scan of e (Hillis-Steele in LDS)
+        __shared__ int64_t sc[1024];
+        sc[tid] = e;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const int64_t v = tid >= o ? sc[tid - o] : 0;
+            __syncthreads();
+            sc[tid] += v;
+            __syncthreads();
+        }
+        const int64_t pos = s_base + sc[tid] - e;
+        if (s < nseg) {
+            seg_pos[s] = pos;
+            const int64_t n = nruns[s];
+            for (int64_t r = cont ? 1 : 0; r < n; ++r) out[pos + r - (cont ? 1 : 0)] = runs[s * cap + r];
+        }
+        __syncthreads();
+        if (tid == 1023) s_base += sc[1023];
+        __syncthreads();
+    }
+    if (tid == 0) *count = s_base;
+    __syncthreads();
+    // continued runs: the owner is the last emitted run before this segment
+    for (int64_t s = 1 + tid; s < nseg; s += 1024) {
+        const int64_t n = nruns[s];
+        if (n == 0 || runs[s * cap].start >= 0) continue;
+        const int64_t before = seg_pos[s];  // runs emitted by the segments before s
+        if (before > 0)
+            atomicMax(reinterpret_cast<unsigned long long *>(&out[before - 1].stop),
+                      (unsigned long long)runs[s * cap].stop);
+    }
+}
+
+__global__ void db_kernel(const double *__restrict__ x, int64_t x0, msd_det *__restrict__ d, int64_t n) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t a = d[j].start, m = d[j].stop - d[j].start;
+    d[j].db = np_sum(ArrRef{x}, a - x0, m) / (double)m;
+}
+
+// numpy's np.sum association over n elements as a program for fresh_kernel (leaves of <= 128)
+void build_program(int64_t n, std::vector<int2> &prog) {
+    prog.clear();
+    struct Rec {
+        static void tree(int64_t base, int64_t m, std::vector<int2> &p) {
+            if (m <= 128) {
+                p.push_back(make_int2(OP_LEAF, (int)((base << 8) | m)));
+                return;
+            }
+            int64_t m2 = m / 2;
+            m2 -= m2 % 8;
+            tree(base, m2, p);
+            tree(base + m2, m - m2, p);
+            p.push_back(make_int2(OP_ADD, 0));
+        }
+    };
+    for (int64_t c = 0; c < n; c += CHUNK) {
+        const int64_t m = n - c < CHUNK ? n - c : CHUNK;
+        Rec::tree(c, m, prog);
+        prog.push_back(make_int2(OP_CHUNK, 0));
+    }
+}
+
+}  // namespace
+}  // namespace msd
+
+using namespace msd;
+
+static SState *st_in(msd_stream_plan *p) { return reinterpret_cast<SState *>(p->d_state); }
+static SState *st_out(msd_stream_plan *p) { return reinterpret_cast<SState *>(p->d_state) + p->nseg; }
+
+extern "C" {
+
+int msd_iq_band_delta_dev(msd_ctx *ctx, const float *spec, int64_t nstreams, int64_t max_frames,
+                          const int64_t *frames, int32_t nperseg, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
+                          int32_t noise_hi, double *band_db, double *noise_db, double *delta, int64_t ld) {
+    if (!ctx || !spec || !frames || !delta || nstreams < 0 || max_frames < 0 || nperseg <= 0 || ld < max_frames)
+        return fail(MSD_ERR_INVALID, "msd_iq_band_delta_dev: bad args");
+    const int h = nperseg / 2;
+    auto ok = [&](int lo, int hi) { return hi < lo || (lo >= -h && hi <= nperseg - h - 1); };
+    if (!ok(band_lo, band_hi) || !ok(noise_lo, noise_hi))
+        return fail(MSD_ERR_INVALID, "msd_iq_band_delta_dev: band outside -N/2 .. N/2-1");
+    if (nstreams == 0 || max_frames == 0) return MSD_OK;
+    DeviceGuard g(ctx->device);
+    KernelTimer timer(ctx, K_IQDELTA);
+    const int64_t waves = nstreams * max_frames;
+    int64_t blocks = (waves + 3) / 4;
+    const int64_t lim = (int64_t)ctx->num_cu * 16;
+    if (blocks > lim) blocks = lim;
+    hipLaunchKernelGGL(iq_band_delta_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, spec, nstreams,
+                       max_frames, frames, (int)nperseg, band_lo, band_hi, noise_lo, noise_hi, band_db, noise_db,
+                       delta, ld);
+    MSD_HIP(hipGetLastError());
+    return MSD_OK;
+}
+
+int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total, int64_t frame0, int64_t n_local,
+                           int64_t seg_len, int64_t cap_per_seg, int64_t head_frames, msd_stream_plan **out) {
+    if (!ctx || !cfg || !out || n_total < 0 || frame0 < 0 || n_local < 0 || frame0 + n_local > n_total ||
+        seg_len < 64 || seg_len % 64 || cap_per_seg <= 0 || head_frames < 0)
+        return fail(MSD_ERR_INVALID, "msd_stream_plan_create: bad args");
+    if (cfg->adaptive && (cfg->window_blocks < 0 || cfg->freeze_after_blocks < 0 || cfg->fixed_init_blocks < 0))
+        return fail(MSD_ERR_INVALID, "msd_stream_plan_create: negative block counts");
+    *out = nullptr;
+    DeviceGuard g(ctx->device);
+    auto *p = new msd_stream_plan();
+    p->ctx = ctx;
+    p->cfg = *cfg;
+    p->n_total = n_total;
+    p->frame0 = frame0;
+    p->n_local = n_local;
+    const int64_t W = cfg->adaptive ? cfg->window_blocks : 0;
+    p->n_tail = W < frame0 ? W : frame0;
+    const int64_t after = n_total - frame0 - n_local;
+    p->head_cap = head_frames;
+    p->n_head = head_frames < after ? head_frames : after;
+    p->seg_len = seg_len;
+    p->nseg = n_local > 0 ? (n_local + seg_len - 1) / seg_len : 0;
+    p->cap = cap_per_seg;
+    const int64_t nseg1 = p->nseg > 0 ? p->nseg : 1;
+    const int64_t nl1 = n_local > 0 ? n_local : 1;
+    const int64_t nchunk = n_local / CHUNK + 2;
+    auto cleanup = [&](hipError_t e, const char *what) {
+        msd_stream_plan_destroy(p);
+        return hip_fail(e, what);
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&p->d_x, sizeof(double) * (p->n_tail + nl1 + p->head_cap))) != hipSuccess)
+        return cleanup(e, "hipMalloc stream x");
+    if ((e = hipMalloc(&p->d_fresh, sizeof(double) * nl1)) != hipSuccess) return cleanup(e, "hipMalloc fresh");
+    if ((e = hipMalloc(&p->d_thr, sizeof(double) * nl1)) != hipSuccess) return cleanup(e, "hipMalloc thr");
+    if ((e = hipMalloc(&p->d_state, sizeof(SState) * 2 * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc state");
+    if ((e = hipMalloc(&p->d_active, sizeof(int32_t) * (nseg1 + 2))) != hipSuccess)
+        return cleanup(e, "hipMalloc active");
+    if ((e = hipMalloc(&p->d_runs, sizeof(msd_det) * nseg1 * cap_per_seg)) != hipSuccess)
+        return cleanup(e, "hipMalloc runs");
+    if ((e = hipMalloc(&p->d_out, sizeof(msd_det) * nseg1 * cap_per_seg)) != hipSuccess)
+        return cleanup(e, "hipMalloc out");
+    if ((e = hipMalloc(&p->d_nruns, sizeof(int32_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc nruns");
+    if ((e = hipMalloc(&p->d_margin, sizeof(double) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc margin");
+    if ((e = hipMalloc(&p->d_count, sizeof(int64_t))) != hipSuccess) return cleanup(e, "hipMalloc count");
+    if ((e = hipMalloc(&p->d_pos, sizeof(int64_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc pos");
+    if ((e = hipMalloc(&p->d_chunks, sizeof(double) * nchunk)) != hipSuccess) return cleanup(e, "hipMalloc chunks");
+    if (W > 0) {
+        std::vector<int2> prog;
+        build_program(W, prog);
+        p->nprog = (int)prog.size();
+        if ((e = hipMalloc(&p->d_prog, sizeof(int2) * prog.size())) != hipSuccess) return cleanup(e, "hipMalloc prog");
+        if ((e = hipMemcpy(p->d_prog, prog.data(), sizeof(int2) * prog.size(), hipMemcpyHostToDevice)) != hipSuccess)
+            return cleanup(e, "hipMemcpy prog");
+    }
+    *out = p;
+    return MSD_OK;
+}
+
+void msd_stream_plan_destroy(msd_stream_plan *p) {
+    if (!p) return;
+    DeviceGuard g(p->ctx->device);
+    hipStreamSynchronize(p->ctx->stream);
+    void *bufs[] = {p->d_x, p->d_fresh, p->d_thr, p->d_state, p->d_active, p->d_runs, p->d_out, p->d_nruns,
+                    p->d_margin, p->d_count, p->d_pos, p->d_chunks, p->d_prog};
+    for (void *b : bufs)
+        if (b) hipFree(b);
+    delete p;
+}
+
+int msd_stream_buffers(msd_stream_plan *p, double **delta, double **tail, int64_t *n_tail, double **head,
+                       int64_t *n_head, double **thresholds) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_buffers: null plan");
+    if (delta) *delta = p->d_x + p->n_tail;
+    if (tail) *tail = p->d_x;
+    if (n_tail) *n_tail = p->n_tail;
+    if (head) *head = p->d_x + p->n_tail + p->n_local;
+    if (n_head) *n_head = p->n_head;
+    if (thresholds) *thresholds = p->d_thr;
+    return MSD_OK;
+}
+
+int msd_stream_chunk_sums(msd_stream_plan *p, int32_t use_mean, double mean, double *sums, int64_t cap,
+                          int64_t *nchunks, int64_t *first_chunk) {
+    if (!p || !nchunks || !first_chunk) return fail(MSD_ERR_INVALID, "msd_stream_chunk_sums: null");
+    const int64_t c0 = (p->frame0 + CHUNK - 1) / CHUNK;
+    const int64_t end = p->frame0 + p->n_local;
+    const int64_t c1 = end > 0 ? (end + CHUNK - 1) / CHUNK : 0;  // chunks starting before end
+    const int64_t nc = c1 > c0 ? c1 - c0 : 0;
+    *first_chunk = c0;
+    *nchunks = nc;
+    if (nc == 0) return MSD_OK;
+    if (!sums || cap < nc) return fail(MSD_ERR_CAPACITY, "msd_stream_chunk_sums: sums buffer too small");
+    const int64_t last_end = (c1 * CHUNK < p->n_total ? c1 * CHUNK : p->n_total);
+    if (last_end > end + p->n_head)
+        return fail(MSD_ERR_UNSUPPORTED, "msd_stream_chunk_sums: the shard's last chunk runs past the head halo");
+    DeviceGuard g(p->ctx->device);
+    const int64_t x0 = p->frame0 - p->n_tail;
+    const unsigned blocks = (unsigned)((nc + 3) / 4);
+    if (use_mean)
+        hipLaunchKernelGGL(chunk_sums_kernel<true>, dim3(blocks), dim3(256), 0, p->ctx->stream, p->d_x, x0, c0, nc,
+                           p->n_total, mean, p->d_chunks);
+    else
+        hipLaunchKernelGGL(chunk_sums_kernel<false>, dim3(blocks), dim3(256), 0, p->ctx->stream, p->d_x, x0, c0, nc,
+                           p->n_total, 0.0, p->d_chunks);
+    MSD_HIP(hipGetLastError());
+    MSD_HIP(hipMemcpyAsync(sums, p->d_chunks, sizeof(double) * nc, hipMemcpyDeviceToHost, p->ctx->stream));
+    MSD_HIP(hipStreamSynchronize(p->ctx->stream));
+    return MSD_OK;
+}
+
+int msd_stream_fresh(msd_stream_plan *p) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_fresh: null plan");
+    if (!p->cfg.adaptive || p->n_local == 0) return MSD_OK;
+    DeviceGuard g(p->ctx->device);
+    KernelTimer timer(p->ctx, K_FRESH);
+    FreshParams P;
+    P.n_local = p->n_local;
+    P.frame0 = p->frame0;
+    P.n_tail = p->n_tail;
+    P.x_len = p->n_tail + p->n_local + p->n_head;
+    P.W = p->cfg.window_blocks;
+    P.F0 = p->cfg.fixed_init_blocks;
+    P.k = p->cfg.k_std;
+    P.nprog = p->nprog;
+    P.wg0 = 0;
+    // frames [0, jshort) have windows shorter than W
+    int64_t jshort = P.W - p->frame0;
+    jshort = jshort < 0 ? 0 : (jshort > p->n_local ? p->n_local : jshort);
+    if (P.W == 0) jshort = p->n_local;  // empty windows: NaN thresholds
+    if (jshort > 0)
+        hipLaunchKernelGGL(fresh_short_kernel, dim3((unsigned)((jshort + 255) / 256)), dim3(256), 0, p->ctx->stream,
+                           p->d_x, P, jshort, p->d_fresh);
+    if (jshort < p->n_local && P.W > 0) {
+        const int64_t wg = (p->n_local + FR_FRAMES - 1) / FR_FRAMES;
+        P.wg0 = jshort / FR_FRAMES;  // skip workgroups that only hold short-window frames
+        hipLaunchKernelGGL(fresh_kernel, dim3((unsigned)(wg - P.wg0)), dim3(FR_THREADS), 0, p->ctx->stream, p->d_x, P,
+                           p->d_prog, p->d_fresh);
+    }
+    MSD_HIP(hipGetLastError());
+    return MSD_OK;
+}
+
+int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *entry, int32_t reset,
+                    msd_stream_state *exit_state, int32_t *rounds) {
+    if (!p || !entry) return fail(MSD_ERR_INVALID, "msd_stream_scan: null");
+    DeviceGuard g(p->ctx->device);
+    hipStream_t st = p->ctx->stream;
+    int32_t nround = 0;
+    if (p->nseg == 0) {
+        if (exit_state) *exit_state = *entry;
+        if (rounds) *rounds = 0;
+        return MSD_OK;
+    }
+    if (reset || !p->scanned) {
+        std::vector<SState> init(p->nseg);
+        for (auto &s : init) s = SState{-1, -2, thr0, 0};
+        std::memcpy(&init[0], entry, sizeof(SState));
+        MSD_HIP(hipMemcpyAsync(st_in(p), init.data(), sizeof(SState) * p->nseg, hipMemcpyHostToDevice, st));
+        std::vector<int32_t> act(p->nseg + 2, 1);
+        act[p->nseg] = 0;
+        act[p->nseg + 1] = 0;
+        MSD_HIP(hipMemcpyAsync(p->d_active, act.data(), sizeof(int32_t) * act.size(), hipMemcpyHostToDevice, st));
+        MSD_HIP(hipStreamSynchronize(st));
+    } else {
+        MSD_HIP(hipMemcpyAsync(st_in(p), entry, sizeof(SState), hipMemcpyHostToDevice, st));
+        int32_t one = 1;
+        MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));
+        MSD_HIP(hipMemcpyAsync(p->d_active, &one, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        MSD_HIP(hipStreamSynchronize(st));
+    }
+    p->thr0 = thr0;
+    ScanParams P;
+    P.n_local = p->n_local;
+    P.frame0 = p->frame0;
+    P.seg_len = p->seg_len;
+    P.nseg = p->nseg;
+    P.cap = p->cap;
+    P.F0 = p->cfg.adaptive ? p->cfg.fixed_init_blocks : p->n_total;  // global mode: thr0 everywhere
+    P.Fa = p->cfg.adaptive ? p->cfg.freeze_after_blocks : 0;
+    P.thr0 = thr0;
+    P.write_thr = 1;
+    int32_t *changed = p->d_active + p->nseg;
+    int32_t *overflow = p->d_active + p->nseg + 1;
+    for (;;) {
+        {
+            KernelTimer timer(p->ctx, K_SSCAN);
+            hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
+                               p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
+                               p->d_margin, p->d_thr, overflow);
+        }
+        MSD_HIP(hipGetLastError());
+        ++nround;
+        MSD_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), st));
+        hipLaunchKernelGGL(propagate_kernel, dim3((unsigned)((p->nseg + 255) / 256)), dim3(256), 0, st, st_in(p),
+                           st_out(p), p->d_active, p->nseg, p->seg_len, p->frame0, P.F0, changed);
+        MSD_HIP(hipGetLastError());
+        int32_t hc[2];
+        MSD_HIP(hipMemcpyAsync(hc, changed, sizeof(hc), hipMemcpyDeviceToHost, st));
+        MSD_HIP(hipStreamSynchronize(st));
+        if (hc[1]) return fail(MSD_ERR_CAPACITY, "msd_stream_scan: more runs in a segment than cap_per_seg");
+        if (hc[0] == 0) break;
+        if (nround > p->nseg + 2) return fail(MSD_ERR_INVALID, "msd_stream_scan: no fixed point");
+    }
+    p->scanned = true;
+    if (exit_state) MSD_HIP(hipMemcpy(exit_state, st_out(p) + (p->nseg - 1), sizeof(SState), hipMemcpyDeviceToHost));
+    if (rounds) *rounds = nround;
+    return MSD_OK;
+}
+
+int msd_stream_runs(msd_stream_plan *p, msd_det *runs, int64_t cap, int64_t *count, double *margin) {
+    if (!p || !count) return fail(MSD_ERR_INVALID, "msd_stream_runs: null");
+    *count = 0;
+    if (margin) *margin = __builtin_inf();
+    if (p->nseg == 0) return MSD_OK;
+    if (!p->scanned) return fail(MSD_ERR_INVALID, "msd_stream_runs: call msd_stream_scan first");
+    DeviceGuard g(p->ctx->device);
+    hipStream_t st = p->ctx->stream;
+    hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(1024), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
+                       p->d_count, p->d_pos);
+    MSD_HIP(hipGetLastError());
+    int64_t n = 0;
+    MSD_HIP(hipMemcpyAsync(&n, p->d_count, sizeof(n), hipMemcpyDeviceToHost, st));
+    std::vector<double> mg(p->nseg);
+    MSD_HIP(hipMemcpyAsync(mg.data(), p->d_margin, sizeof(double) * p->nseg, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
+    *count = n;
+    if (margin)
+        for (double v : mg) *margin = v < *margin ? v : *margin;
+    if (n > cap) return fail(MSD_ERR_CAPACITY, "msd_stream_runs: more runs than capacity");
+    if (n > 0) {
+        if (!runs) return fail(MSD_ERR_INVALID, "msd_stream_runs: null runs");
+        MSD_HIP(hipMemcpy(runs, p->d_out, sizeof(msd_det) * n, hipMemcpyDeviceToHost));
+    }
+    return MSD_OK;
+}
+
+int msd_stream_db(msd_stream_plan *p, msd_det *dets, int64_t n) {
+    if (!p || (!dets && n)) return fail(MSD_ERR_INVALID, "msd_stream_db: null");
+    if (n == 0) return MSD_OK;
+    const int64_t x0 = p->frame0 - p->n_tail, x1 = p->frame0 + p->n_local + p->n_head;
+    for (int64_t j = 0; j < n; ++j)
+        if (dets[j].start < x0 || dets[j].stop > x1 || dets[j].stop <= dets[j].start)
+            return fail(MSD_ERR_UNSUPPORTED, "msd_stream_db: run outside the shard and its halos");
+    DeviceGuard g(p->ctx->device);
+    hipStream_t st = p->ctx->stream;
+    void *d = nullptr;
+    if (int rc = ctx_scratch(p->ctx, 3, sizeof(msd_det) * n, &d)) return rc;
+    MSD_HIP(hipMemcpyAsync(d, dets, sizeof(msd_det) * n, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(db_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p->d_x, x0,
+                       reinterpret_cast<msd_det *>(d), n);
+    MSD_HIP(hipGetLastError());
+    MSD_HIP(hipMemcpyAsync(dets, d, sizeof(msd_det) * n, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
+    return MSD_OK;
+}
+
+}  // extern "C"

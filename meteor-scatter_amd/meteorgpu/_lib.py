@@ -35,6 +35,7 @@ DTYPE_CODES = {
 }
 
 K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE, K_CSTFT = 0, 1, 2, 3, 4, 5, 6
+K_IQDELTA, K_FRESH, K_SSCAN = 7, 8, 9
 OPT_GENERIC_STFT = 1
 COMM_ID_BYTES = 128
 
@@ -113,6 +114,12 @@ METEOR_DTYPE = np.dtype([("start_block", np.int64), ("stop_block", np.int64), ("
                          ("db_max", np.float64), ("db_mean", np.float64), ("db_std", np.float64)])
 
 
+class MsdStreamState(C.Structure):
+    """msd_stream_state: the detector state entering a frame (main.py:455-493 variables)."""
+    _fields_ = [("freeze_until", C.c_int64), ("last_stop", C.c_int64), ("thr", C.c_double),
+                ("reserved", C.c_int64)]
+
+
 class MsdWavInfo(C.Structure):
     _fields_ = [
         ("rate", C.c_int32),
@@ -189,6 +196,23 @@ _SIGS = [
     ("msd_comm_init", C.c_int, [_P, C.c_int, _P, C.c_int, C.POINTER(_P)]),
     ("msd_comm_destroy", None, [_P]),
     ("msd_comm_allreduce_i64", C.c_int, [_P, _P, C.c_int64]),
+    ("msd_comm_allgather", C.c_int, [_P, _P, _P, C.c_size_t]),
+    ("msd_iq_band_delta_dev", C.c_int,
+     [_P, _P, C.c_int64, C.c_int64, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P,
+      C.c_int64]),
+    ("msd_stream_plan_create", C.c_int,
+     [_P, C.POINTER(MsdDetCfg), C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.POINTER(_P)]),
+    ("msd_stream_plan_destroy", None, [_P]),
+    ("msd_stream_buffers", C.c_int,
+     [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_int64), C.POINTER(_P), C.POINTER(C.c_int64),
+      C.POINTER(_P)]),
+    ("msd_stream_chunk_sums", C.c_int,
+     [_P, C.c_int32, C.c_double, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    ("msd_stream_fresh", C.c_int, [_P]),
+    ("msd_stream_scan", C.c_int,
+     [_P, C.c_double, C.POINTER(MsdStreamState), C.c_int32, C.POINTER(MsdStreamState), C.POINTER(C.c_int32)]),
+    ("msd_stream_runs", C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+    ("msd_stream_db", C.c_int, [_P, _P, C.c_int64]),
 ]
 SYMBOLS = [s[0] for s in _SIGS]
 
@@ -336,7 +360,7 @@ class StftPlan:
         self.nbins = nperseg // 2 + 1
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and self.ctx.h:  # a plan outliving its context leaks, never crashes
             self.ctx.lib.msd_stft_plan_destroy(self.h)
             self.h = None
 
@@ -381,7 +405,7 @@ class BlockPlan:
         self.nfft = int(nfft)
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and self.ctx.h:  # a plan outliving its context leaks, never crashes
             self.ctx.lib.msd_block_plan_destroy(self.h)
             self.h = None
 
@@ -446,7 +470,7 @@ class WelchPlan:
         self.block_size = int(cfg.block_size)
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and self.ctx.h:  # a plan outliving its context leaks, never crashes
             self.ctx.lib.msd_welch_plan_destroy(self.h)
             self.h = None
 
@@ -516,7 +540,7 @@ class CStftPlan:
         self.nperseg, self.hop = int(nperseg), int(hop)
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and self.ctx.h:  # a plan outliving its context leaks, never crashes
             self.ctx.lib.msd_cstft_plan_destroy(self.h)
             self.h = None
 
@@ -543,3 +567,108 @@ class CStftPlan:
                 max_frames: int, out: DeviceBuffer):
         check(self.ctx.lib.msd_cstft_psd_dev(self.h, x.ptr, int(dtype_code_iq), off.ptr, length.ptr, int(nstreams),
                                              int(max_frames), out.ptr))
+
+
+class StreamPlan:
+    """One rank's shard of a long stream's per-frame delta and the detector over it
+    (include/msdsp.h, C5 stream detector); driven by meteorgpu.stream.StreamDetector."""
+
+    def __init__(self, ctx: Context, cfg: MsdDetCfg, n_total: int, frame0: int, n_local: int,
+                 seg_len: int = 8192, cap_per_seg: int = 256, head_frames: int = 8192):
+        self.ctx = ctx
+        self.cfg = cfg
+        h = C.c_void_p()
+        check(ctx.lib.msd_stream_plan_create(ctx.h, C.byref(cfg), int(n_total), int(frame0), int(n_local),
+                                             int(seg_len), int(cap_per_seg), int(head_frames), C.byref(h)))
+        self.h = h
+        self.n_total, self.frame0, self.n_local = int(n_total), int(frame0), int(n_local)
+        self.seg_len, self.cap_per_seg = int(seg_len), int(cap_per_seg)
+        d, t, hd, thr = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        nt, nh = C.c_int64(0), C.c_int64(0)
+        check(ctx.lib.msd_stream_buffers(h, C.byref(d), C.byref(t), C.byref(nt), C.byref(hd), C.byref(nh),
+                                         C.byref(thr)))
+        self.d_delta, self.d_tail, self.d_head, self.d_thr = d, t, hd, thr
+        self.n_tail, self.n_head = nt.value, nh.value
+        self.nseg = -(-self.n_local // self.seg_len) if self.n_local else 0
+
+    def close(self):
+        if getattr(self, "h", None) and self.ctx.h:  # a plan outliving its context leaks, never crashes
+            self.ctx.lib.msd_stream_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _put(self, dptr, a: np.ndarray):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        if a.size:
+            check(self.ctx.lib.msd_memcpy_h2d(self.ctx.h, dptr, ptr(a), C.c_size_t(a.nbytes)))
+
+    def _get(self, dptr, n: int) -> np.ndarray:
+        out = np.empty(int(n), np.float64)
+        if n:
+            check(self.ctx.lib.msd_memcpy_d2h(self.ctx.h, ptr(out), dptr, C.c_size_t(out.nbytes)))
+        return out
+
+    def set_delta(self, delta: np.ndarray):
+        if np.asarray(delta).shape != (self.n_local,):
+            raise ValueError("delta must hold the shard's n_local frames")
+        self._put(self.d_delta, delta)
+
+    def delta(self) -> np.ndarray:
+        return self._get(self.d_delta, self.n_local)
+
+    def set_halos(self, tail: np.ndarray, head: np.ndarray):
+        if np.asarray(tail).shape != (self.n_tail,) or np.asarray(head).shape != (self.n_head,):
+            raise ValueError(f"halos must hold {self.n_tail} / {self.n_head} frames")
+        self._put(self.d_tail, tail)
+        self._put(self.d_head, head)
+
+    def thresholds(self) -> np.ndarray:
+        return self._get(self.d_thr, self.n_local)
+
+    def chunk_sums(self, mean: float | None = None) -> tuple[int, np.ndarray]:
+        cap = self.n_local // 8192 + 2
+        out = np.empty(cap, np.float64)
+        n, c0 = C.c_int64(0), C.c_int64(0)
+        check(self.ctx.lib.msd_stream_chunk_sums(self.h, 0 if mean is None else 1, 0.0 if mean is None else mean,
+                                                 ptr(out), cap, C.byref(n), C.byref(c0)))
+        return c0.value, out[: n.value].copy()
+
+    def fresh(self):
+        check(self.ctx.lib.msd_stream_fresh(self.h))
+
+    def scan(self, thr0: float, entry: MsdStreamState, reset: bool) -> tuple[MsdStreamState, int]:
+        ex = MsdStreamState()
+        rounds = C.c_int32(0)
+        check(self.ctx.lib.msd_stream_scan(self.h, float(thr0), C.byref(entry), 1 if reset else 0, C.byref(ex),
+                                           C.byref(rounds)))
+        return ex, rounds.value
+
+    def runs(self) -> tuple[np.ndarray, float]:
+        cap = max(1, self.nseg * self.cap_per_seg)
+        out = np.zeros(cap, dtype=DET_DTYPE)
+        n = C.c_int64(0)
+        mg = C.c_double(0)
+        check(self.ctx.lib.msd_stream_runs(self.h, ptr(out), cap, C.byref(n), C.byref(mg)))
+        return out[: n.value].copy(), mg.value
+
+    def db(self, dets: np.ndarray) -> np.ndarray:
+        d = np.ascontiguousarray(dets, dtype=DET_DTYPE).copy()
+        check(self.ctx.lib.msd_stream_db(self.h, ptr(d), d.shape[0]))
+        return d
+
+
+def iq_band_delta_dev(ctx: Context, spec: DeviceBuffer, nstreams: int, max_frames: int, frames: DeviceBuffer,
+                      nperseg: int, band: tuple[int, int], noise: tuple[int, int], delta, ld: int,
+                      band_db=None, noise_db=None):
+    """delta (device pointer or DeviceBuffer) [s*ld + t] from the frame-major I/Q spectrogram."""
+    dp = delta.ptr if isinstance(delta, DeviceBuffer) else delta
+    bp = band_db.ptr if isinstance(band_db, DeviceBuffer) else band_db
+    np_ = noise_db.ptr if isinstance(noise_db, DeviceBuffer) else noise_db
+    check(ctx.lib.msd_iq_band_delta_dev(ctx.h, spec.ptr, int(nstreams), int(max_frames), frames.ptr, int(nperseg),
+                                        int(band[0]), int(band[1]), int(noise[0]), int(noise[1]), bp, np_, dp,
+                                        int(ld)))

@@ -5,13 +5,20 @@ overlap), the SDR-native form of the reference's spectrogram call (dsp/src/main.
 ``spectrogram_iq(i, q, fs, nperseg=4096, noverlap=3072)`` returns scipy's ``(f, t, Sxx)``
 with ``Sxx`` float32 [N][T] in FFT bin order; the device keeps the frame-major [T][N] layout
 (``IQBatch``), of which scipy's is the transpose.  No CPU fallback.
+
+The detector over the I/Q stream (``proc_iq_samples``, ``IQShardDetector``) is the reference's
+block detector (dsp/src/main.py:380-527) with the STFT frame as the block (block_sec = hop/fs):
+per frame the band and noise energies of the two-sided spectrum (fftfreq masks, main.py:382-388
+semantics) give ``delta = band_dB - noise_dB``, and the global / adaptive detector runs over the
+whole stream — time-sharded over ranks by ``meteorgpu.stream``.
 """
 from __future__ import annotations
 
 import numpy as np
 
 from . import _lib
-from .dsp import context, hann_periodic
+from . import stream as _stream
+from .dsp import OutputDetection, _blocks, _utc, context, hann_periodic, write_csv
 
 
 def _plan(ctx, fs, nperseg, noverlap):
@@ -80,7 +87,117 @@ class IQBatch:
     def run(self):
         self.plan.run_dev(self.d_x, self.code, self.d_off, self.d_len, self.ns, self.T, self.d_out)
 
+    def close(self):
+        self.plan.close()
+        for b in (self.d_x, self.d_off, self.d_len, self.d_out):
+            b.free()
+
     def frames(self, s: int, t0: int, nt: int) -> np.ndarray:
         out = np.empty((nt, self.N), np.float32)
         self.d_out.download(out, byte_offset=((s * self.T + t0) * self.N) * 4)
         return out
+
+
+# ----------------------------------------------------------------- detector over the I/Q stream
+def iq_band_bins(nperseg: int, fs: float, band) -> tuple[int, int]:
+    """Signed bin range [lo, hi] of fftfreq(nperseg, 1/fs) selected by (f >= band[0]) & (f <= band[1])
+    (main.py:382 mask semantics on the two-sided spectrum); (0, -1) if no bin falls in the band."""
+    f = np.fft.fftfreq(nperseg, d=1 / fs)
+    b = np.fft.fftfreq(nperseg, d=1.0 / nperseg).round().astype(np.int64)  # signed bin index
+    sel = (f >= band[0]) & (f <= band[1])
+    if not sel.any():
+        return 0, -1
+    lo, hi = int(b[sel].min()), int(b[sel].max())
+    assert sel.sum() == hi - lo + 1
+    return lo, hi
+
+
+def frame_shard(n_samples: int, nperseg: int, hop: int, rank: int, world: int):
+    """Frames [f0, f1) of an n-sample stream owned by `rank`, and the samples [s0, s1) they read."""
+    from .shard import shard_range
+    T = (n_samples - nperseg) // hop + 1 if n_samples >= nperseg else 0
+    f0, f1 = shard_range(T, rank, world)
+    return T, f0, f1, f0 * hop, ((f1 - 1) * hop + nperseg) if f1 > f0 else f0 * hop
+
+
+class IQShardDetector:
+    """One rank's time shard of an I/Q stream on the GPU: spectrogram (frame-major, kept in HBM) →
+    per-frame band delta written straight into the stream plan → detector over the whole stream."""
+
+    def __init__(self, ctx: _lib.Context, n_samples_total: int, fs, nperseg, noverlap, freq_band, noise_band,
+                 threshold_std_factor=4.0, flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
+                 threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
+                 threshold_fixed_init_duration_sec=10, rank: int = 0, world: int = 1, dtype=np.int16,
+                 seg_len: int = 8192):
+        self.ctx, self.fs, self.N = ctx, fs, int(nperseg)
+        self.hop = self.N - int(noverlap)
+        self.block_sec = self.hop / fs
+        self.T, self.f0, self.f1, self.s0, self.s1 = frame_shard(int(n_samples_total), self.N, self.hop, rank, world)
+        self.band = iq_band_bins(self.N, fs, freq_band)
+        self.noise = iq_band_bins(self.N, fs, noise_band)
+        bs = self.block_sec
+        self.adaptive = bool(flag_adaptive_threshold)
+        self.k = float(threshold_std_factor)
+        self.W = _blocks(threshold_estimation_window_sec, bs) if self.adaptive else 0
+        self.F0 = _blocks(threshold_fixed_init_duration_sec, bs) if self.adaptive else 0
+        Fa = _blocks(threshold_freeze_after_detection_sec, bs) if self.adaptive else 0
+        Fb = _blocks(threshold_freeze_before_detection_sec, bs) if self.adaptive else 0
+        self.batch = IQBatch(ctx, 1, max(self.s1 - self.s0, 1), fs, self.N, noverlap, dtype)
+        self.d_frames = ctx.alloc(8)
+        self.d_frames.upload(np.array([self.batch.T if self.s1 > self.s0 else 0], np.int64))
+        cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
+        self.plan = _lib.StreamPlan(ctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
+        self.ops = _stream.DeviceStreamOps(self.plan)
+
+    def upload(self, iq: np.ndarray, sample_offset: int = 0):
+        """interleaved I/Q of this shard's samples, starting at shard sample `sample_offset`"""
+        self.batch.upload(0, iq, sample_offset)
+
+    def spectrogram_and_delta(self):
+        """async: spectrogram of the shard and its per-frame band delta (into the stream plan)"""
+        if self.f1 > self.f0:
+            self.batch.run()
+            _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
+                                   self.noise, self.plan.d_delta, self.batch.T)
+
+    def detect(self, comm=None) -> _stream.StreamResult:
+        return _stream.StreamDetector(self.ops, comm or _stream.LocalComm(), self.adaptive, self.k, self.W,
+                                      self.F0).run()
+
+    def close(self):
+        self.plan.close()
+        self.batch.close()
+
+
+def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072, threshold_std_factor=4.0,
+                    flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
+                    threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
+                    threshold_fixed_init_duration_sec=10, wav_start_date_time=None, out_csv_file=None,
+                    device: int = 0):
+    """The batch detector of dsp/src/main.py (:380-527, :640-658) over an I/Q recording with the STFT
+    frame as the block.  Returns (detections [OutputDetection], thresholds, delta, result)."""
+    buf, code = interleave(i, q)
+    n = buf.size // 2
+    det = IQShardDetector(context(device), n, fs, nperseg, noverlap, freq_band, noise_band, threshold_std_factor,
+                          flag_adaptive_threshold, threshold_estimation_window_sec,
+                          threshold_freeze_before_detection_sec, threshold_freeze_after_detection_sec,
+                          threshold_fixed_init_duration_sec, dtype=buf.dtype)
+    try:
+        if det.T > 0:
+            det.upload(buf[2 * det.s0: 2 * det.s1])
+        det.spectrogram_and_delta()
+        res = det.detect()
+        delta = det.plan.delta()
+    finally:
+        det.close()
+    bs = det.block_sec
+    out = []
+    for d in res.detections:
+        t_start, t_stop = int(d["start"]) * bs, int(d["stop"]) * bs
+        out.append(OutputDetection(t_start=t_start, t_stop=t_stop, dur_s=t_stop - t_start, dB=np.float64(d["db"]),
+                                   utc_start=_utc(wav_start_date_time, t_start),
+                                   utc_stop=_utc(wav_start_date_time, t_stop)))
+    if out_csv_file is not None:
+        write_csv(out, out_csv_file)
+    thr = [np.float64(v) for v in res.thresholds] if det.adaptive else np.float64(res.thr0)
+    return out, thr, delta, res

@@ -1,0 +1,286 @@
+"""The reference's detector over ONE long stream time-sharded over ranks (BASELINE config C5:
+24 h of 192 kHz I/Q whose STFT frames are the detector's blocks, 8 GPUs).
+
+get_detections_adaptive() (dsp/src/main.py:450-522) is a serial loop over the blocks of one
+recording: its global threshold uses the mean/std of the WHOLE recording (:464-466), every
+adaptive threshold looks back W blocks (:475-480), and the freeze / run state flows from one
+block to the next (:485-493).  Sharding the frames over ranks therefore needs exactly three
+exchanges, all small, done here on the host over a communicator's allgather:
+
+1. halos: each rank sends its last W and first ``head_frames`` delta values; a rank keeps
+   the W frames before its shard (the look-back) and the frames after it (chunk tails, runs
+   that cross the edge);
+2. the global threshold: numpy's add.reduce over n values is ``s = 0.0; s += pairwise(chunk)``
+   over 8192-value chunks in order (np_reduce.h), so the ranks' chunk sums (the chunks that
+   start in each shard), gathered in rank order and added in order, give numpy's sum bit for
+   bit -- once for the mean, once for the squared deviations (np.std);
+3. the state at the shard edges: every rank scans its shard from the clean state, then rank
+   r re-scans from rank r-1's exit state until no entry state changes (at most world + 1
+   rounds, normally 2).
+
+The device work per rank is ``_lib.StreamPlan`` (libmsdsp, stream.hip); ``ops`` may be any
+object with the same methods (the CPU tests drive this protocol with a numpy stand-in over
+gloo).  Results are identical on every rank: the merged detections of the whole stream.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+CHUNK = 8192  # numpy's reduction buffer
+
+
+# ---------------------------------------------------------------- communicators
+class LocalComm:
+    """world size 1"""
+    rank, world = 0, 1
+
+    def allgather(self, a: np.ndarray) -> list[np.ndarray]:
+        return [np.array(a, copy=True)]
+
+
+class TorchComm:
+    """torch.distributed process group (gloo on the host; tests and CPU runs)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+
+    def allgather(self, a: np.ndarray) -> list[np.ndarray]:
+        import torch
+        a = np.ascontiguousarray(a)
+        n = torch.tensor([a.size], dtype=torch.int64)
+        ns = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
+        self.dist.all_gather(ns, n, group=self.group)
+        m = max(int(t.item()) for t in ns)
+        buf = np.zeros(max(m, 1), a.dtype)
+        buf[: a.size] = a
+        t = torch.from_numpy(buf)
+        outs = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(outs, t, group=self.group)
+        return [o.numpy()[: int(k.item())].copy() for o, k in zip(outs, ns)]
+
+
+class RcclComm:
+    """RCCL over the GPUs of one job (msd_comm_allgather on device buffers)."""
+
+    def __init__(self, comm, rank: int, world: int):
+        self.comm, self.rank, self.world = comm, int(rank), int(world)
+        self.ctx = comm.ctx
+
+    def _gather_bytes(self, b: np.ndarray) -> np.ndarray:
+        b = np.ascontiguousarray(b).view(np.uint8)
+        n = b.size
+        send = self.ctx.alloc(max(n, 8))
+        recv = self.ctx.alloc(max(n, 8) * self.world)
+        if n:
+            send.upload(b)
+        _lib.check(self.ctx.lib.msd_comm_allgather(self.comm.h, send.ptr, recv.ptr, n))
+        out = np.empty(n * self.world, np.uint8)
+        if n:
+            recv.download(out)
+        return out
+
+    def allgather(self, a: np.ndarray) -> list[np.ndarray]:
+        a = np.ascontiguousarray(a)
+        ns = self._gather_bytes(np.array([a.size], np.int64)).view(np.int64)
+        m = int(ns.max()) if ns.size else 0
+        buf = np.zeros(max(m, 1), a.dtype)
+        buf[: a.size] = a
+        got = self._gather_bytes(buf).view(a.dtype).reshape(self.world, -1)
+        return [got[r, : int(ns[r])].copy() for r in range(self.world)]
+
+
+# ---------------------------------------------------------------- detector state
+def clean_state(thr0: float) -> tuple[int, int, float]:
+    """(freeze_until_idx, last run's stop, threshold) before block 0 (main.py:454-468)."""
+    return (-1, -2, float(thr0))
+
+
+def same_state(x, y, a: int, F0: int) -> bool:
+    """Do states x and y entering frame a lead to the same future (stream.hip same_state)?"""
+    fx, fy = x[0] >= a, y[0] >= a
+    if fx != fy:
+        return False
+    if fx:
+        if x[0] != y[0]:
+            return False
+        if a >= F0 and np.float64(x[2]).view(np.int64) != np.float64(y[2]).view(np.int64):
+            return False
+    return (x[1] == a - 1) == (y[1] == a - 1)
+
+
+def _pack(s) -> np.ndarray:
+    return np.array([s[0], s[1], np.float64(s[2]).view(np.int64)], np.int64)
+
+
+def _unpack(a: np.ndarray):
+    return (int(a[0]), int(a[1]), float(np.int64(a[2]).view(np.float64)))
+
+
+@dataclass
+class StreamResult:
+    detections: np.ndarray     # DET_DTYPE [start, stop) frame ranges + dB, the whole stream
+    thr0: float                # mean + k*std of the whole stream (main.py:464-466 / :399-400)
+    thresholds: np.ndarray     # this rank's thresholds actually used (adaptive) / [thr0] (global)
+    margin: float              # min |delta - threshold| over the stream
+    rounds: int                # state-exchange rounds
+
+
+class StreamDetector:
+    """Runs the protocol above for one rank.  ``ops`` holds this rank's shard (delta already
+    set) — a ``_lib.StreamPlan`` or a stand-in with the same methods."""
+
+    def __init__(self, ops, comm, adaptive: bool, k_std: float, window_blocks: int = 0,
+                 fixed_init_blocks: int = 0, head_frames: int = CHUNK):
+        self.ops, self.comm = ops, comm
+        self.adaptive, self.k = bool(adaptive), float(k_std)
+        self.W, self.F0 = int(window_blocks), int(fixed_init_blocks)
+        self.H = int(head_frames)
+
+    # 1. halos
+    def exchange_halos(self):
+        ops, r = self.ops, self.comm.rank
+        d = ops.delta()
+        tails = self.comm.allgather(d[max(0, d.size - self.W):] if self.W > 0 else d[:0])
+        heads = self.comm.allgather(d[: self.H])
+        before = np.concatenate([np.zeros(0)] + tails[:r])
+        after = np.concatenate([np.zeros(0)] + heads[r + 1:])
+        tail = before[before.size - ops.n_tail:] if ops.n_tail else before[:0]
+        ops.set_halos(tail, after[: ops.n_head])
+
+    # 2. numpy's sum over the whole stream from the ranks' chunk sums
+    def _global_sum(self, mean=None) -> float:
+        _, sums = self.ops.chunk_sums(mean)
+        s = 0.0
+        for part in self.comm.allgather(sums):
+            for v in part:
+                s += float(v)
+        return s
+
+    def global_threshold(self) -> float:
+        n = self.ops.n_total
+        mean = self._global_sum() / n
+        std = math.sqrt(self._global_sum(mean) / n)
+        return mean + self.k * std
+
+    # 3. the state at the shard edges
+    def scan(self, thr0: float) -> int:
+        ops, comm, r = self.ops, self.comm, self.comm.rank
+        F0 = self.F0 if self.adaptive else ops.n_total
+        entry = clean_state(thr0)
+        exit_, _ = ops.scan(thr0, entry, True)
+        rounds = 1
+        while True:
+            exits = [_unpack(e) for e in comm.allgather(_pack(exit_))]
+            new = exits[r - 1] if r > 0 else entry
+            changed = r > 0 and not same_state(new, entry, ops.frame0, F0)
+            flags = comm.allgather(np.array([1 if changed else 0], np.int64))
+            if not any(int(f[0]) for f in flags):
+                return rounds
+            rounds += 1
+            if changed:
+                entry = new
+                exit_, _ = ops.scan(thr0, entry, False)
+
+    def run(self) -> StreamResult:
+        ops, comm = self.ops, self.comm
+        if ops.n_total == 0:
+            if not self.adaptive:  # above_thresh[0] on an empty array (main.py:412)
+                raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+            return StreamResult(np.zeros(0, _lib.DET_DTYPE), float("nan"), np.zeros(0), math.inf, 0)
+        self.exchange_halos()
+        thr0 = self.global_threshold()
+        if self.adaptive:
+            ops.fresh()
+        rounds = self.scan(thr0)
+        # runs of every shard, merged in stream order (a run continued across an edge has start -1)
+        local, margin = ops.runs()
+        parts = comm.allgather(np.stack([local["start"], local["stop"]], 1).reshape(-1).astype(np.int64))
+        margin = min(float(m[0]) for m in comm.allgather(np.array([margin])))
+        merged: list[list[int]] = []
+        for p in parts:
+            for s, e in p.reshape(-1, 2):
+                if s < 0:
+                    merged[-1][1] = int(e)
+                else:
+                    merged.append([int(s), int(e)])
+        if not self.adaptive and merged and merged[-1][1] == ops.n_total:
+            merged[-1][1] = ops.n_total - 1  # burst_stops gets len-1 (main.py:414-415)
+            if merged[-1][1] - merged[-1][0] <= 0:
+                raise AssertionError("Detection duration must be greater than 0")  # main.py:437
+        dets = np.zeros(len(merged), _lib.DET_DTYPE)
+        if merged:
+            a = np.array(merged, np.int64)
+            dets["start"], dets["stop"] = a[:, 0], a[:, 1]
+        # dB means: the rank whose shard holds the run's start
+        lo, hi = ops.frame0, ops.frame0 + ops.n_local
+        mine = (dets["start"] >= lo) & (dets["start"] < hi)
+        db_local = ops.db(dets[mine])["db"] if mine.any() else np.zeros(0)
+        db_all = np.full(len(dets), np.nan)
+        owners = comm.allgather(np.flatnonzero(mine).astype(np.int64))
+        vals = comm.allgather(np.asarray(db_local, np.float64))
+        for idx, v in zip(owners, vals):
+            db_all[idx] = v
+        dets["db"] = db_all
+        thr = ops.thresholds() if self.adaptive else np.array([thr0])
+        return StreamResult(dets, thr0, thr, margin, rounds)
+
+
+class DeviceStreamOps:
+    """``_lib.StreamPlan`` with the protocol's method signatures."""
+
+    def __init__(self, plan: _lib.StreamPlan):
+        self.plan = plan
+        self.n_total, self.frame0, self.n_local = plan.n_total, plan.frame0, plan.n_local
+        self.n_tail, self.n_head = plan.n_tail, plan.n_head
+        self.last_rounds = 0
+
+    def delta(self):
+        return self.plan.delta()
+
+    def set_halos(self, tail, head):
+        self.plan.set_halos(tail, head)
+
+    def chunk_sums(self, mean=None):
+        return self.plan.chunk_sums(mean)
+
+    def fresh(self):
+        self.plan.fresh()
+
+    def scan(self, thr0, entry, reset):
+        ex, rounds = self.plan.scan(thr0, _lib.MsdStreamState(entry[0], entry[1], entry[2], 0), reset)
+        self.last_rounds += rounds
+        return (ex.freeze_until, ex.last_stop, ex.thr), rounds
+
+    def runs(self):
+        return self.plan.runs()
+
+    def db(self, dets):
+        return self.plan.db(dets)
+
+    def thresholds(self):
+        return self.plan.thresholds()
+
+
+def detect_stream(ctx: _lib.Context, delta_local: np.ndarray, n_total: int, frame0: int, comm=None,
+                  adaptive: bool = True, k_std: float = 4.0, window_blocks: int = 0, freeze_after_blocks: int = 0,
+                  freeze_before_blocks: int = 0, fixed_init_blocks: int = 0, seg_len: int = 8192,
+                  cap_per_seg: int = 256, head_frames: int = CHUNK) -> StreamResult:
+    """Host-buffer convenience: this rank's delta shard [frame0, frame0 + len) of an n_total-frame
+    stream → the detections of the whole stream (identical on every rank)."""
+    comm = comm or LocalComm()
+    d = np.ascontiguousarray(delta_local, dtype=np.float64)
+    cfg = _lib.det_cfg(adaptive, k_std, window_blocks, freeze_before_blocks, freeze_after_blocks, fixed_init_blocks)
+    plan = _lib.StreamPlan(ctx, cfg, n_total, frame0, d.size, seg_len, cap_per_seg, head_frames)
+    try:
+        plan.set_delta(d)
+        return StreamDetector(DeviceStreamOps(plan), comm, adaptive, k_std, window_blocks, fixed_init_blocks,
+                              head_frames).run()
+    finally:
+        plan.close()

@@ -1,0 +1,204 @@
+"""GPU: the C5 stream detector (stream.hip through the C-ABI, meteorgpu.stream / meteorgpu.iq)
+against the oracle of dsp/src/main.py:396-522 over the whole stream.
+
+Bars: run bounds, dB means, every threshold and the global threshold bit-exact on identical delta
+(float64, numpy's pairwise order); the I/Q band delta within DELTA_TOL dB of the float64 scipy
+spectrogram (the spectrogram is float32 on the device: <= 1e-5 relative per bin); end to end on
+I/Q the same detections as the oracle (the test asserts the oracle's margin to its thresholds
+exceeds the delta tolerance, so identical decisions are required, not lucky)."""
+import numpy as np
+import pytest
+
+from detector_kats import ADAPTIVE, GLOBAL
+from stream_np_ops import run_threads, shard_bounds
+from test_stream_protocol import make_delta, oracle
+
+pytestmark = pytest.mark.gpu
+
+DELTA_TOL = 1e-4  # dB
+
+
+def _ctx():
+    from meteorgpu.dsp import context
+    return context(0)
+
+
+def _detect(d, adaptive, k, W, Fa, F0, seg_len=8192, cap=256):
+    from meteorgpu import stream
+    return stream.detect_stream(_ctx(), d, d.size, 0, adaptive=adaptive, k_std=k, window_blocks=W,
+                                freeze_after_blocks=Fa, fixed_init_blocks=F0, seg_len=seg_len, cap_per_seg=cap)
+
+
+def _check(res, d, adaptive, k, W, Fa, F0):
+    want, thr = oracle(d, adaptive, k, W, Fa, F0)
+    got = [(int(a), int(b)) for a, b, _ in res.detections]
+    assert got == [(a, b) for a, b, _ in want]
+    assert np.array_equal(res.detections["db"], np.array([w[2] for w in want], np.float64))
+    if adaptive:
+        assert np.array_equal(res.thresholds, np.asarray(thr, np.float64), equal_nan=True)
+    else:
+        assert res.thr0 == thr
+    return want
+
+
+def test_global_threshold_bit_exact():
+    for n, seed in [(100, 1), (8192, 2), (8193, 3), (50000, 4)]:
+        d = make_delta(n, seed)
+        res = _detect(d, True, 4.0, 50, 10, 5)
+        assert res.thr0 == np.mean(d) + 4.0 * np.std(d)
+
+
+@pytest.mark.parametrize("seg_len", [64, 512, 8192])
+def test_adaptive_segments(seg_len):
+    d = make_delta(30000, 21, rate=0.01)
+    want = _check(_detect(d, True, 4.0, 600, 100, 50, seg_len=seg_len), d, True, 4.0, 600, 100, 50)
+    assert len(want) > 50
+
+
+def test_adaptive_dense_freezes():
+    # freeze longer than segments, detections every few hundred frames: chains across many segments
+    d = make_delta(40000, 22, rate=0.02)
+    _check(_detect(d, True, 2.5, 800, 700, 30, seg_len=128), d, True, 2.5, 800, 700, 30)
+
+
+def test_long_window():
+    # W = 9000 > 8192: every window is two numpy chunks, fresh_kernel's program has 2 chunk ends
+    d = make_delta(36000, 23)
+    _check(_detect(d, True, 4.0, 9000, 300, 100), d, True, 4.0, 9000, 300, 100)
+
+
+def test_c5_window():
+    # the C5 block counts: W = int(120 / (1024/192000)) = 22500, Fa = 3750, F0 = 1875
+    d = make_delta(60000, 24, rate=0.001)
+    _check(_detect(d, True, 4.0, 22500, 3750, 1875), d, True, 4.0, 22500, 3750, 1875)
+
+
+def test_global_mode():
+    d = make_delta(30000, 25)
+    _check(_detect(d, False, 4.0, 0, 0, 0), d, False, 4.0, 0, 0, 0)
+    e = d.copy()
+    e[-3:] = 60.0
+    _check(_detect(e, False, 4.0, 0, 0, 0), e, False, 4.0, 0, 0, 0)
+
+
+@pytest.mark.parametrize("case", ADAPTIVE, ids=[c[0] for c in ADAPTIVE])
+def test_adaptive_kats(case):
+    name, delta, k, (wsec, fb, fa, f0), dets, thr = case
+    d = np.asarray(delta, np.float64)
+    res = _detect(d, True, k, int(wsec), int(fa), int(f0))
+    assert [(int(a), int(b)) for a, b, _ in res.detections] == [(a, b) for a, b, _ in dets]
+    assert np.allclose(res.detections["db"], [x[2] for x in dets])
+    assert np.allclose(res.thresholds, thr, equal_nan=True, rtol=0, atol=1e-12)
+    _check(res, d, True, k, int(wsec), int(fa), int(f0))
+
+
+@pytest.mark.parametrize("case", GLOBAL, ids=[c[0] for c in GLOBAL])
+def test_global_kats(case):
+    name, delta, k, dets, thr, err = case
+    d = np.asarray(delta, np.float64)
+    if err is not None:
+        with pytest.raises(err):
+            _detect(d, False, k, 0, 0, 0)
+        return
+    res = _detect(d, False, k, 0, 0, 0)
+    assert [(int(a), int(b), float(x)) for a, b, x in res.detections] == [(a, b, float(x)) for a, b, x in dets]
+    assert res.thr0 == pytest.approx(thr)
+
+
+def test_sharded_threads():
+    """world 4 in one process (one context per rank-thread), shard edges inside runs and freezes,
+    one empty shard: the rounds of the shard-edge state exchange, on the device kernels"""
+    from meteorgpu import _lib, stream
+    d = make_delta(40000, 26, rate=0.02)
+    want, _ = oracle(d, True, 3.0, 600, 400, 50)
+    a = want[10][0] + 1
+    b = want[30][0] + 20
+    cuts = [a, b, b]
+
+    def body(r, comm):
+        lo, hi = shard_bounds(d.size, 4, r, cuts)
+        ctx = _lib.Context(0)
+        try:
+            cfg = _lib.det_cfg(True, 3.0, 600, 0, 400, 50)
+            plan = _lib.StreamPlan(ctx, cfg, d.size, lo, hi - lo, seg_len=256)
+            plan.set_delta(d[lo:hi])
+            res = stream.StreamDetector(stream.DeviceStreamOps(plan), comm, True, 3.0, 600, 50).run()
+            plan.close()
+            return res
+        finally:
+            ctx.close()
+
+    res = run_threads(4, body)
+    for r in res:
+        assert [(int(x), int(y)) for x, y, _ in r.detections] == [(p, q) for p, q, _ in want]
+        assert np.array_equal(r.detections["db"], np.array([w[2] for w in want]))
+    _, thr = oracle(d, True, 3.0, 600, 400, 50)
+    assert np.array_equal(np.concatenate([r.thresholds for r in res]), np.asarray(thr), equal_nan=True)
+
+
+def test_empty_and_tiny():
+    from meteorgpu import stream
+    r = _detect(np.zeros(0), True, 4.0, 10, 5, 2)
+    assert len(r.detections) == 0
+    with pytest.raises(IndexError):
+        _detect(np.zeros(0), False, 4.0, 0, 0, 0)
+    d = make_delta(37, 27)
+    _check(_detect(d, True, 1.0, 10, 3, 2), d, True, 1.0, 10, 3, 2)
+    assert stream is not None
+
+
+@pytest.mark.parametrize("seed,adaptive", [(1, True), (2, True), (3, False)])
+def test_iq_end_to_end(seed, adaptive):
+    from meteorgpu import iq, synth
+    from oracle import iq_oracle as Q
+    i, q, _ = synth.synth_iq(seed, 192000, 40.0, 1000.0, rate_per_min=20)
+    kw = dict(flag_adaptive_threshold=adaptive, threshold_estimation_window_sec=5,
+              threshold_freeze_after_detection_sec=2, threshold_fixed_init_duration_sec=1)
+    dets, thr, delta, res = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), **kw)
+    rdets, rthr, _, _, rdelta = Q.proc_iq_ref(i, q, 192000, (950, 1050), (-3050, -2950), **kw)
+    assert delta.shape == rdelta.shape
+    assert np.max(np.abs(delta - rdelta)) < DELTA_TOL
+    rt = np.asarray(rthr) if adaptive else rthr
+    assert np.nanmin(np.abs(rdelta - rt)) > 10 * DELTA_TOL  # decisions are not near-ties
+    assert [(d.t_start, d.t_stop) for d in dets] == [(r[0], r[1]) for r in rdets]
+    assert np.allclose([d.dB for d in dets], [r[3] for r in rdets], rtol=0, atol=DELTA_TOL)
+    # on the device's own delta the detector is bit-exact with the oracle's
+    bs = 1024 / 192000
+    from oracle import dsp_oracle as O
+    if adaptive:
+        odets, othr = O.get_detections_adaptive_ref(delta, 4.0, bs, 5, 3, 2, 1)
+        assert np.array_equal(np.asarray(thr), np.asarray(othr), equal_nan=True)
+    else:
+        odets, othr = O.get_detections_ref(delta, 4.0, bs)
+        assert thr == othr
+    assert [(d.t_start, d.t_stop, d.dB) for d in dets] == [(r[0], r[1], r[3]) for r in odets]
+
+
+def test_iq_sharded_threads():
+    """an I/Q stream time-sharded over 3 rank-threads (each its own spectrogram of its samples):
+    the same detections as one process"""
+    from meteorgpu import _lib, iq, synth
+    i, q, _ = synth.synth_iq(4, 192000, 30.0, 1000.0, rate_per_min=30)
+    buf, _ = iq.interleave(i, q)
+    kw = dict(threshold_estimation_window_sec=3, threshold_freeze_after_detection_sec=1,
+              threshold_fixed_init_duration_sec=1)
+    one, *_ = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), **kw)
+
+    def body(r, comm):
+        ctx = _lib.Context(0)
+        try:
+            det = iq.IQShardDetector(ctx, i.size, 192000, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
+                                     3, 3, 1, 1, rank=r, world=3, seg_len=512)
+            det.upload(buf[2 * det.s0: 2 * det.s1])
+            det.spectrogram_and_delta()
+            res = det.detect(comm)
+            det.close()
+            return res
+        finally:
+            ctx.close()
+
+    res = run_threads(3, body)
+    bs = 1024 / 192000
+    for r in res:
+        assert [(int(a) * bs, int(b) * bs) for a, b, _ in r.detections] == [(d.t_start, d.t_stop) for d in one]
+        assert np.array_equal(r.detections["db"], np.array([d.dB for d in one]))

@@ -1,0 +1,144 @@
+"""CPU: the host protocol of the C5 stream detector (meteorgpu/stream.py) — halos, the whole-stream
+threshold from per-shard chunk sums, the shard-edge state rounds and the run merge — run at
+world sizes 1-4 (threads) and 2 (gloo processes) with the numpy stand-in for the device plan
+(tests/stream_np_ops.py), against the single-process oracle of dsp/src/main.py:396-522 over the
+whole stream.  Bit-exact: run bounds, dB means, thresholds and the global threshold."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from stream_np_ops import NumpyStreamOps, run_threads, shard_bounds
+
+from meteorgpu import stream
+from oracle import dsp_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def make_delta(n, seed, rate=0.004, amp=(3.0, 9.0)):
+    """noise + bursts (a few frames up to ~40) — per-frame band delta in dB"""
+    rng = np.random.default_rng(seed)
+    d = rng.normal(0.0, 1.0, n)
+    t = 0
+    while True:
+        t += int(rng.exponential(1 / rate))
+        if t >= n:
+            break
+        L = int(rng.integers(1, 40))
+        d[t: t + L] += rng.uniform(*amp)
+    return d
+
+
+def oracle(d, adaptive, k, W, Fa, F0):
+    if adaptive:
+        dets, thr = O.get_detections_adaptive_ref(d, k, 1.0, W, 0, Fa, F0)
+    else:
+        dets, thr = O.get_detections_ref(d, k, 1.0)
+    return [(int(a), int(b), db) for a, b, _, db, _, _ in dets], thr
+
+
+def run_protocol(d, world, adaptive, k, W, Fa, F0, cuts=None):
+    n = d.size
+
+    def body(r, comm):
+        lo, hi = shard_bounds(n, world, r, cuts)
+        ops = NumpyStreamOps(d[lo:hi], n, lo, adaptive, k, W, Fa, F0)
+        return stream.StreamDetector(ops, comm, adaptive, k, W, F0).run()
+
+    return run_threads(world, body)
+
+
+def check(res, d, adaptive, k, W, Fa, F0):
+    want, thr = oracle(d, adaptive, k, W, Fa, F0)
+    for r in res:  # every rank returns the whole stream's detections
+        got = [(int(a), int(b), float(db)) for a, b, db in r.detections]
+        assert [(a, b) for a, b, _ in got] == [(a, b) for a, b, _ in want]
+        assert np.array_equal(np.array([g[2] for g in got]), np.array([w[2] for w in want]))
+    if adaptive:
+        allthr = np.concatenate([r.thresholds for r in res])
+        assert np.array_equal(allthr, np.asarray(thr, np.float64), equal_nan=True)
+    else:
+        assert res[0].thr0 == thr
+    return want
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_adaptive_shards(world):
+    d = make_delta(30000, 11)
+    want = check(run_protocol(d, world, True, 4.0, 600, 100, 50), d, True, 4.0, 600, 100, 50)
+    assert len(want) > 20
+
+
+def test_runs_and_freezes_across_edges():
+    d = make_delta(30000, 12, rate=0.02)
+    want, _ = oracle(d, True, 3.0, 600, 100, 50)
+    # cut inside detections (continued runs) and inside freezes, plus an empty shard
+    a = want[5][0] + 1
+    b = want[12][0] + 30
+    cuts = [a, a, b, b + 1]
+    check(run_protocol(d, 5, True, 3.0, 600, 100, 50, cuts), d, True, 3.0, 600, 100, 50)
+
+
+def test_long_window_two_chunks():
+    # W > 8192: every window is two numpy reduction chunks; shards shorter than W
+    d = make_delta(26000, 13)
+    check(run_protocol(d, 3, True, 4.0, 9000, 300, 100, cuts=[5000, 9000]), d, True, 4.0, 9000, 300, 100)
+
+
+def test_global_mode_and_end_quirk():
+    d = make_delta(20000, 14)
+    check(run_protocol(d, 3, False, 4.0, 0, 0, 0), d, False, 4.0, 0, 0, 0)
+    e = d.copy()
+    e[-5:] = 50.0  # a run reaching the end: stop = len-1 (main.py:414-415)
+    check(run_protocol(e, 2, False, 4.0, 0, 0, 0), e, False, 4.0, 0, 0, 0)
+    f = d.copy()
+    f[-2] = -50.0
+    f[-1] = 50.0  # one block at the end: t_dur == 0 → assert (main.py:437)
+    with pytest.raises(AssertionError):
+        run_protocol(f, 2, False, 4.0, 0, 0, 0)
+
+
+def test_state_helpers():
+    assert stream.same_state((-1, -2, 1.0), (5, -2, 2.0), 10, 0)       # both unfrozen
+    assert not stream.same_state((12, -2, 1.0), (12, -2, 2.0), 10, 0)  # frozen, thresholds differ
+    assert stream.same_state((12, -2, 1.0), (12, -2, 2.0), 10, 50)     # before F0 thr0 rules
+    assert not stream.same_state((-1, 9, 1.0), (-1, -2, 1.0), 10, 0)   # adjacency of the last run
+    s = (123, -2, float("nan"))
+    assert stream._unpack(stream._pack(s))[:2] == s[:2]
+
+
+def _gloo_rank(rank, world, port, out):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "meteor-scatter_amd"), os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from stream_np_ops import NumpyStreamOps as Ops
+    from meteorgpu import stream as S
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        d = make_delta(25000, 15, rate=0.01)
+        lo, hi = shard_bounds(d.size, world, rank)
+        res = S.StreamDetector(Ops(d[lo:hi], d.size, lo, True, 4.0, 600, 100, 50), S.TorchComm(), True, 4.0,
+                               600, 50).run()
+        np.save(os.path.join(out, f"r{rank}.npy"), np.stack([res.detections["start"], res.detections["stop"]]))
+        np.save(os.path.join(out, f"db{rank}.npy"), res.detections["db"])
+        np.save(os.path.join(out, f"t{rank}.npy"), res.thresholds)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_gloo_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    d = make_delta(25000, 15, rate=0.01)
+    want, thr = oracle(d, True, 4.0, 600, 100, 50)
+    for r in range(2):
+        se = np.load(tmp_path / f"r{r}.npy")
+        assert [(int(a), int(b)) for a, b in se.T] == [(a, b) for a, b, _ in want]
+        assert np.array_equal(np.load(tmp_path / f"db{r}.npy"), np.array([w[2] for w in want]))
+    t = np.concatenate([np.load(tmp_path / f"t{r}.npy") for r in range(2)])
+    assert np.array_equal(t, np.asarray(thr), equal_nan=True)
