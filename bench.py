@@ -212,32 +212,48 @@ def main_live(a, world, rank, local, dist):
 
 
 C5_FS, C5_N, C5_HOP, C5_SECONDS = 192000, 4096, 1024, 3 * 3600
+C5_BAND, C5_NOISE = (950.0, 1050.0), (-3050.0, -2950.0)  # Hz from the SDR centre (two-sided spectrum)
 
 
 def main_c5(a, world, rank, local, dist):
-    """BASELINE config C5: a 24 h 192 kHz I/Q stream time-sharded over the GPUs — each rank
-    owns 3 h (its shard plus the N - hop sample halo the STFT needs is contiguous, so no
-    exchange); two-sided 4096-point power spectrogram at 75 % overlap, frame-major float32."""
-    from meteorgpu import _lib, iq
+    """BASELINE config C5: a 24 h 192 kHz I/Q stream time-sharded over the GPUs (3 h of it per
+    GPU; weak scaling: the stream is 3 h x N long).  A step = the whole path on every rank:
+    two-sided 4096-point power spectrogram at 75 % overlap (frame-major float32, kept in HBM),
+    the per-frame band / noise dB delta, and the reference's adaptive detector over the WHOLE
+    stream (meteorgpu.stream: halo, chunk-sum and shard-edge state exchanges over RCCL)."""
+    from meteorgpu import _lib, iq, stream, synth
+    from meteorgpu.batch import Communicator
     ctx = _lib.Context(local)
-    n = C5_FS * C5_SECONDS + (C5_N - C5_HOP)  # shard + halo
-    b = iq.IQBatch(ctx, 1, n, C5_FS, nperseg=C5_N, noverlap=C5_N - C5_HOP)
-    rng = np.random.default_rng(5000 + rank)
+    shard = C5_FS * C5_SECONDS
+    n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
+    det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
+                             rank=rank, world=world)
     chunk = C5_FS * 60
     pool = []
-    for j in range(4):  # 1-minute chunks: a carrier sweep + noise, int16 I/Q interleaved
-        tt = np.arange(chunk) / C5_FS
-        ph = 2 * np.pi * (1000.0 * (j + 1)) * tt
+    for j in range(4):  # seeded 1-minute chunks: noise + meteor pings at +1 kHz, int16 I/Q interleaved
+        i_, q_, _ = synth.synth_iq(5000 + 10 * rank + j, C5_FS, 60.0, 1000.0, sigma=1000.0, rate_per_min=6,
+                                   snr_db=(10.0, 30.0))
         z = np.empty(2 * chunk, np.int16)
-        z[0::2] = np.clip(np.round(2000 * np.cos(ph) + rng.normal(0, 500, chunk)), -32768, 32767)
-        z[1::2] = np.clip(np.round(2000 * np.sin(ph) + rng.normal(0, 500, chunk)), -32768, 32767)
+        z[0::2], z[1::2] = i_, q_
         pool.append(z)
+    n = det.s1 - det.s0
     pos, k = 0, 0
     while pos < n:
         m = min(chunk, n - pos)
-        b.upload(0, pool[k % len(pool)][: 2 * m], sample_offset=pos)
+        det.upload(pool[k % len(pool)][: 2 * m], sample_offset=pos)
         pos += m
         k += 1
+    comm = stream.LocalComm()
+    rccl = None
+    if dist is not None:
+        obj = [Communicator.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        rccl = Communicator(ctx, world, obj[0], rank)
+        comm = stream.RcclComm(rccl, rank, world)
+
+    def step():
+        det.spectrogram_and_delta()
+        return det.detect(comm, thresholds=False)
 
     def sync_all():
         ctx.synchronize()
@@ -246,15 +262,16 @@ def main_c5(a, world, rank, local, dist):
             torch.cuda.synchronize()
             dist.barrier()
 
+    res = None
     for _ in range(a.warmup):
-        b.run()
+        res = step()
     sync_all()
     ctx.timing(True)
     ctx.timing_reset()
     sync_all()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        b.run()
+        res = step()
     sync_all()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -262,37 +279,53 @@ def main_c5(a, world, rank, local, dist):
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    kms = {}
+    for name, kid in (("cstft", _lib.K_CSTFT), ("band_delta", _lib.K_IQDELTA), ("fresh_thresholds", _lib.K_FRESH),
+                      ("scan", _lib.K_SSCAN)):
+        ms, cnt = ctx.timing_get(kid)
+        kms[name] = round(ms / max(a.steps, 1), 4)
     k_ms, k_n = ctx.timing_get(_lib.K_CSTFT)
     avg_s = k_ms / max(k_n, 1) / 1e3
-    samples = C5_FS * C5_SECONDS  # the shard (the halo is read, not counted)
-    alg_bytes = n * 4 + b.T * C5_N * 4
+    T = det.f1 - det.f0
+    samples = shard  # per rank: its 3 h (the 3072-sample frame tail is read, not counted)
+    alg_bytes = (det.s1 - det.s0) * 4 + T * C5_N * 4
     out = {
-        "metric": "Msamples/s processed (192 kHz I/Q, 4096-pt two-sided spectrogram, 75% overlap)",
+        "metric": "Msamples/s processed (192 kHz I/Q: 4096-pt two-sided spectrogram, 75% overlap, band delta, "
+                  "adaptive detector)",
         "value": round(world * samples * a.steps / elapsed / 1e6, 1),
         "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: 4 seeded 1-minute 192 kHz int16 I/Q chunks (carrier + noise) tiled into a 3 h shard per GPU",
-        "config": {"workload": "C5: 24 h 192 kHz I/Q stream time-sharded 3 h per GPU (+3072-sample halo), "
-                               "spectrogram 4096/1024, float32 [T][4096] frame-major",
-                   "samples_per_gpu": samples, "frames_per_gpu": b.T, "bins": C5_N,
+        "vs_baseline": None, "dtype": "f32 spectrogram / f64 detector",
+        "data": "synthetic: 4 seeded 1-minute 192 kHz int16 I/Q chunks (noise + pings) tiled into 3 h per GPU",
+        "config": {"workload": "C5: 192 kHz I/Q stream time-sharded 3 h per GPU (3 h x N long), spectrogram "
+                               "4096/1024 float32 [T][4096] frame-major + per-frame band dB (950..1050 Hz vs "
+                               "-3050..-2950 Hz) + adaptive detector over the whole stream (k 4, window 120 s = "
+                               f"{det.W} frames, freeze 20 s, fixed init 10 s)",
+                   "samples_per_gpu": samples, "frames_per_gpu": T, "frames_total": det.T, "bins": C5_N,
                    "parallelism": f"time shards over {world} GPU(s), 1 process per GPU"},
+        "detections_per_step": int(len(res.detections)),
+        "state_rounds": int(res.rounds),
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": load_pmc_traffic("cstft", frames=b.T, nperseg=C5_N),
+                     "traffic": load_pmc_traffic("cstft", frames=T, nperseg=C5_N),
                      "kernel": "cstft4096_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
+        "kernel_ms_per_step": kms,
     }
     if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0:
         from oracle import iq_oracle as Q
         m = C5_FS * 60  # one minute of the stream
         z = pool[0]
         t1 = time.perf_counter()
-        Q.spectrogram_iq_ref(z[0:2 * m:2], z[1:2 * m:2], C5_FS, C5_N, C5_N - C5_HOP)
+        Q.proc_iq_ref(z[0:2 * m:2], z[1:2 * m:2], C5_FS, C5_BAND, C5_NOISE, C5_N, C5_N - C5_HOP, 4.0)
         dt = time.perf_counter() - t1
         out["cpu_baseline"] = {"value": round(m / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
                                "sample": f"60 s of the 192 kHz I/Q stream ({dt:.1f} s): scipy.signal.spectrogram "
-                                         f"(complex input, 4096/3072), 1 thread"}
+                                         f"(complex input, 4096/3072) + per-frame band sums + adaptive detector "
+                                         f"(oracle/iq_oracle.py), 1 thread"}
+    det.close()
+    if rccl is not None:
+        rccl.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -72,36 +72,31 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 }
 
 // ------------------------------------------------------------------ band delta per frame
+// one thread per frame: the band bins of a frame are one or two short contiguous runs of its row
+// (~100-400 B), so a thread's loads are few and independent; thousands of frames in flight hide
+// the latency.  Sums in float64, ascending bin order.
+__device__ __forceinline__ double band_energy(const float *__restrict__ row, int N, int lo, int hi) {
+    double acc = 0.0;
+    for (int k = lo; k <= hi; ++k) acc += (double)__builtin_nontemporal_load(row + (k < 0 ? k + N : k));
+    return acc;
+}
+
 __global__ __launch_bounds__(256) void iq_band_delta_kernel(const float *__restrict__ spec, int64_t nstreams,
                                                             int64_t max_frames, const int64_t *__restrict__ frames,
                                                             int N, int blo, int bhi, int nlo, int nhi,
                                                             double *__restrict__ band_db,
                                                             double *__restrict__ noise_db,
                                                             double *__restrict__ delta, int64_t ld) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * 4;
-    for (int64_t g = wave; g < nstreams * max_frames; g += nwaves) {
-        const int64_t s = g / max_frames, t = g - s * max_frames;
-        if (t >= frames[s]) continue;
-        const float *row = spec + (s * max_frames + t) * (int64_t)N;
-        double e[2];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int lo = b ? nlo : blo, hi = b ? nhi : bhi;
-            double acc = 0.0;
-            for (int k = lo + lane; k <= hi; k += 64) acc += (double)row[k < 0 ? k + N : k];
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) acc += shfl_xor_d(acc, o);
-            e[b] = acc;
-        }
-        if (lane == 0) {
-            const double bd = 10.0 * log10(e[0] + 1e-12), nd = 10.0 * log10(e[1] + 1e-12);
-            if (band_db) band_db[s * ld + t] = bd;
-            if (noise_db) noise_db[s * ld + t] = nd;
-            delta[s * ld + t] = bd - nd;
-        }
-    }
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nstreams * max_frames) return;
+    const int64_t s = g / max_frames, t = g - s * max_frames;
+    if (t >= frames[s]) return;
+    const float *row = spec + (s * max_frames + t) * (int64_t)N;
+    const double e0 = band_energy(row, N, blo, bhi), e1 = band_energy(row, N, nlo, nhi);
+    const double bd = 10.0 * log10(e0 + 1e-12), nd = 10.0 * log10(e1 + 1e-12);
+    if (band_db) band_db[s * ld + t] = bd;
+    if (noise_db) noise_db[s * ld + t] = nd;
+    delta[s * ld + t] = bd - nd;
 }
 
 // ------------------------------------------------------------------ chunk sums
@@ -596,10 +591,7 @@ int msd_iq_band_delta_dev(msd_ctx *ctx, const float *spec, int64_t nstreams, int
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
     DeviceGuard g(ctx->device);
     KernelTimer timer(ctx, K_IQDELTA);
-    const int64_t waves = nstreams * max_frames;
-    int64_t blocks = (waves + 3) / 4;
-    const int64_t lim = (int64_t)ctx->num_cu * 16;
-    if (blocks > lim) blocks = lim;
+    const int64_t blocks = (nstreams * max_frames + 255) / 256;
     hipLaunchKernelGGL(iq_band_delta_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, spec, nstreams,
                        max_frames, frames, (int)nperseg, band_lo, band_hi, noise_lo, noise_hi, band_db, noise_db,
                        delta, ld);

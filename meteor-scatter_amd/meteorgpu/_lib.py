@@ -618,8 +618,10 @@ class StreamPlan:
             raise ValueError("delta must hold the shard's n_local frames")
         self._put(self.d_delta, delta)
 
-    def delta(self) -> np.ndarray:
-        return self._get(self.d_delta, self.n_local)
+    def delta(self, lo: int = 0, hi: int | None = None) -> np.ndarray:
+        """the shard's delta [lo, hi) (local frame indices)"""
+        hi = self.n_local if hi is None else hi
+        return self._get(C.c_void_p(self.d_delta.value + 8 * lo), hi - lo) if hi > lo else np.zeros(0)
 
     def set_halos(self, tail: np.ndarray, head: np.ndarray):
         if np.asarray(tail).shape != (self.n_tail,) or np.asarray(head).shape != (self.n_head,):

@@ -160,9 +160,9 @@ class IQShardDetector:
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                    self.noise, self.plan.d_delta, self.batch.T)
 
-    def detect(self, comm=None) -> _stream.StreamResult:
+    def detect(self, comm=None, thresholds: bool = True) -> _stream.StreamResult:
         return _stream.StreamDetector(self.ops, comm or _stream.LocalComm(), self.adaptive, self.k, self.W,
-                                      self.F0).run()
+                                      self.F0).run(thresholds)
 
     def close(self):
         self.plan.close()

@@ -127,7 +127,8 @@ def _unpack(a: np.ndarray):
 class StreamResult:
     detections: np.ndarray     # DET_DTYPE [start, stop) frame ranges + dB, the whole stream
     thr0: float                # mean + k*std of the whole stream (main.py:464-466 / :399-400)
-    thresholds: np.ndarray     # this rank's thresholds actually used (adaptive) / [thr0] (global)
+    thresholds: np.ndarray     # this rank's thresholds actually used (adaptive) / [thr0] (global);
+                               # None when run(thresholds=False)
     margin: float              # min |delta - threshold| over the stream
     rounds: int                # state-exchange rounds
 
@@ -145,10 +146,12 @@ class StreamDetector:
 
     # 1. halos
     def exchange_halos(self):
-        ops, r = self.ops, self.comm.rank
-        d = ops.delta()
-        tails = self.comm.allgather(d[max(0, d.size - self.W):] if self.W > 0 else d[:0])
-        heads = self.comm.allgather(d[: self.H])
+        ops, r, n = self.ops, self.comm.rank, self.ops.n_local
+        if self.comm.world == 1:  # nothing before or after the only shard
+            ops.set_halos(np.zeros(0), np.zeros(0))
+            return
+        tails = self.comm.allgather(ops.delta(max(0, n - self.W), n) if self.W > 0 else np.zeros(0))
+        heads = self.comm.allgather(ops.delta(0, min(self.H, n)))
         before = np.concatenate([np.zeros(0)] + tails[:r])
         after = np.concatenate([np.zeros(0)] + heads[r + 1:])
         tail = before[before.size - ops.n_tail:] if ops.n_tail else before[:0]
@@ -188,7 +191,7 @@ class StreamDetector:
                 entry = new
                 exit_, _ = ops.scan(thr0, entry, False)
 
-    def run(self) -> StreamResult:
+    def run(self, thresholds: bool = True) -> StreamResult:
         ops, comm = self.ops, self.comm
         if ops.n_total == 0:
             if not self.adaptive:  # above_thresh[0] on an empty array (main.py:412)
@@ -228,7 +231,7 @@ class StreamDetector:
         for idx, v in zip(owners, vals):
             db_all[idx] = v
         dets["db"] = db_all
-        thr = ops.thresholds() if self.adaptive else np.array([thr0])
+        thr = None if not thresholds else (ops.thresholds() if self.adaptive else np.array([thr0]))
         return StreamResult(dets, thr0, thr, margin, rounds)
 
 
@@ -241,8 +244,8 @@ class DeviceStreamOps:
         self.n_tail, self.n_head = plan.n_tail, plan.n_head
         self.last_rounds = 0
 
-    def delta(self):
-        return self.plan.delta()
+    def delta(self, lo=0, hi=None):
+        return self.plan.delta(lo, hi)
 
     def set_halos(self, tail, head):
         self.plan.set_halos(tail, head)

@@ -31,8 +31,8 @@ class NumpyStreamOps:
     def _x(self):
         return np.concatenate([self.tail, self.d, self.head])
 
-    def delta(self):
-        return self.d.copy()
+    def delta(self, lo=0, hi=None):
+        return self.d[lo:hi].copy()
 
     def set_halos(self, tail, head):
         assert tail.shape == (self.n_tail,) and head.shape == (self.n_head,)
