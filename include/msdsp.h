@@ -214,7 +214,12 @@ int msd_iq_band_delta_dev(msd_ctx *ctx, const float *spec, int64_t nstreams, int
  *   2. msd_stream_chunk_sums: the pairwise sums of the 8192-frame chunks (of delta, or of
  *      (delta - mean)^2) that START in the shard; in chunk order, s = 0.0; s += c gives
  *      numpy's add.reduce over the whole stream;
- *   3. msd_stream_fresh: every frame's mean + k*std(delta[max(0, i-W):i]) (state-free);
+ *   3. msd_stream_fresh + msd_stream_refine: every frame's mean + k*std(delta[max(0, i-W):i]) is
+ *      state-free but only read where the detector is not frozen.  fresh() writes a cheap
+ *      predictor (prefix sums; exact numpy order for windows shorter than W); each scan marks
+ *      the 512-frame tiles whose fresh thresholds it read; refine() computes those tiles
+ *      numpy-exactly and returns how many it computed.  Scan, refine, scan again until refine
+ *      computes nothing: the last scan then read exact thresholds only;
  *   4. msd_stream_scan: the freeze/run scan of the shard from the state entering frame0,
  *      in parallel segments iterated to a fixed point; returns the state after the shard
  *      (rank r+1 enters with rank r's end state: repeat until no entry state changes);
@@ -242,6 +247,8 @@ int msd_stream_buffers(msd_stream_plan *plan, double **delta, double **tail, int
 int msd_stream_chunk_sums(msd_stream_plan *plan, int32_t use_mean, double mean, double *sums, int64_t cap,
                           int64_t *nchunks, int64_t *first_chunk);
 int msd_stream_fresh(msd_stream_plan *plan); /* async; needs the tail halo */
+/* synchronous; *computed = tiles made exact now (0: the previous scan read exact values only) */
+int msd_stream_refine(msd_stream_plan *plan, int32_t *computed);
 /* thr0 = mean + k*std of the whole stream.  reset = 1: every segment restarts from the clean
  * state (first call); 0: only the entry state changed.  Synchronous; *rounds = scan launches. */
 int msd_stream_scan(msd_stream_plan *plan, double thr0, const msd_stream_state *entry, int32_t reset,

@@ -26,6 +26,7 @@
 #include "np_reduce.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -50,8 +51,12 @@ struct msd_stream_plan {
     int64_t *d_count = nullptr;
     int64_t *d_pos = nullptr;   // [nseg] runs emitted before each segment
     double *d_chunks = nullptr; // chunk sums
-    int2 *d_prog = nullptr;     // fresh-threshold program for windows of exactly W frames
-    int nprog = 0;
+    int4 *d_prog = nullptr;     // fresh-threshold leaf records for windows of exactly W frames
+    int32_t *d_need = nullptr;  // [ntiles] a scan used fresh thresholds in the tile
+    int32_t *d_done = nullptr;  // [ntiles] the tile's exact thresholds are computed (+1: counter)
+    double2 *d_pre = nullptr;   // [nblk + 1] prefix sums of x, x^2 (the predictor)
+    int64_t ntiles = 0, nblk = 0;
+    int nleaf = 0;
     double thr0 = 0;
     bool scanned = false;
 };
@@ -127,35 +132,85 @@ __global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restric
 }
 
 // ------------------------------------------------------------------ fresh thresholds
-// program ops (int2 {op, arg}): LEAF {len | off << 8 in .y? } -> see build_program
-enum { OP_LEAF = 0, OP_ADD = 1, OP_CHUNK = 2 };
+// the program: one record per leaf of numpy's tree over a W-element window, in order,
+// {offset, length (<= 128), adds that follow it, 1 if a chunk ends after them}
+constexpr int FR_MAXREC_LDS = 512;  // records kept in LDS (W up to ~32K); more are read from HBM
 
-constexpr int FR_THREADS = 256;
-constexpr int FR_F = 8;                          // frames per lane
-constexpr int FR_FRAMES = FR_THREADS * FR_F;     // 2048 frames per workgroup
+#ifndef MSD_FR_THREADS
+#define MSD_FR_THREADS 128
+#endif
+#ifndef MSD_FR_F
+#define MSD_FR_F 4
+#endif
+constexpr int FR_THREADS = MSD_FR_THREADS;       // a workgroup computes one tile
+constexpr int FR_F = MSD_FR_F;                   // frames per lane
+constexpr int FR_FRAMES = FR_THREADS * FR_F;     // frames per tile
 constexpr int FR_STAGE = FR_FRAMES + 128;        // staged elements per leaf (leaf <= 128)
-constexpr int FR_PADDED = FR_STAGE + FR_STAGE / 4;  // 2 pad doubles per 8: conflict-free b128 reads
+// pad (conflict-free LDS reads): F = 8: 2 doubles per 8 (16-B reads); F = 4: 1 per 4 (8-B reads)
+constexpr int FR_PADDED = FR_STAGE + FR_STAGE / 4;
 constexpr int FR_LOADS = (FR_STAGE + FR_THREADS - 1) / FR_THREADS;
-constexpr int FR_DEPTH = 10;
+constexpr int FR_DEPTH = 7;
 
-__device__ __forceinline__ int padded(int q) { return q + 2 * (q >> 3); }
+__device__ __forceinline__ int padded(int q) { return FR_F == 8 ? q + 2 * (q >> 3) : q + (q >> 2); }
 
 struct FreshParams {
     int64_t n_local, frame0, n_tail, x_len, W, F0;
     double k;
-    int nprog;
-    int64_t wg0;  // first workgroup (blocks below it only hold frames with short windows)
+    int nleaf;
 };
 
 // one pass of the program over this lane's 8 frames: out[f] = numpy np.sum of the window of frame f
 // (SQ: of (x - mean[f])^2)
 template <bool SQ>
 __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t xbase, int64_t x_len,
-                                           const int2 *__restrict__ prog, int nprog, double *stage,
+                                           const int4 *recs, int nleaf, double *stage,
                                            const double (&mean)[FR_F], double (&out)[FR_F]) {
     const int tid = threadIdx.x;
-    double stk[FR_F][FR_DEPTH];
+#if MSD_FR_F == 8
+    // 8 frames: the pending partial sums live in scratch (a runtime-indexed array; 8 x 7 doubles
+    // would not fit beside the 64 accumulators), touched once per leaf / add
+    double stk_[FR_DEPTH + 1][FR_F];
     int sp = 0;
+    auto top = [&](int d, int f) -> double & { return stk_[sp - 1 - d][f]; };
+    auto push = [&](const double (&v)[FR_F]) {
+#pragma unroll
+        for (int f = 0; f < FR_F; ++f) stk_[sp][f] = v[f];
+        ++sp;
+    };
+    auto pop = [&]() {  // removes stk[0] after an add folded it into stk[1] (or into acc)
+        --sp;
+    };
+    auto add_top = [&]() {
+#pragma unroll
+        for (int f = 0; f < FR_F; ++f) top(1, f) = top(1, f) + top(0, f);
+        pop();
+    };
+#else
+    // the tree's pending partial sums, top at stk[0]: a push shifts the stack down, an add pops
+    // the top into the next entry and shifts up -- static register indices only (a runtime-indexed
+    // array would live in scratch); depth <= 7 for numpy's trees of <= 8192 elements
+    double stk[FR_DEPTH][FR_F];
+    auto top = [&](int d, int f) -> double & { return stk[d][f]; };
+    auto push = [&](const double (&v)[FR_F]) {
+#pragma unroll
+        for (int d = FR_DEPTH - 1; d > 0; --d)
+#pragma unroll
+            for (int f = 0; f < FR_F; ++f) stk[d][f] = stk[d - 1][f];
+#pragma unroll
+        for (int f = 0; f < FR_F; ++f) stk[0][f] = v[f];
+    };
+    auto pop = [&]() {
+#pragma unroll
+        for (int d = 0; d < FR_DEPTH - 1; ++d)
+#pragma unroll
+            for (int f = 0; f < FR_F; ++f) stk[d][f] = stk[d + 1][f];
+    };
+    auto add_top = [&]() {
+#pragma unroll
+        for (int f = 0; f < FR_F; ++f) stk[1][f] = stk[1][f] + stk[0][f];
+        pop();
+    };
+#endif
     double acc[FR_F];
 #pragma unroll
     for (int f = 0; f < FR_F; ++f) acc[f] = 0.0;
@@ -178,35 +233,19 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
             if (q < FR_STAGE) buf[padded(q)] = pre[j];
         }
     };
-    int nextleaf = 0;
-    while (nextleaf < nprog && prog[nextleaf].x != OP_LEAF) ++nextleaf;
     int buf = 0;
-    if (nextleaf < nprog) {
-        fetch(prog[nextleaf].y >> 8);
-        commit(stage);
-    }
+    int4 cur = recs[0];
+    fetch(cur.x);
+    commit(stage);
     __syncthreads();
-    for (int pc = 0; pc < nprog; ++pc) {
-        const int2 op = prog[pc];
-        if (op.x == OP_ADD) {
-#pragma unroll
-            for (int f = 0; f < FR_F; ++f) stk[f][sp - 2] = stk[f][sp - 2] + stk[f][sp - 1];
-            --sp;
-            continue;
-        }
-        if (op.x == OP_CHUNK) {
-#pragma unroll
-            for (int f = 0; f < FR_F; ++f) acc[f] = acc[f] + stk[f][sp - 1];
-            --sp;
-            continue;
-        }
-        // LEAF: prefetch the following leaf while this one is summed
-        const int len = op.y & 255;
-        int nl = pc + 1;
-        while (nl < nprog && prog[nl].x != OP_LEAF) ++nl;
-        if (nl < nprog) fetch(prog[nl].y >> 8);
+    for (int li = 0; li < nleaf; ++li) {
+        // prefetch the following leaf while this one is summed
+        const bool has_next = li + 1 < nleaf;
+        const int4 nxt = has_next ? recs[li + 1] : cur;
+        if (has_next) fetch(nxt.x);
+        const int len = cur.y;
         const double *st = stage + buf * FR_PADDED;
-        const int l8 = tid * 8;  // this lane's first element (frame f reads st[l8 + f + m])
+        const int l8 = tid * FR_F;  // this lane's first element (frame f reads st[l8 + f + m])
         auto elem = [&](int q) -> double { return st[padded(l8 + q)]; };
         double res[FR_F];
         if (len >= 8) {
@@ -218,13 +257,18 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
 #pragma unroll
                 for (int k = 0; k < 8; ++k) r[f][k] = -0.0;
             auto group = [&](int g, auto first, auto last) {
-                const double2 *vp = reinterpret_cast<const double2 *>(st + padded(l8 + 8 * g));
                 double v[8];
+                if constexpr (FR_F == 8) {
+                    const double2 *vp = reinterpret_cast<const double2 *>(st + padded(l8 + 8 * g));
 #pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    const double2 t = vp[h];
-                    v[2 * h] = t.x;
-                    v[2 * h + 1] = t.y;
+                    for (int h = 0; h < 4; ++h) {
+                        const double2 t = vp[h];
+                        v[2 * h] = t.x;
+                        v[2 * h + 1] = t.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int h = 0; h < 8; ++h) v[h] = st[padded(l8 + 8 * g + h)];
                 }
 #pragma unroll
                 for (int f = 0; f < FR_F; ++f) {
@@ -281,34 +325,54 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
                 }
             }
         }
+        push(res);
+        for (int a = 0; a < cur.z; ++a) add_top();  // the adds after the leaf: left + right
+        if (cur.w) {  // chunk end: s += pairwise(chunk)
 #pragma unroll
-        for (int f = 0; f < FR_F; ++f) stk[f][sp] = res[f];
-        ++sp;
-        if (nl < nprog) {
+            for (int f = 0; f < FR_F; ++f) acc[f] = acc[f] + top(0, f);
+            pop();
+        }
+        if (has_next) {
             commit(stage + (buf ^ 1) * FR_PADDED);
             buf ^= 1;
         }
         __syncthreads();
+        cur = nxt;
     }
 #pragma unroll
     for (int f = 0; f < FR_F; ++f) out[f] = acc[f];
 }
 
+// exact thresholds of the 512-frame tiles a scan used fresh thresholds in (need) and that are
+// not computed yet (done); the others keep the predictor's values, which no final scan reads
 __global__ __launch_bounds__(FR_THREADS) void fresh_kernel(const double *__restrict__ x, FreshParams P,
-                                                           const int2 *__restrict__ prog,
-                                                           double *__restrict__ fresh) {
+                                                           const int4 *__restrict__ prog,
+                                                           double *__restrict__ fresh, const int32_t *__restrict__ need,
+                                                           int32_t *__restrict__ done, int32_t *__restrict__ count) {
     __shared__ __attribute__((aligned(16))) double stage[2 * FR_PADDED];
-    const int64_t wg = P.wg0 + blockIdx.x;
+    const int64_t wg = blockIdx.x;
+    if (!need[wg] || done[wg]) return;
+    if (threadIdx.x == 0) {
+        done[wg] = 1;
+        atomicAdd(count, 1);
+    }
+    if (P.frame0 + (wg + 1) * FR_FRAMES - 1 < P.W) return;  // short windows only: exact already
     const int64_t j0 = wg * FR_FRAMES + threadIdx.x * FR_F;  // this lane's first local frame
     // element m of the window of local frame j sits at x[n_tail + j - W + m]
     const int64_t xbase = P.n_tail + wg * FR_FRAMES - P.W;
     double mean[FR_F], s[FR_F];
 #pragma unroll
     for (int f = 0; f < FR_F; ++f) mean[f] = 0.0;
-    fresh_pass<false>(x, xbase, P.x_len, prog, P.nprog, stage, mean, s);
+    __shared__ int4 s_rec[FR_MAXREC_LDS];
+    const bool in_lds = P.nleaf <= FR_MAXREC_LDS;
+    if (in_lds)
+        for (int i = threadIdx.x; i < P.nleaf; i += FR_THREADS) s_rec[i] = prog[i];
+    const int4 *recs = in_lds ? s_rec : prog;
+    __syncthreads();
+    fresh_pass<false>(x, xbase, P.x_len, recs, P.nleaf, stage, mean, s);
 #pragma unroll
     for (int f = 0; f < FR_F; ++f) mean[f] = s[f] / (double)P.W;
-    fresh_pass<true>(x, xbase, P.x_len, prog, P.nprog, stage, mean, s);
+    fresh_pass<true>(x, xbase, P.x_len, recs, P.nleaf, stage, mean, s);
 #pragma unroll
     for (int f = 0; f < FR_F; ++f) {
         const int64_t j = j0 + f;
@@ -318,6 +382,73 @@ __global__ __launch_bounds__(FR_THREADS) void fresh_kernel(const double *__restr
             fresh[j] = mean[f] + P.k * sd;
         }
     }
+}
+
+// ---- the predictor: mean + k*std of every window from prefix sums of x and x^2 (not numpy's
+// rounding; it only tells the first scan which tiles need exact thresholds)
+constexpr int PB = 64;  // elements per prefix block
+__global__ __launch_bounds__(256) void blocksum_kernel(const double *__restrict__ x, int64_t x_len, int64_t nblk,
+                                                       double2 *__restrict__ blk) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    double s = 0.0, q = 0.0;
+    const int64_t e = (b + 1) * PB < x_len ? (b + 1) * PB : x_len;
+    for (int64_t i = b * PB; i < e; ++i) {
+        const double v = x[i];
+        s += v;
+        q += v * v;
+    }
+    blk[b] = make_double2(s, q);
+}
+
+// exclusive prefix over the blocks, in place, one workgroup
+__global__ __launch_bounds__(1024) void blockscan_kernel(double2 *__restrict__ blk, int64_t nblk) {
+    __shared__ double2 tot[1024];
+    const int tid = threadIdx.x;
+    const int64_t per = (nblk + 1023) / 1024;
+    const int64_t b0 = tid * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int64_t b = b0; b < b1; ++b) acc = make_double2(acc.x + blk[b].x, acc.y + blk[b].y);
+    tot[tid] = acc;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const double2 v = tid >= o ? tot[tid - o] : make_double2(0.0, 0.0);
+        __syncthreads();
+        tot[tid] = make_double2(tot[tid].x + v.x, tot[tid].y + v.y);
+        __syncthreads();
+    }
+    double2 run = tid > 0 ? tot[tid - 1] : make_double2(0.0, 0.0);
+    for (int64_t b = b0; b < b1; ++b) {
+        const double2 v = blk[b];
+        blk[b] = run;
+        run = make_double2(run.x + v.x, run.y + v.y);
+    }
+}
+
+__device__ __forceinline__ double2 prefix_at(const double *__restrict__ x, const double2 *__restrict__ pre,
+                                             int64_t e) {  // sums of x[0..e)
+    const int64_t b = e / PB;
+    double2 r = pre[b];
+    for (int64_t i = b * PB; i < e; ++i) {
+        const double v = x[i];
+        r.x += v;
+        r.y += v * v;
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(256) void approx_kernel(const double *__restrict__ x, const double2 *__restrict__ pre,
+                                                     FreshParams P, int64_t jbeg, double *__restrict__ fresh) {
+    const int64_t j = jbeg + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.n_local) return;
+    const int64_t i = P.frame0 + j;
+    if (i < P.F0) return;
+    const int64_t e = P.n_tail + j;
+    const double2 hi = prefix_at(x, pre, e), lo = prefix_at(x, pre, e - P.W);
+    const double m = (hi.x - lo.x) / (double)P.W;
+    double v = (hi.y - lo.y) / (double)P.W - m * m;
+    v = v > 0.0 ? v : 0.0;
+    fresh[j] = m + P.k * sqrt(v);
 }
 
 // frames with i < W: window delta[0:i] (only the shard that holds the stream's first W frames)
@@ -347,7 +478,7 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
                                                   SState *__restrict__ out_state, const int32_t *__restrict__ active,
                                                   msd_det *__restrict__ runs, int32_t *__restrict__ nruns,
                                                   double *__restrict__ seg_margin, double *__restrict__ thr_used,
-                                                  int32_t *__restrict__ overflow) {
+                                                  int32_t *__restrict__ overflow, int32_t *__restrict__ need) {
     const int64_t s = blockIdx.x;
     if (!active[s]) return;
     const int lane = threadIdx.x;
@@ -373,7 +504,7 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
         const double t_unf = init ? thr0 : fresh[j];
         const uint64_t A_unf = __ballot(valid && dv > t_unf);
         double t_fin = t_unf;
-        uint64_t D = 0;
+        uint64_t D = 0, U = 0;  // detected, unfrozen (fresh threshold used)
         int p = 0;
         while (p < nvalid) {
             const int64_t i = pos + p;
@@ -394,17 +525,20 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
             } else {  // unfrozen: fresh (or fixed) thresholds until the first detection
                 const uint64_t m = A_unf & bits_from(p);
                 if (!m) {
+                    U |= bits_from(p);
                     thr_cur = __shfl(t_unf, nvalid - 1);
                     p = nvalid;
                     break;
                 }
                 const int u = __builtin_ctzll(m);
+                U |= bits_from(p) & bits_upto(u);
                 D |= 1ull << u;
                 thr_cur = __shfl(t_unf, u);
                 fz = pos + u + P.Fa;
                 p = u + 1;
             }
         }
+        if (need && (U & __ballot(valid && !init)) && lane == 0) need[k / FR_FRAMES] = 1;
         if (valid) {
             const double mg = fabs(dv - t_fin);
             if (mg < min_margin) min_margin = mg;
@@ -546,26 +680,27 @@ __global__ void db_kernel(const double *__restrict__ x, int64_t x0, msd_det *__r
     d[j].db = np_sum(ArrRef{x}, a - x0, m) / (double)m;
 }
 
-// numpy's np.sum association over n elements as a program for fresh_kernel (leaves of <= 128)
-void build_program(int64_t n, std::vector<int2> &prog) {
-    prog.clear();
+// numpy's np.sum association over n elements (8192-element chunks, each a pairwise tree with
+// leaves of <= 128) as leaf records for fresh_kernel
+void build_program(int64_t n, std::vector<int4> &rec) {
+    rec.clear();
     struct Rec {
-        static void tree(int64_t base, int64_t m, std::vector<int2> &p) {
+        static void tree(int64_t base, int64_t m, std::vector<int4> &r) {
             if (m <= 128) {
-                p.push_back(make_int2(OP_LEAF, (int)((base << 8) | m)));
+                r.push_back(make_int4((int)base, (int)m, 0, 0));
                 return;
             }
             int64_t m2 = m / 2;
             m2 -= m2 % 8;
-            tree(base, m2, p);
-            tree(base + m2, m - m2, p);
-            p.push_back(make_int2(OP_ADD, 0));
+            tree(base, m2, r);
+            tree(base + m2, m - m2, r);
+            r.back().z += 1;  // the add combining the two halves follows the right half's last leaf
         }
     };
     for (int64_t c = 0; c < n; c += CHUNK) {
         const int64_t m = n - c < CHUNK ? n - c : CHUNK;
-        Rec::tree(c, m, prog);
-        prog.push_back(make_int2(OP_CHUNK, 0));
+        Rec::tree(c, m, rec);
+        rec.back().w = 1;
     }
 }
 
@@ -646,12 +781,18 @@ int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total
     if ((e = hipMalloc(&p->d_count, sizeof(int64_t))) != hipSuccess) return cleanup(e, "hipMalloc count");
     if ((e = hipMalloc(&p->d_pos, sizeof(int64_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc pos");
     if ((e = hipMalloc(&p->d_chunks, sizeof(double) * nchunk)) != hipSuccess) return cleanup(e, "hipMalloc chunks");
+    p->ntiles = (nl1 + FR_FRAMES - 1) / FR_FRAMES;
+    p->nblk = (p->n_tail + nl1 + p->head_cap) / PB + 1;
+    if ((e = hipMalloc(&p->d_need, sizeof(int32_t) * p->ntiles)) != hipSuccess) return cleanup(e, "hipMalloc need");
+    if ((e = hipMalloc(&p->d_done, sizeof(int32_t) * (p->ntiles + 1))) != hipSuccess)
+        return cleanup(e, "hipMalloc done");
+    if ((e = hipMalloc(&p->d_pre, sizeof(double2) * (p->nblk + 1))) != hipSuccess) return cleanup(e, "hipMalloc pre");
     if (W > 0) {
-        std::vector<int2> prog;
+        std::vector<int4> prog;
         build_program(W, prog);
-        p->nprog = (int)prog.size();
-        if ((e = hipMalloc(&p->d_prog, sizeof(int2) * prog.size())) != hipSuccess) return cleanup(e, "hipMalloc prog");
-        if ((e = hipMemcpy(p->d_prog, prog.data(), sizeof(int2) * prog.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        p->nleaf = (int)prog.size();
+        if ((e = hipMalloc(&p->d_prog, sizeof(int4) * prog.size())) != hipSuccess) return cleanup(e, "hipMalloc prog");
+        if ((e = hipMemcpy(p->d_prog, prog.data(), sizeof(int4) * prog.size(), hipMemcpyHostToDevice)) != hipSuccess)
             return cleanup(e, "hipMemcpy prog");
     }
     *out = p;
@@ -663,7 +804,7 @@ void msd_stream_plan_destroy(msd_stream_plan *p) {
     DeviceGuard g(p->ctx->device);
     hipStreamSynchronize(p->ctx->stream);
     void *bufs[] = {p->d_x, p->d_fresh, p->d_thr, p->d_state, p->d_active, p->d_runs, p->d_out, p->d_nruns,
-                    p->d_margin, p->d_count, p->d_pos, p->d_chunks, p->d_prog};
+                    p->d_margin, p->d_count, p->d_pos, p->d_chunks, p->d_prog, p->d_need, p->d_done, p->d_pre};
     for (void *b : bufs)
         if (b) hipFree(b);
     delete p;
@@ -710,12 +851,7 @@ int msd_stream_chunk_sums(msd_stream_plan *p, int32_t use_mean, double mean, dou
     return MSD_OK;
 }
 
-int msd_stream_fresh(msd_stream_plan *p) {
-    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_fresh: null plan");
-    if (!p->cfg.adaptive || p->n_local == 0) return MSD_OK;
-    DeviceGuard g(p->ctx->device);
-    KernelTimer timer(p->ctx, K_FRESH);
-    FreshParams P;
+static void fresh_params(msd_stream_plan *p, FreshParams &P) {
     P.n_local = p->n_local;
     P.frame0 = p->frame0;
     P.n_tail = p->n_tail;
@@ -723,22 +859,63 @@ int msd_stream_fresh(msd_stream_plan *p) {
     P.W = p->cfg.window_blocks;
     P.F0 = p->cfg.fixed_init_blocks;
     P.k = p->cfg.k_std;
-    P.nprog = p->nprog;
-    P.wg0 = 0;
-    // frames [0, jshort) have windows shorter than W
+    P.nleaf = p->nleaf;
+}
+
+int msd_stream_fresh(msd_stream_plan *p) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_fresh: null plan");
+    if (!p->cfg.adaptive || p->n_local == 0) return MSD_OK;
+    DeviceGuard g(p->ctx->device);
+    hipStream_t st = p->ctx->stream;
+    KernelTimer timer(p->ctx, K_FRESH);
+    FreshParams P;
+    fresh_params(p, P);
+    // MSD_FRESH_ALL=1: every tile exact up front (A/B timing of the exact kernel; same results)
+    static const bool all = [] {
+        const char *e = getenv("MSD_FRESH_ALL");
+        return e && e[0] == '1';
+    }();
+    MSD_HIP(hipMemsetAsync(p->d_need, 0, sizeof(int32_t) * p->ntiles, st));
+    if (all) MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_need), 1, p->ntiles, st));
+    MSD_HIP(hipMemsetAsync(p->d_done, 0, sizeof(int32_t) * (p->ntiles + 1), st));
+    // frames [0, jshort) have windows shorter than W: exact right away
     int64_t jshort = P.W - p->frame0;
     jshort = jshort < 0 ? 0 : (jshort > p->n_local ? p->n_local : jshort);
     if (P.W == 0) jshort = p->n_local;  // empty windows: NaN thresholds
     if (jshort > 0)
-        hipLaunchKernelGGL(fresh_short_kernel, dim3((unsigned)((jshort + 255) / 256)), dim3(256), 0, p->ctx->stream,
-                           p->d_x, P, jshort, p->d_fresh);
-    if (jshort < p->n_local && P.W > 0) {
-        const int64_t wg = (p->n_local + FR_FRAMES - 1) / FR_FRAMES;
-        P.wg0 = jshort / FR_FRAMES;  // skip workgroups that only hold short-window frames
-        hipLaunchKernelGGL(fresh_kernel, dim3((unsigned)(wg - P.wg0)), dim3(FR_THREADS), 0, p->ctx->stream, p->d_x, P,
-                           p->d_prog, p->d_fresh);
+        hipLaunchKernelGGL(fresh_short_kernel, dim3((unsigned)((jshort + 255) / 256)), dim3(256), 0, st, p->d_x, P,
+                           jshort, p->d_fresh);
+    if (jshort < p->n_local) {  // the predictor for full windows
+        const int64_t nb = P.x_len / PB + 1;
+        hipLaunchKernelGGL(blocksum_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, p->d_x, P.x_len,
+                           nb, p->d_pre);
+        hipLaunchKernelGGL(blockscan_kernel, dim3(1), dim3(1024), 0, st, p->d_pre, nb);
+        const int64_t m = p->n_local - jshort;
+        hipLaunchKernelGGL(approx_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, p->d_x, p->d_pre, P,
+                           jshort, p->d_fresh);
     }
     MSD_HIP(hipGetLastError());
+    return MSD_OK;
+}
+
+int msd_stream_refine(msd_stream_plan *p, int32_t *computed) {
+    if (!p || !computed) return fail(MSD_ERR_INVALID, "msd_stream_refine: null");
+    *computed = 0;
+    if (!p->cfg.adaptive || p->n_local == 0 || p->cfg.window_blocks == 0) return MSD_OK;
+    DeviceGuard g(p->ctx->device);
+    hipStream_t st = p->ctx->stream;
+    FreshParams P;
+    fresh_params(p, P);
+    int32_t *count = p->d_done + p->ntiles;
+    MSD_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), st));
+    {
+        KernelTimer timer(p->ctx, K_FRESH);
+        hipLaunchKernelGGL(fresh_kernel, dim3((unsigned)p->ntiles), dim3(FR_THREADS), 0, st, p->d_x, P, p->d_prog,
+                           p->d_fresh, p->d_need, p->d_done, count);
+    }
+    MSD_HIP(hipGetLastError());
+    MSD_HIP(hipMemcpyAsync(computed, count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
     return MSD_OK;
 }
 
@@ -788,7 +965,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
             KernelTimer timer(p->ctx, K_SSCAN);
             hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
                                p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
-                               p->d_margin, p->d_thr, overflow);
+                               p->d_margin, p->d_thr, overflow, p->cfg.adaptive ? p->d_need : nullptr);
         }
         MSD_HIP(hipGetLastError());
         ++nround;

@@ -209,6 +209,7 @@ _SIGS = [
     ("msd_stream_chunk_sums", C.c_int,
      [_P, C.c_int32, C.c_double, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("msd_stream_fresh", C.c_int, [_P]),
+    ("msd_stream_refine", C.c_int, [_P, C.POINTER(C.c_int32)]),
     ("msd_stream_scan", C.c_int,
      [_P, C.c_double, C.POINTER(MsdStreamState), C.c_int32, C.POINTER(MsdStreamState), C.POINTER(C.c_int32)]),
     ("msd_stream_runs", C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
@@ -642,6 +643,11 @@ class StreamPlan:
 
     def fresh(self):
         check(self.ctx.lib.msd_stream_fresh(self.h))
+
+    def refine(self) -> int:
+        n = C.c_int32(0)
+        check(self.ctx.lib.msd_stream_refine(self.h, C.byref(n)))
+        return n.value
 
     def scan(self, thr0: float, entry: MsdStreamState, reset: bool) -> tuple[MsdStreamState, int]:
         ex = MsdStreamState()

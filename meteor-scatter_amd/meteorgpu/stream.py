@@ -18,6 +18,10 @@ exchanges, all small, done here on the host over a communicator's allgather:
    r re-scans from rank r-1's exit state until no entry state changes (at most world + 1
    rounds, normally 2).
 
+The adaptive thresholds are only read where the detector is not frozen, so the first scan runs
+on cheap predicted thresholds, marks what it read, the device computes those numpy-exactly
+(``refine``), and the scan repeats until a scan read nothing that was not exact (normally 2).
+
 The device work per rank is ``_lib.StreamPlan`` (libmsdsp, stream.hip); ``ops`` may be any
 object with the same methods (the CPU tests drive this protocol with a numpy stand-in over
 gloo).  Results are identical on every rank: the merged detections of the whole stream.
@@ -202,6 +206,11 @@ class StreamDetector:
         if self.adaptive:
             ops.fresh()
         rounds = self.scan(thr0)
+        while self.adaptive:  # until the last scan read exact thresholds only, on every rank
+            n = ops.refine()
+            if not any(int(f[0]) for f in comm.allgather(np.array([n], np.int64))):
+                break
+            rounds += self.scan(thr0)
         # runs of every shard, merged in stream order (a run continued across an edge has start -1)
         local, margin = ops.runs()
         parts = comm.allgather(np.stack([local["start"], local["stop"]], 1).reshape(-1).astype(np.int64))
@@ -255,6 +264,9 @@ class DeviceStreamOps:
 
     def fresh(self):
         self.plan.fresh()
+
+    def refine(self):
+        return self.plan.refine()
 
     def scan(self, thr0, entry, reset):
         ex, rounds = self.plan.scan(thr0, _lib.MsdStreamState(entry[0], entry[1], entry[2], 0), reset)

@@ -66,6 +66,9 @@ class NumpyStreamOps:
                     warnings.simplefilter("ignore")
                     self.fr[j] = np.mean(win) + self.k * np.std(win)
 
+    def refine(self):
+        return 0  # fresh() is exact already
+
     def scan(self, thr0, entry, reset):
         fz, last, thr = entry
         runs = []
