@@ -306,7 +306,10 @@ int msd_cstft_psd_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
     DeviceGuard g(p->ctx->device);
     const int64_t total = nstreams * max_frames;
-    int64_t wgs = (int64_t)p->ctx->num_cu * 3;  // LDS (36 KB) and registers allow 3 per CU
+#ifndef MSD_CS_WG_PER_CU
+#define MSD_CS_WG_PER_CU 3
+#endif
+    int64_t wgs = (int64_t)p->ctx->num_cu * MSD_CS_WG_PER_CU;  // persistent: LDS (37 KB) allows 4 per CU
     if (wgs > total) wgs = total;
     const int64_t per = (total + wgs - 1) / wgs;
     wgs = (total + per - 1) / per;

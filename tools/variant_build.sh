@@ -8,6 +8,6 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 W=$(mktemp -d /tmp/var_XXXX)
 mkdir -p "$W/meteor-scatter_amd" && cp -r "$ROOT/meteor-scatter_amd/csrc" "$W/meteor-scatter_amd/" && cp -r "$ROOT/include" "$W/"
 rm -rf "$W/meteor-scatter_amd/csrc/build"
-make -s -C "$W/meteor-scatter_amd/csrc" -j8 EXTRA="$EXTRA" OUT="$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp_$TAG.so" >/dev/null
+make -s -C "$W/meteor-scatter_amd/csrc" -j8 EXTRA="$EXTRA" ${MKARGS:-} OUT="$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp_$TAG.so" >/dev/null
 rm -rf "$W"
 echo "built meteorgpu/libmsdsp_$TAG.so (EXTRA=$EXTRA)"
