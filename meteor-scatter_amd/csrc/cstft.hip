@@ -212,7 +212,14 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
             for (int j = 0; j < 16; ++j) v[j] = buf[(16 * k2a + j) * 17 + q3];
             dft16(v);
 #pragma unroll
-            for (int k2b = 0; k2b < 16; ++k2b) of[tid + 256 * k2b] = v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y;
+            for (int k2b = 0; k2b < 16; ++k2b) {
+                const float pw = v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y;
+#ifndef MSD_NO_NT_STORE  // streaming (non-temporal) stores: the output is written once, never re-read here (A/B: -1 to -2 %)
+                __builtin_nontemporal_store(pw, of + tid + 256 * k2b);
+#else
+                of[tid + 256 * k2b] = pw;
+#endif
+            }
             // no barrier at the end: the next frame writes buf / red only after its first
             // barrier, which every wave reaches after its pass-3 reads of this frame
         };
