@@ -6,8 +6,9 @@
 //   iq_band_delta_kernel   frame-major spectrogram [T][N] -> band / noise dB, delta (main.py:380-393)
 //   chunk_sums_kernel      numpy's add.reduce over the whole stream is s = 0.0; s += pairwise(chunk)
 //                          for 8192-element chunks in order: each wave sums one chunk that starts
-//                          in the shard (64 lanes x one 128-element leaf, butterfly = numpy's
-//                          balanced tree); the host adds the chunk sums of all ranks in order
+//                          in the shard (wave_chunk_sum: each lane follows its bits down numpy's
+//                          recursion, the tree folds back with xor shuffles); the host adds the
+//                          chunk sums of all ranks in order
 //   fresh_kernel           mean + k*std(delta[i-W:i]) for every frame i >= W.  The pairwise tree of
 //                          a W-element window has the same shape for every i, so the host turns it
 //                          into a program (leaf / add / chunk-end ops) that every lane runs on its
@@ -25,6 +26,7 @@
 #include "msd_internal.h"
 #include "np_reduce.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -104,6 +106,49 @@ __global__ __launch_bounds__(256) void iq_band_delta_kernel(const float *__restr
     delta[s * ld + t] = bd - nd;
 }
 
+// numpy's pairwise sum of one chunk a(cb .. cb+m), m <= 8192, by one wave.  Lane L follows the
+// path of its 6 bits down numpy's recursion (bit 5 first: 0 = left half); the node where the path
+// stops (a leaf of <= 128, or depth 6) is summed by the lane whose remaining bits are zero; the
+// tree is then folded bottom-up with xor shuffles, adding only across nodes that were split.
+// IEEE addition commutes, so left + right in either order gives numpy's bits.
+template <typename A>
+__device__ __forceinline__ double wave_chunk_sum(const A &a, int64_t cb, int64_t m) {
+#pragma clang fp contract(off)
+    const int L = threadIdx.x & 63;
+    int64_t base = 0, size = m;
+    int D = 6;  // depth of this lane's node
+    for (int d = 0; d < 6; ++d) {
+        if (size <= 128) {
+            D = d;
+            break;
+        }
+        int64_t n2 = size / 2;
+        n2 -= n2 % 8;
+        if ((L >> (5 - d)) & 1) {
+            base += n2;
+            size -= n2;
+        } else {
+            size = n2;
+        }
+    }
+    const bool canon = (L & ((1 << (6 - D)) - 1)) == 0;
+    double v = canon ? np_pairwise_rec<2>(a, cb + base, size) : 0.0;
+    for (int d = 5; d >= 0; --d) {  // node at depth d split iff this lane's path went deeper
+        const double o = __builtin_bit_cast(double, __shfl_xor(__builtin_bit_cast(long long, v), 1 << (5 - d), 64));
+        if (D > d) v = v + o;
+    }
+    return __builtin_bit_cast(double, __shfl(__builtin_bit_cast(long long, v), 0, 64));
+}
+
+// np.sum of a(base .. base+n): s = 0.0; s += pairwise(chunk) over 8192-element chunks
+template <typename A>
+__device__ double wave_np_sum(const A &a, int64_t base, int64_t n) {
+#pragma clang fp contract(off)
+    double s = 0.0;
+    for (int64_t c = 0; c < n; c += NP_BUFSIZE) s += wave_chunk_sum(a, base + c, n - c < NP_BUFSIZE ? n - c : NP_BUFSIZE);
+    return s;
+}
+
 // ------------------------------------------------------------------ chunk sums
 // x: the stream around the shard (x[j] = frame x0 + j); chunk c covers frames [8192c, min(8192(c+1),
 // n_total)).  One wave per chunk that starts in the shard.
@@ -117,18 +162,8 @@ __global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restric
     const int64_t g = (first_chunk + c) * CHUNK;
     const int64_t m = n_total - g < CHUNK ? n_total - g : CHUNK;
     const double *p = x + (g - x0);
-    if (m == CHUNK) {  // 64 leaves of 128; numpy's tree over them is balanced: a butterfly
-        double r;
-        if constexpr (SQ)
-            r = np_pairwise_leaf(SqDevRef{p, mean}, (int64_t)lane * 128, 128);
-        else
-            r = np_pairwise_leaf(ArrRef{p}, (int64_t)lane * 128, 128);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) r = r + shfl_xor_d(r, o);
-        if (lane == 0) out[c] = r;
-    } else if (lane == 0) {  // the stream's last, short chunk
-        out[c] = SQ ? np_pairwise(SqDevRef{p, mean}, 0, m) : np_pairwise(ArrRef{p}, 0, m);
-    }
+    const double r = SQ ? wave_chunk_sum(SqDevRef{p, mean}, 0, m) : wave_chunk_sum(ArrRef{p}, 0, m);
+    if (lane == 0) out[c] = r;
 }
 
 // ------------------------------------------------------------------ fresh thresholds
@@ -452,15 +487,19 @@ __global__ __launch_bounds__(256) void approx_kernel(const double *__restrict__ 
 }
 
 // frames with i < W: window delta[0:i] (only the shard that holds the stream's first W frames)
+// frames with i < W: window delta[0:i], a different tree per frame (only the shard that holds the
+// stream's first W frames); one wave per frame
 __global__ __launch_bounds__(256) void fresh_short_kernel(const double *__restrict__ x, FreshParams P,
                                                           int64_t jend, double *__restrict__ fresh) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= jend) return;
-    const int64_t i = P.frame0 + j;
-    if (i < P.F0) return;
-    double m, sd;
-    np_mean_std(x, P.n_tail + j - i, i, m, sd);  // x index of global frame 0 = n_tail - frame0
-    fresh[j] = m + P.k * sd;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t j = (int64_t)blockIdx.x * 4 + w; j < jend; j += (int64_t)gridDim.x * 4) {
+        const int64_t i = P.frame0 + j;
+        if (i < P.F0) continue;
+        const int64_t base = P.n_tail + j - i;  // x index of global frame 0 = n_tail - frame0
+        const double m = wave_np_sum(ArrRef{x}, base, i) / (double)i;
+        const double v = wave_np_sum(SqDevRef{x, m}, base, i);
+        if (lane == 0) fresh[j] = m + P.k * sqrt(v / (double)i);
+    }
 }
 
 // ------------------------------------------------------------------ scan
@@ -883,8 +922,8 @@ int msd_stream_fresh(msd_stream_plan *p) {
     jshort = jshort < 0 ? 0 : (jshort > p->n_local ? p->n_local : jshort);
     if (P.W == 0) jshort = p->n_local;  // empty windows: NaN thresholds
     if (jshort > 0)
-        hipLaunchKernelGGL(fresh_short_kernel, dim3((unsigned)((jshort + 255) / 256)), dim3(256), 0, st, p->d_x, P,
-                           jshort, p->d_fresh);
+        hipLaunchKernelGGL(fresh_short_kernel, dim3((unsigned)std::min<int64_t>((jshort + 3) / 4, 4096)), dim3(256), 0,
+                           st, p->d_x, P, jshort, p->d_fresh);
     if (jshort < p->n_local) {  // the predictor for full windows
         const int64_t nb = P.x_len / PB + 1;
         hipLaunchKernelGGL(blocksum_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, p->d_x, P.x_len,

@@ -202,9 +202,9 @@ class StreamDetector:
                 raise IndexError("index 0 is out of bounds for axis 0 with size 0")
             return StreamResult(np.zeros(0, _lib.DET_DTYPE), float("nan"), np.zeros(0), math.inf, 0)
         self.exchange_halos()
-        thr0 = self.global_threshold()
-        if self.adaptive:
+        if self.adaptive:  # state-free, independent of thr0: queued before the chunk-sum round trips
             ops.fresh()
+        thr0 = self.global_threshold()
         rounds = self.scan(thr0)
         while self.adaptive:  # until the last scan read exact thresholds only, on every rank
             n = ops.refine()
