@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Copy one round's measurements from gpurun_out/round_<tag> (tools/profile_round.sh) into
+profiles/: the bench lines, rocprofv3 kernel statistics, PMC summaries and the HBM traffic files
+bench.py reads for roofline.traffic.  Usage: tools/profile_collect.py TAG"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = os.path.join(root, "gpurun_out", f"round_{tag}")
+dst = os.path.join(root, "profiles")
+pmc = os.path.join(root, "gpurun_out", "pmc")
+
+
+def last_json(path):
+    with open(path) as fh:
+        return json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
+
+
+json.dump(last_json(f"{src}/bench.json"), open(f"{dst}/{tag}_bench.json", "w"))
+for wl, suffix in (("", ""), ("_live", "_live"), ("_c5", "_c5")):
+    shutil.copy(f"{src}/kt{wl}/kt_kernel_stats.csv", f"{dst}/{tag}_kernel_stats{suffix}.csv")
+    json.dump(last_json(f"{src}/kt{wl}.log"), open(f"{dst}/{tag}_bench{suffix}_under_rocprof.json", "w"))
+for sub, name, kernel, match in ((tag, "stft", "stft1024_kernel<short, 0>", {"files": 1440, "nperseg": 1024}),
+                                 (f"{tag}_c5", "cstft", "cstft4096_kernel<short, 4>", None),
+                                 (f"{tag}_c5det", None, None, None)):
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "pmc_summary.py"), f"{pmc}/{sub}"],
+                         capture_output=True, text=True, check=True).stdout
+    suffix = sub[len(tag):]
+    open(f"{dst}/{tag}_pmc_summary{suffix}.txt", "w").write(out)
+    if name is None:
+        continue
+    summ = json.load(open(f"{pmc}/{sub}/summary.json"))[kernel]
+    rec = {"kernel": kernel, "hbm_bytes_per_launch": summ["hbm_bytes"], "fetch_size_kib": summ["FETCH_SIZE"],
+           "write_size_kib": summ["WRITE_SIZE"],
+           "rule": "HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950: FETCH_SIZE reports half of wide "
+                   "streaming reads, MI355X_MICROARCH.md HBM/rocprofv3 section)",
+           "source": f"tools/pmc_stft.sh {sub} (4 separate --pmc passes), per-dispatch averages"}
+    if match:
+        rec.update(match)
+    else:  # C5: frames per launch and nperseg as bench.py reports them
+        b = last_json(f"{src}/kt_c5.log")
+        rec.update({"frames": b["config"]["frames_per_gpu"], "nperseg": 4096})
+    json.dump(rec, open(f"{dst}/{name}_pmc.json", "w"), indent=1)
+print("profiles updated for", tag)
