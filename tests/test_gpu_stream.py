@@ -202,3 +202,28 @@ def test_iq_sharded_threads():
     for r in res:
         assert [(int(a) * bs, int(b) * bs) for a, b, _ in r.detections] == [(d.t_start, d.t_stop) for d in one]
         assert np.array_equal(r.detections["db"], np.array([d.dB for d in one]))
+
+
+def test_stream_detector_over_rccl_single_rank():
+    """The C5 exchange path through RCCL (msd_comm_allgather behind stream.RcclComm) at world
+    size 1 on the one-GPU box: variable-length allgathers round-trip, and the detector run
+    through them equals the oracle."""
+    from meteorgpu import _lib, stream
+    from meteorgpu.batch import Communicator
+    ctx = _lib.Context(0)
+    comm = Communicator(ctx, 1, Communicator.unique_id(), 0)
+    try:
+        rc = stream.RcclComm(comm, 0, 1)
+        for a in (np.arange(5, dtype=np.int64), np.linspace(0, 1, 1000), np.zeros(0)):
+            got = rc.allgather(a)
+            assert len(got) == 1 and got[0].dtype == a.dtype and np.array_equal(got[0], a)
+        d = make_delta(30000, 31, rate=0.01)
+        cfg = _lib.det_cfg(True, 4.0, 600, 0, 100, 50)
+        plan = _lib.StreamPlan(ctx, cfg, d.size, 0, d.size, seg_len=1024)
+        plan.set_delta(d)
+        res = stream.StreamDetector(stream.DeviceStreamOps(plan), rc, True, 4.0, 600, 50).run()
+        plan.close()
+        _check(res, d, True, 4.0, 600, 100, 50)
+    finally:
+        comm.close()
+        ctx.close()
