@@ -74,9 +74,6 @@ struct SState {  // msd_stream_state
     int64_t reserved;
 };
 
-__device__ __forceinline__ double shfl_xor_d(double v, int m) {
-    return __builtin_bit_cast(double, __shfl_xor(__builtin_bit_cast(long long, v), m, 64));
-}
 
 // ------------------------------------------------------------------ band delta per frame
 // one thread per frame: the band bins of a frame are one or two short contiguous runs of its row
@@ -327,6 +324,9 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
             using T_ = std::integral_constant<bool, true>;
             using F_ = std::integral_constant<bool, false>;
             group(0, T_{}, F_{});
+#ifdef MSD_FR_UNROLL
+#pragma unroll MSD_FR_UNROLL
+#endif
             for (int g = 1; g < G; ++g) group(g, F_{}, F_{});
             group(G, F_{}, T_{});
 #pragma unroll
@@ -999,28 +999,36 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
     P.write_thr = 1;
     int32_t *changed = p->d_active + p->nseg;
     int32_t *overflow = p->d_active + p->nseg + 1;
+    // rounds are enqueued three at a time (a round with no active segment costs two empty
+    // launches); the host checks the last round's change count, so a typical fixed point
+    // (2-3 rounds) costs one round trip
+    constexpr int R = 3;
+    SState ex{};
     for (;;) {
-        {
-            KernelTimer timer(p->ctx, K_SSCAN);
-            hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
-                               p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
-                               p->d_margin, p->d_thr, overflow, p->cfg.adaptive ? p->d_need : nullptr);
+        for (int r = 0; r < R; ++r) {
+            {
+                KernelTimer timer(p->ctx, K_SSCAN);
+                hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
+                                   p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
+                                   p->d_margin, p->d_thr, overflow, p->cfg.adaptive ? p->d_need : nullptr);
+            }
+            MSD_HIP(hipGetLastError());
+            ++nround;
+            MSD_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), st));
+            hipLaunchKernelGGL(propagate_kernel, dim3((unsigned)((p->nseg + 255) / 256)), dim3(256), 0, st, st_in(p),
+                               st_out(p), p->d_active, p->nseg, p->seg_len, p->frame0, P.F0, changed);
+            MSD_HIP(hipGetLastError());
         }
-        MSD_HIP(hipGetLastError());
-        ++nround;
-        MSD_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), st));
-        hipLaunchKernelGGL(propagate_kernel, dim3((unsigned)((p->nseg + 255) / 256)), dim3(256), 0, st, st_in(p),
-                           st_out(p), p->d_active, p->nseg, p->seg_len, p->frame0, P.F0, changed);
-        MSD_HIP(hipGetLastError());
         int32_t hc[2];
         MSD_HIP(hipMemcpyAsync(hc, changed, sizeof(hc), hipMemcpyDeviceToHost, st));
+        MSD_HIP(hipMemcpyAsync(&ex, st_out(p) + (p->nseg - 1), sizeof(SState), hipMemcpyDeviceToHost, st));
         MSD_HIP(hipStreamSynchronize(st));
         if (hc[1]) return fail(MSD_ERR_CAPACITY, "msd_stream_scan: more runs in a segment than cap_per_seg");
         if (hc[0] == 0) break;
-        if (nround > p->nseg + 2) return fail(MSD_ERR_INVALID, "msd_stream_scan: no fixed point");
+        if (nround > p->nseg + 2 + R) return fail(MSD_ERR_INVALID, "msd_stream_scan: no fixed point");
     }
     p->scanned = true;
-    if (exit_state) MSD_HIP(hipMemcpy(exit_state, st_out(p) + (p->nseg - 1), sizeof(SState), hipMemcpyDeviceToHost));
+    if (exit_state) std::memcpy(exit_state, &ex, sizeof(SState));
     if (rounds) *rounds = nround;
     return MSD_OK;
 }

@@ -215,21 +215,18 @@ class StreamDetector:
         local, margin = ops.runs()
         parts = comm.allgather(np.stack([local["start"], local["stop"]], 1).reshape(-1).astype(np.int64))
         margin = min(float(m[0]) for m in comm.allgather(np.array([margin])))
-        merged: list[list[int]] = []
-        for p in parts:
-            for s, e in p.reshape(-1, 2):
-                if s < 0:
-                    merged[-1][1] = int(e)
-                else:
-                    merged.append([int(s), int(e)])
-        if not self.adaptive and merged and merged[-1][1] == ops.n_total:
-            merged[-1][1] = ops.n_total - 1  # burst_stops gets len-1 (main.py:414-415)
-            if merged[-1][1] - merged[-1][0] <= 0:
+        allr = np.concatenate([np.zeros(0, np.int64)] + parts).reshape(-1, 2)
+        if allr.size and allr[0, 0] < 0:
+            raise RuntimeError("stream detector: the first shard's first run continues a previous shard")
+        heads = np.flatnonzero(allr[:, 0] >= 0)  # a run continued over shard edges (start -1) joins its predecessor
+        dets = np.zeros(heads.size, _lib.DET_DTYPE)
+        if heads.size:
+            dets["start"] = allr[heads, 0]
+            dets["stop"] = np.maximum.reduceat(allr[:, 1], heads)
+        if not self.adaptive and dets.size and dets["stop"][-1] == ops.n_total:
+            dets["stop"][-1] = ops.n_total - 1  # burst_stops gets len-1 (main.py:414-415)
+            if dets["stop"][-1] - dets["start"][-1] <= 0:
                 raise AssertionError("Detection duration must be greater than 0")  # main.py:437
-        dets = np.zeros(len(merged), _lib.DET_DTYPE)
-        if merged:
-            a = np.array(merged, np.int64)
-            dets["start"], dets["stop"] = a[:, 0], a[:, 1]
         # dB means: the rank whose shard holds the run's start
         lo, hi = ops.frame0, ops.frame0 + ops.n_local
         mine = (dets["start"] >= lo) & (dets["start"] < hi)
