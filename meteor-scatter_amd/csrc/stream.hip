@@ -1010,7 +1010,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
                 KernelTimer timer(p->ctx, K_SSCAN);
                 hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
                                    p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
-                                   p->d_margin, p->d_thr, overflow, p->cfg.adaptive ? p->d_need : nullptr);
+                                   p->d_margin, p->d_thr, overflow, nullptr);
             }
             MSD_HIP(hipGetLastError());
             ++nround;
@@ -1026,6 +1026,20 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
         if (hc[1]) return fail(MSD_ERR_CAPACITY, "msd_stream_scan: more runs in a segment than cap_per_seg");
         if (hc[0] == 0) break;
         if (nround > p->nseg + 2 + R) return fail(MSD_ERR_INVALID, "msd_stream_scan: no fixed point");
+    }
+    if (p->cfg.adaptive) {
+        // the tiles whose fresh thresholds the fixed point reads: one more pass over every segment
+        // from its final entry state (same results), marking them -- the speculative rounds above
+        // would also mark tiles that only a wrong entry state reads
+        MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_active), 1, p->nseg, st));
+        {
+            KernelTimer timer(p->ctx, K_SSCAN);
+            hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail, p->d_fresh, P,
+                               st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns, p->d_margin, p->d_thr,
+                               overflow, p->d_need);
+        }
+        MSD_HIP(hipGetLastError());
+        MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));
     }
     p->scanned = true;
     if (exit_state) std::memcpy(exit_state, &ex, sizeof(SState));
