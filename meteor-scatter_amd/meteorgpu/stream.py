@@ -76,18 +76,22 @@ class RcclComm:
     def __init__(self, comm, rank: int, world: int):
         self.comm, self.rank, self.world = comm, int(rank), int(world)
         self.ctx = comm.ctx
+        self._cap, self._send, self._recv = 0, None, None  # grow-only device staging buffers
 
     def _gather_bytes(self, b: np.ndarray) -> np.ndarray:
         b = np.ascontiguousarray(b).view(np.uint8)
         n = b.size
-        send = self.ctx.alloc(max(n, 8))
-        recv = self.ctx.alloc(max(n, 8) * self.world)
+        if n > self._cap or self._send is None:
+            self._cap = max(n, 4096, 2 * self._cap)
+            self._send = self.ctx.alloc(self._cap)
+            self._recv = self.ctx.alloc(self._cap * self.world)
+        send, recv = self._send, self._recv
         if n:
             send.upload(b)
         _lib.check(self.ctx.lib.msd_comm_allgather(self.comm.h, send.ptr, recv.ptr, n))
         out = np.empty(n * self.world, np.uint8)
         if n:
-            recv.download(out)
+            recv.download(out)  # rank r's n bytes sit at r * n (ncclAllGather packs them)
         return out
 
     def allgather(self, a: np.ndarray) -> list[np.ndarray]:

@@ -227,3 +227,21 @@ def test_stream_detector_over_rccl_single_rank():
     finally:
         comm.close()
         ctx.close()
+
+
+def test_iq_dc_band_float32_global():
+    """a band straddling DC (its bins sit at both ends of the FFT-order row), float32 I/Q input,
+    the global detector: band delta within DELTA_TOL of scipy, same detections"""
+    from meteorgpu import iq, synth
+    from oracle import iq_oracle as Q
+    i, q, _ = synth.synth_iq(8, 192000, 20.0, 30.0, rate_per_min=6, snr_db=(25, 35))
+    fi, fq = (i / 32768).astype(np.float32), (q / 32768).astype(np.float32)
+    band, noise = (-80.0, 80.0), (2000.0, 2200.0)
+    assert iq.iq_band_bins(4096, 192000, band)[0] < 0 <= iq.iq_band_bins(4096, 192000, band)[1]
+    kw = dict(flag_adaptive_threshold=False)
+    dets, thr, delta, _ = iq.proc_iq_samples(fi, fq, 192000, band, noise, **kw)
+    rdets, rthr, _, _, rdelta = Q.proc_iq_ref(fi, fq, 192000, band, noise, **kw)
+    assert np.max(np.abs(delta - rdelta)) < DELTA_TOL
+    assert np.min(np.abs(rdelta - rthr)) > 10 * DELTA_TOL
+    assert len(rdets) > 0
+    assert [(d.t_start, d.t_stop) for d in dets] == [(r[0], r[1]) for r in rdets]
