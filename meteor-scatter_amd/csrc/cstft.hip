@@ -84,11 +84,11 @@ struct IQ<int16_t> {  // interleaved int16 I, Q
     __device__ static raw_t load(const int16_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
     __device__ static int re_i(raw_t r) { return (int)(int16_t)(r & 0xffffu); }
     __device__ static int im_i(raw_t r) { return (int)(int16_t)(r >> 16); }
-    __device__ static float2 f(raw_t r) { return make_float2((float)re_i(r), (float)im_i(r)); }
+    __device__ static float2 f(raw_t r) { return make_float2(cvt_i16_lo(r), cvt_i16_hi(r)); }
     using acc_t = int;
     __device__ static int wave_sum(int v) { return wave_sum_i(v); }
-    __device__ static int acc_re(raw_t r) { return re_i(r); }
-    __device__ static int acc_im(raw_t r) { return im_i(r); }
+    __device__ static int add_re(raw_t r, int acc) { return dot2_i16<1, 0>(r, acc); }
+    __device__ static int add_im(raw_t r, int acc) { return dot2_i16<0, 1>(r, acc); }
 };
 template <>
 struct IQ<float> {  // interleaved float32 I, Q (complex64)
@@ -97,8 +97,8 @@ struct IQ<float> {  // interleaved float32 I, Q (complex64)
     __device__ static float2 f(raw_t r) { return r; }
     using acc_t = float;
     __device__ static float wave_sum(float v) { return wave_sum_f(v); }
-    __device__ static float acc_re(raw_t r) { return r.x; }
-    __device__ static float acc_im(raw_t r) { return r.y; }
+    __device__ static float add_re(raw_t r, float acc) { return acc + r.x; }
+    __device__ static float add_im(raw_t r, float acc) { return acc + r.y; }
 };
 
 // SH = hop / 256 when the hop is a multiple of 256 below N (C5: hop 1024 → 4), else 0.
@@ -163,8 +163,8 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 v[r] = io::f(raw[r]);
-                sr += io::acc_re(raw[r]);
-                si += io::acc_im(raw[r]);
+                sr = io::add_re(raw[r], sr);
+                si = io::add_im(raw[r], si);
             }
             sr = io::wave_sum(sr);  // DPP row sums + readlane: no LDS round trips
             si = io::wave_sum(si);

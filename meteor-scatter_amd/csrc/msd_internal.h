@@ -123,6 +123,34 @@ __device__ __forceinline__ float wave_sum_f(float v) {
     return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 
+// int16 pairs packed in a 32-bit word (PCM16 samples, int16 I/Q): SDWA conversion of either half
+// straight to float (no separate shift / bit-field extract), and integer sums by v_dot2 (one
+// instruction adds both halves, or one of them, to an accumulator)
+#ifndef MSD_NO_SDWA
+__device__ __forceinline__ float cvt_i16_lo(uint32_t r) {
+    float f;
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(f) : "v"(r));
+    return f;
+}
+__device__ __forceinline__ float cvt_i16_hi(uint32_t r) {
+    float f;
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "=v"(f) : "v"(r));
+    return f;
+}
+typedef short msd_short2 __attribute__((ext_vector_type(2)));
+template <int WLO, int WHI>
+__device__ __forceinline__ int dot2_i16(uint32_t r, int acc) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(msd_short2, r), msd_short2{WLO, WHI}, acc, false);
+}
+#else
+__device__ __forceinline__ float cvt_i16_lo(uint32_t r) { return (float)(int16_t)(r & 0xffffu); }
+__device__ __forceinline__ float cvt_i16_hi(uint32_t r) { return (float)(int16_t)(r >> 16); }
+template <int WLO, int WHI>
+__device__ __forceinline__ int dot2_i16(uint32_t r, int acc) {
+    return acc + WLO * (int)(int16_t)(r & 0xffffu) + WHI * (int)(int16_t)(r >> 16);
+}
+#endif
+
 // makes `dev` current for the scope
 struct DeviceGuard {
     int prev = -1;

@@ -119,8 +119,9 @@ struct PairIO<int16_t> {
     __device__ static raw_t zero() { return 0u; }
     __device__ static int ilo(raw_t r) { return (int)(int16_t)(r & 0xffffu); }
     __device__ static int ihi(raw_t r) { return (int)(int16_t)(r >> 16); }
-    __device__ static float lo(raw_t r) { return (float)ilo(r); }
-    __device__ static float hi(raw_t r) { return (float)ihi(r); }
+    __device__ static float lo(raw_t r) { return cvt_i16_lo(r); }
+    __device__ static float hi(raw_t r) { return cvt_i16_hi(r); }
+    __device__ static int sum2(raw_t r, int acc) { return dot2_i16<1, 1>(r, acc); }
 };
 template <>
 struct PairIO<uint8_t> {
@@ -132,6 +133,7 @@ struct PairIO<uint8_t> {
     __device__ static int ihi(raw_t r) { return (int)((r >> 8) & 0xffu); }
     __device__ static float lo(raw_t r) { return (float)ilo(r); }
     __device__ static float hi(raw_t r) { return (float)ihi(r); }
+    __device__ static int sum2(raw_t r, int acc) { return acc + ilo(r) + ihi(r); }
 };
 template <>
 struct PairIO<float> {
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 if constexpr (IO::kInt) {
                     int s = 0;
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) s += IO::ilo(raw[q][r]) + IO::ihi(raw[q][r]);
+                    for (int r = 0; r < 8; ++r) s = IO::sum2(raw[q][r], s);
                     s = row_sum_i(s);
                     const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
                                     __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
