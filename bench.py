@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=16, help="processes of the multi-core CPU baseline "
                     "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
+    ap.add_argument("--shard-day", action="store_true",
+                    help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
+                         "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "
+                         "of a day per GPU (the default, weak scaling)")
     ap.add_argument("--workload", choices=("c3", "live", "c5", "files"), default="c3",
                     help="c3: the headline day batch (default); live: the phase-2 live detector "
                          "(Welch band powers + state machine) over a day of 4 kHz audio; c5: 192 kHz I/Q, "
@@ -411,16 +415,21 @@ def main():
                              f"same path as cpu_baseline; CPU: {cpu_model()}"}
     ctx = _lib.Context(local)
     n = FS * SECONDS
-    F = a.files
+    if a.shard_day:  # C4 strong scaling: files [lo, hi) of one day
+        from meteorgpu.shard import shard_range
+        lo, hi = shard_range(a.files, rank, world)
+    else:  # rank r holds day r (weak scaling)
+        lo, hi = 0, a.files
+    F = hi - lo
     bp = BatchPipeline(ctx, F, n, FS, nperseg=NPERSEG, noverlap=NOVERLAP, freq_band=BAND, noise_band=NOISE,
                        with_spectrogram=not a.no_spectrogram)
     for i in range(F):
-        bp.upload_file(i, pool[(i + rank) % POOL])
-    # rank r holds day r: file i starts at minute i of 2025-06-(1+r) 00:00 UTC
+        bp.upload_file(i, pool[(lo + i + (0 if a.shard_day else rank)) % POOL])
+    # file i starts at minute i of the day: 2025-06-01 (one day sharded) or 2025-06-(1+r) (a day per rank)
     epoch = datetime.datetime(1970, 1, 1)
-    day0 = datetime.datetime(2025, 6, 1) + datetime.timedelta(days=rank)
+    day0 = datetime.datetime(2025, 6, 1) + datetime.timedelta(days=0 if a.shard_day else rank)
     us = lambda t: (t - epoch) // datetime.timedelta(microseconds=1)  # noqa: E731
-    bp.set_start_times(np.array([us(day0 + datetime.timedelta(minutes=i)) for i in range(F)], np.int64),
+    bp.set_start_times(np.array([us(day0 + datetime.timedelta(minutes=lo + i)) for i in range(F)], np.int64),
                        us(day0))
     comm = None
     if dist is not None:
@@ -471,7 +480,7 @@ def main():
     blk_ms, blk_launches = ctx.timing_get(_lib.K_BLOCK)
     det_ms, det_launches = ctx.timing_get(_lib.K_DSCAN)
 
-    samples = world * F * n
+    samples = (a.files if a.shard_day else world * F) * n
     value = samples * a.steps / elapsed / 1e6
     out = {
         "metric": "Msamples/s processed (48 kHz SDR stream) + % HBM roofline, 1/2/4/8 MI355X",
@@ -482,7 +491,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.shard_day else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic: {POOL} seeded 60 s 48 kHz int16 noise+ping recordings replicated over {F} files/GPU",
@@ -495,7 +504,9 @@ def main():
             "samples_per_file": n,
             "frames_per_file": bp.T,
             "bins": bp.K,
-            "parallelism": f"files sharded over {world} GPU(s), 1 process per GPU",
+            "parallelism": (f"one day of {a.files} files sharded over {world} GPU(s) (C4, strong scaling)"
+                            if a.shard_day else f"a day of files per GPU over {world} GPU(s) (weak scaling)")
+                           + ", 1 process per GPU",
         },
         "detections_per_step": total_dets,
     }
