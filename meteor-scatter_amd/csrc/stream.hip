@@ -169,10 +169,10 @@ __global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restric
 constexpr int FR_MAXREC_LDS = 512;  // records kept in LDS (W up to ~32K); more are read from HBM
 
 #ifndef MSD_FR_THREADS
-#define MSD_FR_THREADS 128
+#define MSD_FR_THREADS 64
 #endif
 #ifndef MSD_FR_F
-#define MSD_FR_F 4
+#define MSD_FR_F 8
 #endif
 constexpr int FR_THREADS = MSD_FR_THREADS;       // a workgroup computes one tile
 constexpr int FR_F = MSD_FR_F;                   // frames per lane

@@ -245,3 +245,24 @@ def test_iq_dc_band_float32_global():
     assert np.min(np.abs(rdelta - rthr)) > 10 * DELTA_TOL
     assert len(rdets) > 0
     assert [(d.t_start, d.t_stop) for d in dets] == [(r[0], r[1]) for r in rdets]
+
+
+def test_iq_csv_matches_oracle(tmp_path):
+    """proc_iq_samples writes the reference's detection CSV (main.py:640-658) byte for byte as the
+    oracle does from its own detections, UTC columns included"""
+    import datetime
+    from meteorgpu import iq, synth
+    from oracle import dsp_oracle as O
+    from oracle import iq_oracle as Q
+    i, q, _ = synth.synth_iq(1, 192000, 40.0, 1000.0, rate_per_min=20)
+    t0 = datetime.datetime(2025, 6, 1, 13, 59, 50)
+    kw = dict(threshold_estimation_window_sec=5, threshold_freeze_after_detection_sec=2,
+              threshold_fixed_init_duration_sec=1, wav_start_date_time=t0)
+    out = tmp_path / "gpu.csv"
+    dets, *_ = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), out_csv_file=str(out), **kw)
+    rdets, *_ = Q.proc_iq_ref(i, q, 192000, (950, 1050), (-3050, -2950), **kw)
+    ref = tmp_path / "ref.csv"
+    # the dB column is compared within DELTA_TOL elsewhere; here the device's dB values stand in
+    O.write_csv_ref([(r[0], r[1], r[2], d.dB, r[4], r[5]) for r, d in zip(rdets, dets)], str(ref))
+    assert len(dets) == len(rdets) > 0
+    assert out.read_bytes() == ref.read_bytes()
