@@ -266,3 +266,32 @@ def test_iq_csv_matches_oracle(tmp_path):
     O.write_csv_ref([(r[0], r[1], r[2], d.dB, r[4], r[5]) for r, d in zip(rdets, dets)], str(ref))
     assert len(dets) == len(rdets) > 0
     assert out.read_bytes() == ref.read_bytes()
+
+
+def test_capacity_and_halo_errors_are_loud():
+    """more runs in a segment than its capacity, or a shard whose last numpy chunk runs past its
+    head halo, raise MsdError (never silently truncated results)"""
+    from meteorgpu import _lib, stream
+    d = make_delta(20000, 32, rate=0.05)
+    with pytest.raises(_lib.MsdError) as e:
+        _detect(d, True, 2.0, 300, 0, 10, seg_len=8192, cap=1)
+    assert e.value.code == _lib.MSD_ERR_CAPACITY
+
+    def body(r, comm):
+        lo, hi = shard_bounds(d.size, 2, r)
+        ctx = _lib.Context(0)
+        try:
+            cfg = _lib.det_cfg(True, 4.0, 300, 0, 50, 10)
+            plan = _lib.StreamPlan(ctx, cfg, d.size, lo, hi - lo, seg_len=1024, head_frames=100)
+            plan.set_delta(d[lo:hi])
+            try:
+                return stream.StreamDetector(stream.DeviceStreamOps(plan), comm, True, 4.0, 300, 10,
+                                             head_frames=100).run()
+            finally:
+                plan.close()
+        finally:
+            ctx.close()
+
+    with pytest.raises(_lib.MsdError) as e:
+        run_threads(2, body)
+    assert e.value.code == _lib.MSD_ERR_UNSUPPORTED
