@@ -90,6 +90,60 @@ __device__ __forceinline__ void dft8_windowed(float2 *v, const float2 *d, const 
     dft8_tail(v, a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]);
 }
 
+#ifdef MSD_STFT_PK
+// ---- frame-pair packed arithmetic (experiment MSD_STFT_PK, off by default): the wave's two frames A, B ride in the two halves of
+// 64-bit register pairs, {A.re, B.re} and {A.im, B.im}, so every butterfly is one v_pk_add_f32 /
+// v_pk_mul_f32 / v_pk_fma_f32 for both frames; twiddles and window values, shared by the frames,
+// are broadcast.  Half the VALU instructions of the scalar path, but no faster (A/B +1 %): in
+// isolation v_pk_add_f32 issues in 5.0 cycles vs 2.9 for v_add_f32 and v_pk_fma_f32 in 5.1 vs 4.2
+// (tools/ubench/pk_rate2.hip), in this kernel's mix a packed op costs about two scalar ones.
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct C2 {
+    f2 re, im;
+};
+__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
+__device__ __forceinline__ C2 padd(C2 a, C2 b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ C2 psub(C2 a, C2 b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ C2 pmi(C2 a) { return {a.im, -a.re}; }  // a * (-i)
+__device__ __forceinline__ C2 ptw(C2 a, float2 w) {               // a * w, w shared by both frames
+    const f2 wx = splat(w.x), wy = splat(w.y);
+    return {a.re * wx - a.im * wy, a.re * wy + a.im * wx};
+}
+__device__ __forceinline__ void pdft4(C2 &a0, C2 &a1, C2 &a2, C2 &a3) {
+    const C2 t0 = padd(a0, a2), t1 = psub(a0, a2), t2 = padd(a1, a3), t3 = pmi(psub(a1, a3));
+    a0 = padd(t0, t2);
+    a1 = padd(t1, t3);
+    a2 = psub(t0, t2);
+    a3 = psub(t1, t3);
+}
+__device__ __forceinline__ void pdft8_tail(C2 *v, C2 a0, C2 a1, C2 a2, C2 a3, C2 b0, C2 b1, C2 b2, C2 b3) {
+    const f2 s = splat(0.70710678118654752440f);
+    b1 = {(b1.re + b1.im) * s, (b1.im - b1.re) * s};
+    b2 = pmi(b2);
+    b3 = {(b3.im - b3.re) * s, -(b3.re + b3.im) * s};
+    pdft4(a0, a1, a2, a3);
+    pdft4(b0, b1, b2, b3);
+    v[0] = a0; v[2] = a1; v[4] = a2; v[6] = a3;
+    v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
+}
+__device__ __forceinline__ void pdft8(C2 *v) {
+    pdft8_tail(v, padd(v[0], v[4]), padd(v[1], v[5]), padd(v[2], v[6]), padd(v[3], v[7]), psub(v[0], v[4]),
+               psub(v[1], v[5]), psub(v[2], v[6]), psub(v[3], v[7]));
+}
+// dft8 of the windowed points (window pair w = (w_even, w_odd) per point, shared by the frames)
+__device__ __forceinline__ void pdft8_windowed(C2 *v, const float2 *w) {
+    C2 a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const f2 px = v[j + 4].re * splat(w[j + 4].x), py = v[j + 4].im * splat(w[j + 4].y);
+        const f2 qx = splat(w[j].x), qy = splat(w[j].y);
+        a[j] = {__builtin_elementwise_fma(v[j].re, qx, px), __builtin_elementwise_fma(v[j].im, qy, py)};
+        b[j] = {__builtin_elementwise_fma(v[j].re, qx, -px), __builtin_elementwise_fma(v[j].im, qy, -py)};
+    }
+    pdft8_tail(v, a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]);
+}
+#endif
+
 // Transpose-scratch layout (float2 index): bit 4 of n flips bits 1 and 3, plus 4 float2 of
 // padding per 32.  Together with the pass-3 lane table below it makes all four transpose
 // access patterns (16-B pass-1 writes, 8-B reads, 8-B pass-2 writes, pass-3 reads) free of
@@ -257,6 +311,116 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     FileCur prev = cur;
     bool have_prev = false;
 
+#ifdef MSD_STFT_PK  // experiment (off): frame-pair packed math; A/B +1 % — the v_pk ops cost about two scalar ops here
+    f2 *scr2 = reinterpret_cast<f2 *>(scr);  // the scratch as {A, B} pairs: re round, then im round
+    for (int64_t tl = tb; tl < te; ++tl) {
+        const bool has_next = tl + 1 < te;
+        const FileCur nxt = has_next ? advance(cur) : cur;
+        C2 P[8];
+        float2 wv[8];
+        // ---- detrend (consumes raw); the window is applied inside pass 1
+        {
+            float mean[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if constexpr (IO::kInt) {
+                    int s = 0;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) s = IO::sum2(raw[q][r], s);
+                    s = row_sum_i(s);
+                    const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
+                                    __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
+                    mean[q] = detrend ? (float)((double)tot * (1.0 / 1024.0)) : 0.f;
+                } else {
+                    float s = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) s += IO::lo(raw[q][r]) + IO::hi(raw[q][r]);
+                    s = row_sum_f(s);
+                    auto rl = [](float a, int lane) {
+                        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), lane));
+                    };
+                    const float tot = (rl(s, 0) + rl(s, 16)) + (rl(s, 32) + rl(s, 48));
+                    mean[q] = detrend ? tot * (1.0f / 1024.0f) : 0.f;
+                }
+            }
+            const f2 mv = {mean[0], mean[1]};
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                wv[r] = t_win[r * 64 + l];
+                P[r].re = f2{IO::lo(raw[0][r]), IO::lo(raw[1][r])} - mv;
+                P[r].im = f2{IO::hi(raw[0][r]), IO::hi(raw[1][r])} - mv;
+            }
+        }
+        if (have_prev) write_out(prev);
+        // ---- prefetch the next tile's frame pair into the (now free) sample registers
+        if (has_next) load_pair<T>(x, nxt, nxt.ti * F_TT + wcol, hop, l, raw);
+
+        // ---- pass 1 (Ns = 1): out[8 l + r]; transposed in two rounds (re pairs, im pairs)
+        pdft8_windowed(P, wv);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) scr2[phys(8 * l + r)] = h ? P[r].im : P[r].re;
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) (h ? P[r].im : P[r].re) = scr2[phys(l + 64 * r)];
+            wave_sync();
+        }
+        // ---- pass 2 (Ns = 8): out[64 (l>>3) + (l&7) + 8 r]
+        const int o2 = 64 * (l >> 3) + (l & 7);
+#pragma unroll
+        for (int r = 1; r < 8; ++r) P[r] = ptw(P[r], t_tw2[r * 64 + l]);
+        pdft8(P);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) scr2[phys(o2 + 8 * r)] = h ? P[r].im : P[r].re;
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) (h ? P[r].im : P[r].re) = scr2[phys(pi + 64 * r)];
+            wave_sync();
+        }
+        // ---- pass 3 (Ns = 64): butterfly pi(l) → lane holds Z[pi(l) + 64 r]
+#pragma unroll
+        for (int r = 1; r < 8; ++r) P[r] = ptw(P[r], t_tw3[r * 64 + l]);
+        pdft8(P);
+        // ---- post (see the unpacked branch below for the algebra), both frames at once
+        f2 pa[4], pb[4];
+        const f2 sc0 = splat(l == 0 ? 0.5f : 1.0f);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float2 wk = t_post[r * 64 + l];
+            const C2 sv = P[7 - r];
+            C2 m;
+            m.re = f2{dpp_f<0xB1>(sv.re.x), dpp_f<0xB1>(sv.re.y)};
+            m.im = f2{dpp_f<0xB1>(sv.im.x), dpp_f<0xB1>(sv.im.y)};
+            if (l < 2) m = (l == 0) ? P[(8 - r) & 7] : sv;
+            const C2 z = P[r];
+            const C2 e = {z.re + m.re, z.im - m.im};
+            const C2 o = {z.im + m.im, m.re - z.re};  // -i (z - conj m)
+            const C2 t = ptw(o, wk);
+            const C2 X1 = padd(e, t), X2 = psub(e, t);
+            pa[r] = X1.re * X1.re + X1.im * X1.im;
+            pb[r] = X2.re * X2.re + X2.im * X2.im;
+            if (r == 0) {
+                pa[r] *= sc0;
+                pb[r] *= sc0;
+            }
+        }
+        const f2 p256 = (P[4].re * P[4].re + P[4].im * P[4].im) * splat(4.0f);  // lane 0: bin 256
+        lds_barrier();  // the previous tile's write-out has finished reading the tile
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            *reinterpret_cast<f2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = pa[r];
+            *reinterpret_cast<f2 *>(&tile[(512 - pi - 64 * r) * F_PITCH + wcol]) = pb[r];
+        }
+        if (l == 0) *reinterpret_cast<f2 *>(&tile[256 * F_PITCH + wcol]) = p256;
+        lds_barrier();  // tile complete
+        prev = cur;
+        have_prev = true;
+        cur = nxt;
+    }
+#else
     for (int64_t tl = tb; tl < te; ++tl) {
         const bool has_next = tl + 1 < te;
         const FileCur nxt = has_next ? advance(cur) : cur;
@@ -400,6 +564,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         have_prev = true;
         cur = nxt;
     }
+#endif
     write_out(prev);  // the last tile (complete since the loop's final barrier)
 }
 
