@@ -128,7 +128,10 @@ class IQShardDetector:
                  threshold_std_factor=4.0, flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                  threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                  threshold_fixed_init_duration_sec=10, rank: int = 0, world: int = 1, dtype=np.int16,
-                 seg_len: int = 8192):
+                 seg_len: int = 8192, chunk_frames: int | None = None):
+        """chunk_frames: keep only that many frames of spectrogram in HBM and stream the shard through
+        it (``process_host``); the detector still sees the whole shard's delta.  A 24 h 192 kHz
+        stream (66 GB of int16 I/Q, 265 GB of spectrogram) then runs on one GPU."""
         self.ctx, self.fs, self.N = ctx, fs, int(nperseg)
         self.hop = self.N - int(noverlap)
         self.block_sec = self.hop / fs
@@ -142,7 +145,10 @@ class IQShardDetector:
         self.F0 = _blocks(threshold_fixed_init_duration_sec, bs) if self.adaptive else 0
         Fa = _blocks(threshold_freeze_after_detection_sec, bs) if self.adaptive else 0
         Fb = _blocks(threshold_freeze_before_detection_sec, bs) if self.adaptive else 0
-        self.batch = IQBatch(ctx, 1, max(self.s1 - self.s0, 1), fs, self.N, noverlap, dtype)
+        nloc = self.f1 - self.f0
+        self.chunk = int(chunk_frames) if chunk_frames and 0 < int(chunk_frames) < nloc else None
+        nb = (self.chunk - 1) * self.hop + self.N if self.chunk else max(self.s1 - self.s0, 1)
+        self.batch = IQBatch(ctx, 1, nb, fs, self.N, noverlap, dtype)
         self.d_frames = ctx.alloc(8)
         self.d_frames.upload(np.array([self.batch.T if self.s1 > self.s0 else 0], np.int64))
         cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
@@ -160,6 +166,26 @@ class IQShardDetector:
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                    self.noise, self.plan.d_delta, self.batch.T)
 
+    def process_host(self, iq_shard: np.ndarray):
+        """interleaved I/Q of the shard's samples [s0, s1) on the host → the shard's delta in the
+        stream plan, `chunk_frames` frames at a time (or all at once without chunking)"""
+        iq_shard = np.ascontiguousarray(iq_shard)
+        nloc = self.f1 - self.f0
+        if not self.chunk:
+            if nloc > 0:
+                self.upload(iq_shard)
+            self.spectrogram_and_delta()
+            return
+        for c0 in range(0, nloc, self.chunk):
+            nf = min(self.chunk, nloc - c0)
+            a = c0 * self.hop
+            b = a + (nf - 1) * self.hop + self.N
+            self.batch.upload(0, iq_shard[2 * a: 2 * b])
+            self.d_frames.upload(np.array([nf], np.int64))
+            self.batch.run()  # frames past nf read stale samples; their powers are not used
+            _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
+                                   self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T)
+
     def detect(self, comm=None, thresholds: bool = True) -> _stream.StreamResult:
         return _stream.StreamDetector(self.ops, comm or _stream.LocalComm(), self.adaptive, self.k, self.W,
                                       self.F0).run(thresholds)
@@ -173,19 +199,19 @@ def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072
                     flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                     threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                     threshold_fixed_init_duration_sec=10, wav_start_date_time=None, out_csv_file=None,
-                    device: int = 0):
+                    device: int = 0, chunk_sec: float | None = None):
     """The batch detector of dsp/src/main.py (:380-527, :640-658) over an I/Q recording with the STFT
-    frame as the block.  Returns (detections [OutputDetection], thresholds, delta, result)."""
+    frame as the block.  Returns (detections [OutputDetection], thresholds, delta, result).
+    chunk_sec: stream the spectrogram through HBM in chunks of that many seconds (long recordings)."""
     buf, code = interleave(i, q)
     n = buf.size // 2
     det = IQShardDetector(context(device), n, fs, nperseg, noverlap, freq_band, noise_band, threshold_std_factor,
                           flag_adaptive_threshold, threshold_estimation_window_sec,
                           threshold_freeze_before_detection_sec, threshold_freeze_after_detection_sec,
-                          threshold_fixed_init_duration_sec, dtype=buf.dtype)
+                          threshold_fixed_init_duration_sec, dtype=buf.dtype,
+                          chunk_frames=int(chunk_sec * fs / (nperseg - noverlap)) if chunk_sec else None)
     try:
-        if det.T > 0:
-            det.upload(buf[2 * det.s0: 2 * det.s1])
-        det.spectrogram_and_delta()
+        det.process_host(buf[2 * det.s0: 2 * det.s1])
         res = det.detect()
         delta = det.plan.delta()
     finally:

@@ -295,3 +295,17 @@ def test_capacity_and_halo_errors_are_loud():
     with pytest.raises(_lib.MsdError) as e:
         run_threads(2, body)
     assert e.value.code == _lib.MSD_ERR_UNSUPPORTED
+
+
+def test_iq_chunked_spectrogram_matches_whole():
+    """streaming the spectrogram through HBM in chunks (long recordings on one GPU) gives the same
+    delta, bit for bit, and the same detections as one pass"""
+    from meteorgpu import iq, synth
+    i, q, _ = synth.synth_iq(2, 192000, 40.0, 1000.0, rate_per_min=20)
+    kw = dict(threshold_estimation_window_sec=5, threshold_freeze_after_detection_sec=2,
+              threshold_fixed_init_duration_sec=1)
+    d1, t1, delta1, _ = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), **kw)
+    d2, t2, delta2, _ = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), chunk_sec=3.3, **kw)
+    assert np.array_equal(delta1, delta2)
+    assert [(d.t_start, d.t_stop, d.dB) for d in d1] == [(d.t_start, d.t_stop, d.dB) for d in d2]
+    assert np.array_equal(np.asarray(t1), np.asarray(t2), equal_nan=True)
