@@ -142,3 +142,26 @@ def test_gloo_world2(tmp_path):
         assert np.array_equal(np.load(tmp_path / f"db{r}.npy"), np.array([w[2] for w in want]))
     t = np.concatenate([np.load(tmp_path / f"t{r}.npy") for r in range(2)])
     assert np.array_equal(t, np.asarray(thr), equal_nan=True)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_configs_and_cuts(seed):
+    """seeded random detector settings and shard cuts (including empty shards and cuts inside
+    runs): the protocol equals the one-process oracle"""
+    rng = np.random.default_rng(9000 + seed)
+    n = int(rng.integers(300, 4000))
+    d = make_delta(n, 100 + seed, rate=float(rng.uniform(0.002, 0.05)))
+    adaptive = bool(rng.integers(0, 4) > 0)
+    k = float(rng.choice([1.5, 2.5, 4.0]))
+    W, Fa, F0 = int(rng.integers(0, 400)), int(rng.integers(0, 300)), int(rng.integers(0, 200))
+    world = int(rng.integers(1, 5))
+    cuts = sorted(int(c) for c in rng.integers(0, n + 1, world - 1))
+    try:
+        want = oracle(d, adaptive, k, W, Fa, F0)
+    except AssertionError:
+        with pytest.raises(AssertionError):
+            run_protocol(d, world, adaptive, k, W, Fa, F0, cuts)
+        return
+    res = run_protocol(d, world, adaptive, k, W, Fa, F0, cuts)
+    check(res, d, adaptive, k, W, Fa, F0)
+    assert want is not None
