@@ -227,3 +227,23 @@ def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072
         write_csv(out, out_csv_file)
     thr = [np.float64(v) for v in res.thresholds] if det.adaptive else np.float64(res.thr0)
     return out, thr, delta, res
+
+
+def proc_iq_wav_file(file_path, freq_band, noise_band, nperseg=4096, noverlap=3072, threshold_std_factor=4.0,
+                     flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
+                     threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
+                     threshold_fixed_init_duration_sec=10, wav_start_date_time=None, out_csv_file=None,
+                     device: int = 0, chunk_sec: float | None = None):
+    """proc_iq_samples on a 2-channel (I, Q) WAV recording, read by the native reader (the SDR's
+    I/Q recording; dsp/src/main.py:249-268 reads the demodulated mono audio instead).  Returns
+    (detections, thresholds, delta, result) and writes the reference's CSV if asked."""
+    import os
+    from . import ingest
+    assert os.path.isfile(file_path), f"File {file_path} does not exist"
+    info = ingest.probe(file_path)
+    assert info.channels == 2, "Only 2-channel (I, Q) WAV files are supported"
+    fs, data = ingest.read(file_path)
+    return proc_iq_samples(data[:, 0], data[:, 1], fs, freq_band, noise_band, nperseg, noverlap,
+                           threshold_std_factor, flag_adaptive_threshold, threshold_estimation_window_sec,
+                           threshold_freeze_before_detection_sec, threshold_freeze_after_detection_sec,
+                           threshold_fixed_init_duration_sec, wav_start_date_time, out_csv_file, device, chunk_sec)

@@ -354,3 +354,16 @@ def test_random_sharded_device(seed):
         assert np.array_equal(np.concatenate([r.thresholds for r in res]), np.asarray(thr), equal_nan=True)
     else:
         assert res[0].thr0 == thr
+
+
+def test_iq_wav_file(tmp_path):
+    """a 2-channel I/Q WAV through the native reader gives the same detections and CSV as the samples"""
+    from meteorgpu import iq, synth, wav
+    i, q, _ = synth.synth_iq(1, 192000, 40.0, 1000.0, rate_per_min=20)
+    path = tmp_path / "iq.wav"
+    wav.write(path, 192000, np.stack([i, q], 1))
+    kw = dict(threshold_estimation_window_sec=5, threshold_freeze_after_detection_sec=2,
+              threshold_fixed_init_duration_sec=1)
+    a, *_ = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), out_csv_file=str(tmp_path / "a.csv"), **kw)
+    b, *_ = iq.proc_iq_wav_file(str(path), (950, 1050), (-3050, -2950), out_csv_file=str(tmp_path / "b.csv"), **kw)
+    assert len(a) > 0 and (tmp_path / "a.csv").read_bytes() == (tmp_path / "b.csv").read_bytes()

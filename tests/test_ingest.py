@@ -106,3 +106,15 @@ def test_wav_day_matches_single_file_drop_in(tmp_path):
         assert [(int(a["start"]), int(a["stop"]), float(a["db"])) for a in d] == ref
         total += len(ref)
     assert total > 0 and int(hist.sum()) == total
+
+
+def test_iq_wav_file_rejects_mono(tmp_path):
+    """the I/Q entry point asserts a 2-channel file before touching the GPU"""
+    import pytest as _pt
+    from meteorgpu import iq, wav
+    p = tmp_path / "mono.wav"
+    wav.write(p, 192000, np.zeros(4096, np.int16))
+    with _pt.raises(AssertionError, match="2-channel"):
+        iq.proc_iq_wav_file(str(p), (950, 1050), (-3050, -2950))
+    with _pt.raises(AssertionError, match="does not exist"):
+        iq.proc_iq_wav_file(str(tmp_path / "nope.wav"), (950, 1050), (-3050, -2950))
