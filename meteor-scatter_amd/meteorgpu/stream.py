@@ -46,6 +46,8 @@ class LocalComm:
     def allgather(self, a: np.ndarray) -> list[np.ndarray]:
         return [np.array(a, copy=True)]
 
+    allgather_fixed = allgather  # every rank sends the same number of elements
+
 
 class TorchComm:
     """torch.distributed process group (gloo on the host; tests and CPU runs)."""
@@ -68,6 +70,13 @@ class TorchComm:
         outs = [torch.zeros_like(t) for _ in range(self.world)]
         self.dist.all_gather(outs, t, group=self.group)
         return [o.numpy()[: int(k.item())].copy() for o, k in zip(outs, ns)]
+
+    def allgather_fixed(self, a: np.ndarray) -> list[np.ndarray]:
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(a).copy())
+        outs = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(outs, t, group=self.group)
+        return [o.numpy().copy() for o in outs]
 
 
 class RcclComm:
@@ -102,6 +111,11 @@ class RcclComm:
         buf[: a.size] = a
         got = self._gather_bytes(buf).view(a.dtype).reshape(self.world, -1)
         return [got[r, : int(ns[r])].copy() for r in range(self.world)]
+
+    def allgather_fixed(self, a: np.ndarray) -> list[np.ndarray]:
+        a = np.ascontiguousarray(a)
+        got = self._gather_bytes(a).view(a.dtype).reshape(self.world, -1)
+        return [got[r].copy() for r in range(self.world)]
 
 
 # ---------------------------------------------------------------- detector state
@@ -158,8 +172,11 @@ class StreamDetector:
         if self.comm.world == 1:  # nothing before or after the only shard
             ops.set_halos(np.zeros(0), np.zeros(0))
             return
-        tails = self.comm.allgather(ops.delta(max(0, n - self.W), n) if self.W > 0 else np.zeros(0))
-        heads = self.comm.allgather(ops.delta(0, min(self.H, n)))
+        tail = ops.delta(max(0, n - self.W), n) if self.W > 0 else np.zeros(0)
+        head = ops.delta(0, min(self.H, n))
+        got = self.comm.allgather(np.concatenate([[float(tail.size)], tail, head]))  # one exchange
+        tails = [g[1: 1 + int(g[0])] for g in got]
+        heads = [g[1 + int(g[0]):] for g in got]
         before = np.concatenate([np.zeros(0)] + tails[:r])
         after = np.concatenate([np.zeros(0)] + heads[r + 1:])
         tail = before[before.size - ops.n_tail:] if ops.n_tail else before[:0]
@@ -188,15 +205,17 @@ class StreamDetector:
         exit_, _ = ops.scan(thr0, entry, True)
         rounds = 1
         while True:
-            exits = [_unpack(e) for e in comm.allgather(_pack(exit_))]
-            new = exits[r - 1] if r > 0 else entry
-            changed = r > 0 and not same_state(new, entry, ops.frame0, F0)
-            flags = comm.allgather(np.array([1 if changed else 0], np.int64))
-            if not any(int(f[0]) for f in flags):
+            # one exchange per round: every rank's exit and entry state and first frame, so each
+            # rank decides every rank's "entry changed" alike
+            got = comm.allgather_fixed(np.concatenate([_pack(exit_), _pack(entry), [ops.frame0]]))
+            exits = [_unpack(g[0:3]) for g in got]
+            changed = [q > 0 and not same_state(exits[q - 1], _unpack(got[q][3:6]), int(got[q][6]), F0)
+                       for q in range(comm.world)]
+            if not any(changed):
                 return rounds
             rounds += 1
-            if changed:
-                entry = new
+            if changed[r]:
+                entry = exits[r - 1]
                 exit_, _ = ops.scan(thr0, entry, False)
 
     def run(self, thresholds: bool = True) -> StreamResult:
@@ -212,13 +231,15 @@ class StreamDetector:
         rounds = self.scan(thr0)
         while self.adaptive:  # until the last scan read exact thresholds only, on every rank
             n = ops.refine()
-            if not any(int(f[0]) for f in comm.allgather(np.array([n], np.int64))):
+            if not any(int(f[0]) for f in comm.allgather_fixed(np.array([n], np.int64))):
                 break
             rounds += self.scan(thr0)
         # runs of every shard, merged in stream order (a run continued across an edge has start -1)
         local, margin = ops.runs()
-        parts = comm.allgather(np.stack([local["start"], local["stop"]], 1).reshape(-1).astype(np.int64))
-        margin = min(float(m[0]) for m in comm.allgather(np.array([margin])))
+        got = comm.allgather(np.concatenate([np.array([margin], np.float64).view(np.int64),
+                                             np.stack([local["start"], local["stop"]], 1).reshape(-1)]).astype(np.int64))
+        margin = min(float(g[:1].view(np.float64)[0]) for g in got)
+        parts = [g[1:] for g in got]
         allr = np.concatenate([np.zeros(0, np.int64)] + parts).reshape(-1, 2)
         if allr.size and allr[0, 0] < 0:
             raise RuntimeError("stream detector: the first shard's first run continues a previous shard")
@@ -236,10 +257,10 @@ class StreamDetector:
         mine = (dets["start"] >= lo) & (dets["start"] < hi)
         db_local = ops.db(dets[mine])["db"] if mine.any() else np.zeros(0)
         db_all = np.full(len(dets), np.nan)
-        owners = comm.allgather(np.flatnonzero(mine).astype(np.int64))
-        vals = comm.allgather(np.asarray(db_local, np.float64))
-        for idx, v in zip(owners, vals):
-            db_all[idx] = v
+        for g in comm.allgather(np.concatenate([np.flatnonzero(mine).astype(np.int64),
+                                                np.asarray(db_local, np.float64).view(np.int64)])):
+            m = g.size // 2  # the owner's detection indices, then their dB bits
+            db_all[g[:m]] = g[m:].view(np.float64)
         dets["db"] = db_all
         thr = None if not thresholds else (ops.thresholds() if self.adaptive else np.array([thr0]))
         return StreamResult(dets, thr0, thr, margin, rounds)
