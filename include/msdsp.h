@@ -69,8 +69,12 @@ int msd_memcpy_d2h(msd_ctx *ctx, void *dst, const void *src, size_t bytes);
 int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
 
 /* Options: MSD_OPT_GENERIC_STFT = 1 → use the generic STFT kernel even where a
- * specialised one exists (A/B testing of the kernels; results must agree). */
+ * specialised one exists (A/B testing of the kernels; results must agree).
+ * MSD_OPT_FRESH_ALL = 1 → the C5 stream detector computes every adaptive threshold exactly up
+ * front instead of only where a scan reads it (A/B of that scheme; results must agree; also
+ * set by MSD_FRESH_ALL=1 in the environment). */
 #define MSD_OPT_GENERIC_STFT 1
+#define MSD_OPT_FRESH_ALL 2
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.

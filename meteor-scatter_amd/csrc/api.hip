@@ -222,6 +222,7 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
     if (!ctx) return fail(MSD_ERR_INVALID, "null ctx");
     switch (option) {
         case MSD_OPT_GENERIC_STFT: ctx->force_generic = value != 0; return MSD_OK;
+        case MSD_OPT_FRESH_ALL: ctx->fresh_all = value != 0; return MSD_OK;
         default: return fail(MSD_ERR_INVALID, "msd_set_option: unknown option");
     }
 }

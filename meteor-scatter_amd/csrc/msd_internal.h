@@ -39,6 +39,7 @@ struct msd_ctx {
     hipEvent_t fence_ev = nullptr;      // cross-stream ordering (msd_fence)
     bool timing = false;
     bool force_generic = false;  // MSD_OPT_GENERIC_STFT
+    bool fresh_all = false;      // MSD_OPT_FRESH_ALL
     std::vector<msd::EventPair> pending;  // recorded, not yet folded into totals
     std::vector<hipEvent_t> pool;         // reusable events
     double total_ms[msd::K_COUNT] = {};

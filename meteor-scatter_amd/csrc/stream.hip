@@ -915,7 +915,7 @@ int msd_stream_fresh(msd_stream_plan *p) {
         return e && e[0] == '1';
     }();
     MSD_HIP(hipMemsetAsync(p->d_need, 0, sizeof(int32_t) * p->ntiles, st));
-    if (all) MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_need), 1, p->ntiles, st));
+    if (all || p->ctx->fresh_all) MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_need), 1, p->ntiles, st));
     MSD_HIP(hipMemsetAsync(p->d_done, 0, sizeof(int32_t) * (p->ntiles + 1), st));
     // frames [0, jshort) have windows shorter than W: exact right away
     int64_t jshort = P.W - p->frame0;

@@ -37,6 +37,7 @@ DTYPE_CODES = {
 K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE, K_CSTFT = 0, 1, 2, 3, 4, 5, 6
 K_IQDELTA, K_FRESH, K_SSCAN = 7, 8, 9
 OPT_GENERIC_STFT = 1
+OPT_FRESH_ALL = 2
 COMM_ID_BYTES = 128
 
 

@@ -367,3 +367,23 @@ def test_iq_wav_file(tmp_path):
     a, *_ = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), out_csv_file=str(tmp_path / "a.csv"), **kw)
     b, *_ = iq.proc_iq_wav_file(str(path), (950, 1050), (-3050, -2950), out_csv_file=str(tmp_path / "b.csv"), **kw)
     assert len(a) > 0 and (tmp_path / "a.csv").read_bytes() == (tmp_path / "b.csv").read_bytes()
+
+
+def test_fresh_all_option_agrees():
+    """MSD_OPT_FRESH_ALL (every adaptive threshold exact up front) and the default scheme (only
+    where a scan reads them) give identical results"""
+    from meteorgpu import _lib, stream
+    d = make_delta(30000, 41, rate=0.01)
+    out = []
+    for opt in (0, 1):
+        ctx = _lib.Context(0)
+        try:
+            ctx.set_option(_lib.OPT_FRESH_ALL, opt)
+            out.append(stream.detect_stream(ctx, d, d.size, 0, adaptive=True, k_std=4.0, window_blocks=2000,
+                                            freeze_after_blocks=500, fixed_init_blocks=100, seg_len=1024))
+        finally:
+            ctx.close()
+    a, b = out
+    assert np.array_equal(a.detections, b.detections)
+    assert np.array_equal(a.thresholds, b.thresholds, equal_nan=True)
+    _check(a, d, True, 4.0, 2000, 500, 100)
