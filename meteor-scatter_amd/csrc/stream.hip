@@ -532,15 +532,25 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
     bool have = false;
     double min_margin = __builtin_inf();
 
+    // the next step's delta and fresh threshold are loaded one step ahead (the loads do not depend
+    // on the state), so the scalar walk of a step overlaps the memory latency of the next
+    auto ld = [&](int64_t k, double &dv, double &fr) {
+        const int64_t j = k + lane < b ? k + lane : (k < b ? k : a);
+        dv = delta[j];
+        fr = fresh[j];
+    };
+    double dv_n, fr_n;
+    ld(a, dv_n, fr_n);
     for (int64_t k = a; k < b; k += 64) {
         const int nvalid = (int)(b - k < 64 ? b - k : 64);
         const bool valid = lane < nvalid;
         const int64_t j = valid ? k + lane : k;
         const int64_t gi = P.frame0 + j;  // global frame of this lane
         const int64_t pos = P.frame0 + k;
-        const double dv = delta[j];
+        const double dv = dv_n, fr = fr_n;
+        ld(k + 64, dv_n, fr_n);
         const bool init = gi < P.F0;
-        const double t_unf = init ? thr0 : fresh[j];
+        const double t_unf = init ? thr0 : fr;
         const uint64_t A_unf = __ballot(valid && dv > t_unf);
         double t_fin = t_unf;
         uint64_t D = 0, U = 0;  // detected, unfrozen (fresh threshold used)
