@@ -1,3 +1,5 @@
+"""Debug (GPU box): wall time of each phase of one C5 step (spectrogram + delta, then every
+StreamDetector device call with a synchronize) on the 3 h bench shard."""
 import os, sys, time
 sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "..", "meteor-scatter_amd")]
 import numpy as np

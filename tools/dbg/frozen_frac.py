@@ -1,3 +1,5 @@
+"""Debug (GPU box): fraction of frames / 512-frame tiles where the adaptive detector recomputes
+its threshold on the C5 bench stream (how much exact-threshold work the refine scheme needs)."""
 import sys, os
 sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "..", "meteor-scatter_amd")]
 import numpy as np

@@ -1,3 +1,5 @@
+"""Debug (GPU box): tiles computed by each msd_stream_refine call on an N-minute bench-like I/Q
+stream (argv[1] minutes), against the tiles where the thresholds actually change."""
 import sys, os
 sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "..", "meteor-scatter_amd")]
 import numpy as np
