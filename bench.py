@@ -309,6 +309,7 @@ def main_c5(a, world, rank, local, dist):
                    "parallelism": f"time shards over {world} GPU(s), 1 process per GPU"},
         "detections_per_step": int(len(res.detections)),
         "state_rounds": int(res.rounds),
+        "exact_threshold_frames": int(res.refined),
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": load_pmc_traffic("cstft", frames=T, nperseg=C5_N),

@@ -250,8 +250,15 @@ int msd_stream_buffers(msd_stream_plan *plan, double **delta, double **tail, int
  * (cap >= chunks), *first_chunk = global index of the first chunk. */
 int msd_stream_chunk_sums(msd_stream_plan *plan, int32_t use_mean, double mean, double *sums, int64_t cap,
                           int64_t *nchunks, int64_t *first_chunk);
+/* on = 1 (default): every threshold the scan reads is numpy-exact, so the thresholds buffer holds
+ * the reference's `thresholds` list.  on = 0 (decisions only): thresholds are predicted with a
+ * rounding-error bound, and made exact only for the frames where a decision is within the bound
+ * or where a detection holds the threshold; the detections are the same, the thresholds buffer
+ * is not the reference's list.  Call before msd_stream_fresh. */
+int msd_stream_set_exact_thresholds(msd_stream_plan *plan, int32_t on);
 int msd_stream_fresh(msd_stream_plan *plan); /* async; needs the tail halo */
-/* synchronous; *computed = tiles made exact now (0: the previous scan read exact values only) */
+/* synchronous; *computed = tiles (decisions only: frames) made exact now (0: the previous scan
+ * read exact values only where they decide) */
 int msd_stream_refine(msd_stream_plan *plan, int32_t *computed);
 /* thr0 = mean + k*std of the whole stream.  reset = 1: every segment restarts from the clean
  * state (first call); 0: only the entry state changed.  Synchronous; *rounds = scan launches. */

@@ -15,6 +15,10 @@
 //                          own 8 consecutive frames: one LDS element feeds 8 frames' accumulators
 //                          (register blocking), the leaves stream through double-buffered LDS
 //   fresh_short_kernel     frames i < W (windows delta[0:i], a different tree per frame)
+//   approx_kernel          every frame's threshold from prefix sums (the predictor) and, in
+//                          decisions-only mode, a rounding-error bound on |predicted - numpy|
+//   fresh_list_kernel      decisions-only mode: numpy-exact thresholds of the frames the scan
+//                          listed (near ties, triggers), one wave per frame
 //   scan_kernel            the freeze/run state machine, one wave per segment: lane j evaluates
 //                          frame pos+j; with the freeze state fixed the decisions of 64 frames are
 //                          two ballots (fresh threshold / held threshold), and only the frames
@@ -57,10 +61,17 @@ struct msd_stream_plan {
     int32_t *d_need = nullptr;  // [ntiles] a scan used fresh thresholds in the tile
     int32_t *d_done = nullptr;  // [ntiles] the tile's exact thresholds are computed (+1: counter)
     double2 *d_pre = nullptr;   // [nblk + 1] prefix sums of x, x^2 (the predictor)
+    // decisions-only mode (msd_stream_set_exact_thresholds(plan, 0)): exact thresholds per frame,
+    // only where a decision or a held threshold depends on them
+    double *d_eps = nullptr;      // [n_local] bound on |predicted - numpy threshold|
+    uint8_t *d_exact = nullptr;   // [n_local] fresh[j] is numpy-exact
+    int32_t *d_list = nullptr;    // [n_local] frames the last marking pass needs exact
+    bool decide = false;
     int64_t ntiles = 0, nblk = 0;
     int nleaf = 0;
     double thr0 = 0;
     bool scanned = false;
+    bool want_exact = true;  // msd_stream_set_exact_thresholds
 };
 
 namespace msd {
@@ -189,6 +200,8 @@ struct FreshParams {
     int64_t n_local, frame0, n_tail, x_len, W, F0;
     double k;
     int nleaf;
+    int64_t pre_per;  // prefix blocks per thread of blockscan_kernel (error bound of the predictor)
+    double eps_scale; // test hook (MSD_STREAM_EPS_SCALE): widens the bound, more frames made exact
 };
 
 // one pass of the program over this lane's 8 frames: out[f] = numpy np.sum of the window of frame f
@@ -287,7 +300,7 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
 #pragma unroll
             for (int f = 0; f < FR_F; ++f)
 #pragma unroll
-                for (int k = 0; k < 8; ++k) r[f][k] = -0.0;
+                for (int k = 0; k < 8; ++k) r[f][k] = SQ ? 0.0 : -0.0;  // squares are >= +0: +0.0 is exact
             auto group = [&](int g, auto first, auto last) {
                 double v[8];
                 if constexpr (FR_F == 8) {
@@ -472,18 +485,51 @@ __device__ __forceinline__ double2 prefix_at(const double *__restrict__ x, const
     return r;
 }
 
+// eps (decisions-only mode): a bound on |predicted - numpy's threshold| from the rounding-error
+// bounds of both (u = 2^-53; an element passes through at most d additions: |error of a sum| <=
+// d u sum|x|, with sum|x| <= sqrt(len sum x^2)), times 4.  Frames whose |delta - predicted| exceeds it
+// are decided exactly by the prediction.  NaN anywhere gives a NaN bound, which the scan treats as a
+// near tie (exact threshold computed).
+__device__ __forceinline__ double sd_err(double e, double sig_lo) {  // |sqrt(a) - sigma| given |a - sigma^2| <= e
+    const double r = sqrt(e);
+    return sig_lo > 0.0 ? fmin(r, e / sig_lo) : r;
+}
+
 __global__ __launch_bounds__(256) void approx_kernel(const double *__restrict__ x, const double2 *__restrict__ pre,
-                                                     FreshParams P, int64_t jbeg, double *__restrict__ fresh) {
+                                                     FreshParams P, int64_t jbeg, double *__restrict__ fresh,
+                                                     double *__restrict__ eps) {
     const int64_t j = jbeg + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= P.n_local) return;
     const int64_t i = P.frame0 + j;
     if (i < P.F0) return;
     const int64_t e = P.n_tail + j;
-    const double2 hi = prefix_at(x, pre, e), lo = prefix_at(x, pre, e - P.W);
-    const double m = (hi.x - lo.x) / (double)P.W;
-    double v = (hi.y - lo.y) / (double)P.W - m * m;
+    const int64_t len = i < P.W ? i : P.W;  // windows before frame W are delta[0:i] (x index 0 = frame 0)
+    const double2 hi = prefix_at(x, pre, e), lo = prefix_at(x, pre, e - len);
+    const double fl = (double)len;
+    const double m = (hi.x - lo.x) / fl;
+    double v = (hi.y - lo.y) / fl - m * m;
     v = v > 0.0 ? v : 0.0;
-    fresh[j] = m + P.k * sqrt(v);
+    const double sd = sqrt(v);
+    const double thr = m + P.k * sd;
+    fresh[j] = thr;
+    if (!eps) return;
+    const double u = 0x1p-53, ak = fabs(P.k);
+    // predictor: prefix sums through <= 63 + per + 10 + per + 63 additions (+1 for x*x)
+    const double d2 = 140.0 + 2.0 * (double)P.pre_per;
+    const double S1 = hi.x - lo.x, S2 = hi.y - lo.y;
+    const double eS1 = 1.01 * d2 * u * (sqrt((double)e * hi.y) + sqrt((double)(e - len) * lo.y)) + u * fabs(S1);
+    const double eS2 = 1.01 * (d2 + 1.0) * u * (hi.y + lo.y) + u * fabs(S2);
+    const double em_a = eS1 / fl + 2.0 * u * fabs(m);
+    const double ev_a = (eS2 + u * fabs(S2)) / fl + em_a * (2.0 * fabs(m) + em_a) + u * m * m + 2.0 * u * v;
+    const double sig_lo = sqrt(fmax(v - ev_a, 0.0));
+    // numpy: s = 0.0; s += pairwise(8192-chunk): leaves of <= 128 (16 adds per accumulator, 3 to
+    // combine, 7 remainder), <= 6 tree levels, one add per chunk
+    const double d1 = 48.0 + fl / 8192.0;
+    const double A = sqrt(fl * (S2 + eS2));  // >= sum |x| over the window
+    const double em_np = d1 * u * A / fl + 2.0 * u * (fabs(m) + em_a);
+    const double ev_np = 1.01 * (d1 + 4.0) * u * (v + ev_a + em_np * em_np) + em_np * em_np;
+    const double es = sd_err(ev_a, sig_lo) + sd_err(ev_np, sig_lo) + 4.0 * u * (sd + sqrt(ev_a + ev_np));
+    eps[j] = P.eps_scale * 4.0 * (em_a + em_np + ak * es + 4.0 * u * (fabs(thr) + ak * sd));
 }
 
 // frames with i < W: window delta[0:i] (only the shard that holds the stream's first W frames)
@@ -502,6 +548,27 @@ __global__ __launch_bounds__(256) void fresh_short_kernel(const double *__restri
     }
 }
 
+// decisions-only mode: the frames the marking pass listed, numpy-exact, one wave per frame
+__global__ __launch_bounds__(256) void fresh_list_kernel(const double *__restrict__ x, FreshParams P,
+                                                         const int32_t *__restrict__ list,
+                                                         const int32_t *__restrict__ count, double *__restrict__ fresh,
+                                                         uint8_t *__restrict__ exact) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t n = *count;
+    for (int64_t q = (int64_t)blockIdx.x * 4 + w; q < n; q += (int64_t)gridDim.x * 4) {
+        const int64_t j = list[q];
+        const int64_t i = P.frame0 + j;
+        const int64_t len = i < P.W ? i : P.W;
+        const int64_t base = P.n_tail + j - len;
+        const double m = wave_np_sum(ArrRef{x}, base, len) / (double)len;
+        const double v = wave_np_sum(SqDevRef{x, m}, base, len);
+        if (lane == 0) {
+            fresh[j] = m + P.k * sqrt(v / (double)len);
+            exact[j] = 1;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ scan
 struct ScanParams {
     int64_t n_local, frame0, seg_len, nseg, cap, F0, Fa;
@@ -517,7 +584,9 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
                                                   SState *__restrict__ out_state, const int32_t *__restrict__ active,
                                                   msd_det *__restrict__ runs, int32_t *__restrict__ nruns,
                                                   double *__restrict__ seg_margin, double *__restrict__ thr_used,
-                                                  int32_t *__restrict__ overflow, int32_t *__restrict__ need) {
+                                                  int32_t *__restrict__ overflow, int32_t *__restrict__ need,
+                                                  const double *__restrict__ eps, const uint8_t *__restrict__ exact,
+                                                  int32_t *__restrict__ list, int32_t *__restrict__ list_count) {
     const int64_t s = blockIdx.x;
     if (!active[s]) return;
     const int lane = threadIdx.x;
@@ -588,6 +657,21 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
             }
         }
         if (need && (U & __ballot(valid && !init)) && lane == 0) need[k / FR_FRAMES] = 1;
+        if (list) {  // decisions-only marking: near ties and triggers on predicted thresholds
+            const bool unf = valid && !init && ((U >> lane) & 1ull);
+            bool cand = false;
+            if (unf && !exact[j]) {
+                const bool near = !(fabs(dv - fr) > eps[j]);  // NaN: near
+                cand = near || ((D >> lane) & 1ull);
+            }
+            const uint64_t mk = __ballot(cand);
+            if (mk) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(list_count, __builtin_popcountll(mk));
+                base = __shfl(base, 0);
+                if (cand) list[base + __builtin_popcountll(mk & ((1ull << lane) - 1ull))] = (int32_t)j;
+            }
+        }
         if (valid) {
             const double mg = fabs(dv - t_fin);
             if (mg < min_margin) min_margin = mg;
@@ -836,6 +920,9 @@ int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total
     if ((e = hipMalloc(&p->d_done, sizeof(int32_t) * (p->ntiles + 1))) != hipSuccess)
         return cleanup(e, "hipMalloc done");
     if ((e = hipMalloc(&p->d_pre, sizeof(double2) * (p->nblk + 1))) != hipSuccess) return cleanup(e, "hipMalloc pre");
+    if ((e = hipMalloc(&p->d_eps, sizeof(double) * nl1)) != hipSuccess) return cleanup(e, "hipMalloc eps");
+    if ((e = hipMalloc(&p->d_exact, nl1)) != hipSuccess) return cleanup(e, "hipMalloc exact");
+    if ((e = hipMalloc(&p->d_list, sizeof(int32_t) * nl1)) != hipSuccess) return cleanup(e, "hipMalloc list");
     if (W > 0) {
         std::vector<int4> prog;
         build_program(W, prog);
@@ -853,7 +940,8 @@ void msd_stream_plan_destroy(msd_stream_plan *p) {
     DeviceGuard g(p->ctx->device);
     hipStreamSynchronize(p->ctx->stream);
     void *bufs[] = {p->d_x, p->d_fresh, p->d_thr, p->d_state, p->d_active, p->d_runs, p->d_out, p->d_nruns,
-                    p->d_margin, p->d_count, p->d_pos, p->d_chunks, p->d_prog, p->d_need, p->d_done, p->d_pre};
+                    p->d_margin, p->d_count, p->d_pos, p->d_chunks, p->d_prog, p->d_need, p->d_done, p->d_pre,
+                    p->d_eps, p->d_exact, p->d_list};
     for (void *b : bufs)
         if (b) hipFree(b);
     delete p;
@@ -909,6 +997,15 @@ static void fresh_params(msd_stream_plan *p, FreshParams &P) {
     P.F0 = p->cfg.fixed_init_blocks;
     P.k = p->cfg.k_std;
     P.nleaf = p->nleaf;
+    P.pre_per = (P.x_len / PB + 1 + 1023) / 1024;
+    const char *es = getenv("MSD_STREAM_EPS_SCALE");
+    P.eps_scale = es && atof(es) >= 1.0 ? atof(es) : 1.0;  // never narrower than the bound
+}
+
+int msd_stream_set_exact_thresholds(msd_stream_plan *p, int32_t on) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_set_exact_thresholds: null plan");
+    p->want_exact = on != 0;
+    return MSD_OK;
 }
 
 int msd_stream_fresh(msd_stream_plan *p) {
@@ -927,10 +1024,14 @@ int msd_stream_fresh(msd_stream_plan *p) {
     MSD_HIP(hipMemsetAsync(p->d_need, 0, sizeof(int32_t) * p->ntiles, st));
     if (all || p->ctx->fresh_all) MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_need), 1, p->ntiles, st));
     MSD_HIP(hipMemsetAsync(p->d_done, 0, sizeof(int32_t) * (p->ntiles + 1), st));
+    // decisions-only: every frame predicted (with its error bound), exact ones listed by the scan
+    p->decide = !p->want_exact && P.W > 0 && !(all || p->ctx->fresh_all);
+    if (p->decide) MSD_HIP(hipMemsetAsync(p->d_exact, 0, p->n_local, st));
     // frames [0, jshort) have windows shorter than W: exact right away
     int64_t jshort = P.W - p->frame0;
     jshort = jshort < 0 ? 0 : (jshort > p->n_local ? p->n_local : jshort);
     if (P.W == 0) jshort = p->n_local;  // empty windows: NaN thresholds
+    if (p->decide) jshort = 0;
     if (jshort > 0)
         hipLaunchKernelGGL(fresh_short_kernel, dim3((unsigned)std::min<int64_t>((jshort + 3) / 4, 4096)), dim3(256), 0,
                            st, p->d_x, P, jshort, p->d_fresh);
@@ -941,7 +1042,7 @@ int msd_stream_fresh(msd_stream_plan *p) {
         hipLaunchKernelGGL(blockscan_kernel, dim3(1), dim3(1024), 0, st, p->d_pre, nb);
         const int64_t m = p->n_local - jshort;
         hipLaunchKernelGGL(approx_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, p->d_x, p->d_pre, P,
-                           jshort, p->d_fresh);
+                           jshort, p->d_fresh, p->decide ? p->d_eps : nullptr);
     }
     MSD_HIP(hipGetLastError());
     return MSD_OK;
@@ -956,6 +1057,18 @@ int msd_stream_refine(msd_stream_plan *p, int32_t *computed) {
     FreshParams P;
     fresh_params(p, P);
     int32_t *count = p->d_done + p->ntiles;
+    if (p->decide) {  // the frames the last marking pass listed
+        {
+            KernelTimer timer(p->ctx, K_FRESH);
+            hipLaunchKernelGGL(fresh_list_kernel, dim3(1024), dim3(256), 0, st, p->d_x, P, p->d_list, count,
+                               p->d_fresh, p->d_exact);
+        }
+        MSD_HIP(hipGetLastError());
+        MSD_HIP(hipMemcpyAsync(computed, count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        MSD_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), st));
+        MSD_HIP(hipStreamSynchronize(st));
+        return MSD_OK;
+    }
     MSD_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), st));
     {
         KernelTimer timer(p->ctx, K_FRESH);
@@ -1020,7 +1133,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
                 KernelTimer timer(p->ctx, K_SSCAN);
                 hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
                                    p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
-                                   p->d_margin, p->d_thr, overflow, nullptr);
+                                   p->d_margin, p->d_thr, overflow, nullptr, nullptr, nullptr, nullptr, nullptr);
             }
             MSD_HIP(hipGetLastError());
             ++nround;
@@ -1040,13 +1153,16 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
     if (p->cfg.adaptive) {
         // the tiles whose fresh thresholds the fixed point reads: one more pass over every segment
         // from its final entry state (same results), marking them -- the speculative rounds above
-        // would also mark tiles that only a wrong entry state reads
+        // would also mark tiles that only a wrong entry state reads.  Decisions-only mode lists the
+        // frames instead (near ties and triggers on predicted thresholds), appended at the counter
+        // after d_done, which msd_stream_refine consumes and clears
         MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_active), 1, p->nseg, st));
         {
             KernelTimer timer(p->ctx, K_SSCAN);
             hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail, p->d_fresh, P,
                                st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns, p->d_margin, p->d_thr,
-                               overflow, p->d_need);
+                               overflow, p->decide ? nullptr : p->d_need, p->d_eps, p->d_exact,
+                               p->decide ? p->d_list : nullptr, p->d_done + p->ntiles);
         }
         MSD_HIP(hipGetLastError());
         MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));

@@ -209,6 +209,7 @@ _SIGS = [
       C.POINTER(_P)]),
     ("msd_stream_chunk_sums", C.c_int,
      [_P, C.c_int32, C.c_double, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    ("msd_stream_set_exact_thresholds", C.c_int, [_P, C.c_int32]),
     ("msd_stream_fresh", C.c_int, [_P]),
     ("msd_stream_refine", C.c_int, [_P, C.POINTER(C.c_int32)]),
     ("msd_stream_scan", C.c_int,
@@ -631,7 +632,17 @@ class StreamPlan:
         self._put(self.d_tail, tail)
         self._put(self.d_head, head)
 
+    exact_thresholds = True
+
+    def set_exact_thresholds(self, on: bool):
+        """False: only the detections are numpy-exact (msd_stream_set_exact_thresholds)."""
+        check(self.ctx.lib.msd_stream_set_exact_thresholds(self.h, 1 if on else 0))
+        self.exact_thresholds = bool(on)
+
     def thresholds(self) -> np.ndarray:
+        if not self.exact_thresholds:
+            raise RuntimeError("StreamPlan.thresholds: the plan computes exact decisions only "
+                               "(set_exact_thresholds(False))")
         return self._get(self.d_thr, self.n_local)
 
     def chunk_sums(self, mean: float | None = None) -> tuple[int, np.ndarray]:

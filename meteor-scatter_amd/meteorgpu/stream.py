@@ -21,6 +21,10 @@ exchanges, all small, done here on the host over a communicator's allgather:
 The adaptive thresholds are only read where the detector is not frozen, so the first scan runs
 on cheap predicted thresholds, marks what it read, the device computes those numpy-exactly
 (``refine``), and the scan repeats until a scan read nothing that was not exact (normally 2).
+Without the thresholds output (``run(thresholds=False)``) only decisions need exact values: the
+predictor carries a rounding-error bound, and only frames whose delta lies within the bound of
+their predicted threshold, or that trigger a detection (whose threshold is then held), are made
+exact -- a few thousand frames a day instead of every unfrozen frame.
 
 The device work per rank is ``_lib.StreamPlan`` (libmsdsp, stream.hip); ``ops`` may be any
 object with the same methods (the CPU tests drive this protocol with a numpy stand-in over
@@ -153,6 +157,8 @@ class StreamResult:
                                # None when run(thresholds=False)
     margin: float              # min |delta - threshold| over the stream
     rounds: int                # state-exchange rounds
+    refined: int = 0           # this rank's exact-threshold work units (tiles; frames without the
+                               # thresholds output)
 
 
 class StreamDetector:
@@ -226,11 +232,16 @@ class StreamDetector:
             return StreamResult(np.zeros(0, _lib.DET_DTYPE), float("nan"), np.zeros(0), math.inf, 0)
         self.exchange_halos()
         if self.adaptive:  # state-free, independent of thr0: queued before the chunk-sum round trips
+            # without the thresholds output only the decisions need exact thresholds: predicted
+            # ones with an error bound elsewhere (same detections)
+            ops.set_exact_thresholds(thresholds)
             ops.fresh()
         thr0 = self.global_threshold()
         rounds = self.scan(thr0)
+        refined = 0
         while self.adaptive:  # until the last scan read exact thresholds only, on every rank
             n = ops.refine()
+            refined += n
             if not any(int(f[0]) for f in comm.allgather_fixed(np.array([n], np.int64))):
                 break
             rounds += self.scan(thr0)
@@ -263,7 +274,7 @@ class StreamDetector:
             db_all[g[:m]] = g[m:].view(np.float64)
         dets["db"] = db_all
         thr = None if not thresholds else (ops.thresholds() if self.adaptive else np.array([thr0]))
-        return StreamResult(dets, thr0, thr, margin, rounds)
+        return StreamResult(dets, thr0, thr, margin, rounds, refined)
 
 
 class DeviceStreamOps:
@@ -283,6 +294,9 @@ class DeviceStreamOps:
 
     def chunk_sums(self, mean=None):
         return self.plan.chunk_sums(mean)
+
+    def set_exact_thresholds(self, on):
+        self.plan.set_exact_thresholds(on)
 
     def fresh(self):
         self.plan.fresh()

@@ -53,6 +53,9 @@ class NumpyStreamOps:
             c += 1
         return c0, np.array(out, np.float64)
 
+    def set_exact_thresholds(self, on):
+        pass  # fresh() is exact everywhere
+
     def fresh(self):
         x, x0 = self._x(), self.frame0 - self.n_tail
         for j in range(self.n_local):

@@ -311,8 +311,7 @@ def test_iq_chunked_spectrogram_matches_whole():
     assert np.array_equal(np.asarray(t1), np.asarray(t2), equal_nan=True)
 
 
-@pytest.mark.parametrize("seed", range(8))
-def test_random_sharded_device(seed):
+def _random_case(seed, thresholds=True):
     """seeded random settings, segment lengths and shard cuts through the device plans (one
     context per rank-thread): bit-exact with the one-process oracle"""
     from meteorgpu import _lib, stream
@@ -339,7 +338,7 @@ def test_random_sharded_device(seed):
             plan.set_delta(d[lo:hi])
             try:
                 return stream.StreamDetector(stream.DeviceStreamOps(plan), comm, adaptive, k, W, F0,
-                                             head_frames=16384).run()
+                                             head_frames=16384).run(thresholds)
             finally:
                 plan.close()
         finally:
@@ -350,10 +349,63 @@ def test_random_sharded_device(seed):
     for r in res:
         assert [(int(a), int(b)) for a, b, _ in r.detections] == [(a, b) for a, b, _ in want]
         assert np.array_equal(r.detections["db"], np.array([w[2] for w in want], np.float64))
-    if adaptive:
+    if not thresholds:
+        assert all(r.thresholds is None for r in res)
+    elif adaptive:
         assert np.array_equal(np.concatenate([r.thresholds for r in res]), np.asarray(thr), equal_nan=True)
     else:
         assert res[0].thr0 == thr
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_sharded_device(seed):
+    _random_case(seed)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_sharded_decisions_only(seed):
+    """run(thresholds=False): predicted thresholds with an error bound, exact only at near ties
+    and triggers -- the same detections"""
+    _random_case(seed, thresholds=False)
+
+
+@pytest.mark.parametrize("seed", [1, 5])
+def test_decisions_only_wide_bound(seed, monkeypatch):
+    """the bound widened (MSD_STREAM_EPS_SCALE) until every unfrozen frame is a near tie: the
+    per-frame exact path carries the whole detector"""
+    monkeypatch.setenv("MSD_STREAM_EPS_SCALE", "1e30")
+    _random_case(seed, thresholds=False)
+
+
+def test_decisions_only_exact_ties():
+    """frames whose delta is the numpy threshold itself, or one ulp either side: the prediction
+    cannot decide them, the exact values must"""
+    from meteorgpu import stream
+    k, W, Fa, F0 = 3.0, 3000, 200, 100
+    d = make_delta(30000, 77, rate=0.001)
+    tied = []
+    for n, i in enumerate(range(W + 500, d.size, 700)):
+        win = d[i - W: i]
+        t = np.mean(win) + k * np.std(win)
+        d[i] = [t, np.nextafter(t, np.inf), np.nextafter(t, -np.inf)][n % 3]
+        tied.append((i, t))
+    want, thr = oracle(d, True, k, W, Fa, F0)
+    used = [i for i, t in tied if thr[i] == t]  # the oracle was unfrozen there: a real tie
+    assert len(used) >= 20  # 29 on this stream, a third of them detections (one ulp above)
+    res = stream.detect_stream(_ctx(), d, d.size, 0, adaptive=True, k_std=k, window_blocks=W,
+                               freeze_after_blocks=Fa, fixed_init_blocks=F0, seg_len=1024)
+    _check(res, d, True, k, W, Fa, F0)
+    ctxd = _ctx()
+    from meteorgpu import _lib
+    cfg = _lib.det_cfg(True, k, W, 0, Fa, F0)
+    plan = _lib.StreamPlan(ctxd, cfg, d.size, 0, d.size, seg_len=1024)
+    try:
+        plan.set_delta(d)
+        r = stream.StreamDetector(stream.DeviceStreamOps(plan), stream.LocalComm(), True, k, W, F0).run(False)
+    finally:
+        plan.close()
+    assert [(int(a), int(b)) for a, b, _ in r.detections] == [(a, b) for a, b, _ in want]
+    assert np.array_equal(r.detections["db"], np.array([w[2] for w in want], np.float64))
 
 
 def test_iq_wav_file(tmp_path):
