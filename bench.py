@@ -231,7 +231,7 @@ def main_c5(a, world, rank, local, dist):
     shard = C5_FS * C5_SECONDS
     n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
-                             rank=rank, world=world)
+                             rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")))
     chunk = C5_FS * 60
     pool = []
     for j in range(4):  # seeded 1-minute chunks: noise + meteor pings at +1 kHz, int16 I/Q interleaved

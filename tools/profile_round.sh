@@ -17,4 +17,4 @@ for wl in live c5; do
 done
 bash "$ROOT/tools/pmc_stft.sh" "$TAG" || exit 1
 REGEX=cstft bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline
-REGEX="fresh_kernel|scan_kernel|approx_kernel|iq_band_delta" bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5det" --workload c5 --steps 1 --warmup 0 --no-cpu-baseline
+REGEX="fresh_list_kernel|scan_kernel|approx_kernel|iq_band_delta" bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5det" --workload c5 --steps 1 --warmup 0 --no-cpu-baseline
