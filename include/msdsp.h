@@ -261,7 +261,9 @@ int msd_stream_fresh(msd_stream_plan *plan); /* async; needs the tail halo */
  * read exact values only where they decide) */
 int msd_stream_refine(msd_stream_plan *plan, int32_t *computed);
 /* thr0 = mean + k*std of the whole stream.  reset = 1: every segment restarts from the clean
- * state (first call); 0: only the entry state changed.  Synchronous; *rounds = scan launches. */
+ * state (first call); 2: every segment re-scans from its last fixed-point entry state (after a
+ * refine changed thresholds); 0: only the shard's entry state changed.  Synchronous; *rounds =
+ * scan launches. */
 int msd_stream_scan(msd_stream_plan *plan, double thr0, const msd_stream_state *entry, int32_t reset,
                     msd_stream_state *exit_state, int32_t *rounds);
 /* the shard's runs in order, host out; stop is exclusive; margin = min |delta - thr| */

@@ -585,7 +585,7 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
                                                   msd_det *__restrict__ runs, int32_t *__restrict__ nruns,
                                                   double *__restrict__ seg_margin, double *__restrict__ thr_used,
                                                   int32_t *__restrict__ overflow, int32_t *__restrict__ need,
-                                                  const double *__restrict__ eps, const uint8_t *__restrict__ exact,
+                                                  const double *__restrict__ eps, uint8_t *__restrict__ exact,
                                                   int32_t *__restrict__ list, int32_t *__restrict__ list_count) {
     const int64_t s = blockIdx.x;
     if (!active[s]) return;
@@ -603,21 +603,28 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
 
     // the next step's delta and fresh threshold are loaded one step ahead (the loads do not depend
     // on the state), so the scalar walk of a step overlaps the memory latency of the next
-    auto ld = [&](int64_t k, double &dv, double &fr) {
+    // (and, when listing, the bound and the exact flag)
+    auto ld = [&](int64_t k, double &dv, double &fr, double &ep, uint8_t &ex) {
         const int64_t j = k + lane < b ? k + lane : (k < b ? k : a);
         dv = delta[j];
         fr = fresh[j];
+        if (list) {
+            ep = eps[j];
+            ex = exact[j];
+        }
     };
-    double dv_n, fr_n;
-    ld(a, dv_n, fr_n);
+    double dv_n, fr_n, ep_n = 0.0;
+    uint8_t ex_n = 1;
+    ld(a, dv_n, fr_n, ep_n, ex_n);
     for (int64_t k = a; k < b; k += 64) {
         const int nvalid = (int)(b - k < 64 ? b - k : 64);
         const bool valid = lane < nvalid;
         const int64_t j = valid ? k + lane : k;
         const int64_t gi = P.frame0 + j;  // global frame of this lane
         const int64_t pos = P.frame0 + k;
-        const double dv = dv_n, fr = fr_n;
-        ld(k + 64, dv_n, fr_n);
+        const double dv = dv_n, fr = fr_n, ep = ep_n;
+        const uint8_t ex = ex_n;
+        ld(k + 64, dv_n, fr_n, ep_n, ex_n);
         const bool init = gi < P.F0;
         const double t_unf = init ? thr0 : fr;
         const uint64_t A_unf = __ballot(valid && dv > t_unf);
@@ -658,11 +665,14 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
         }
         if (need && (U & __ballot(valid && !init)) && lane == 0) need[k / FR_FRAMES] = 1;
         if (list) {  // decisions-only marking: near ties and triggers on predicted thresholds
+            // exact[j]: 0 predicted, 2 listed (computed by the next refine), 1 exact; a frame is
+            // listed once, whichever round (speculative or final) reads it first
             const bool unf = valid && !init && ((U >> lane) & 1ull);
             bool cand = false;
-            if (unf && !exact[j]) {
-                const bool near = !(fabs(dv - fr) > eps[j]);  // NaN: near
+            if (unf && !ex) {
+                const bool near = !(fabs(dv - fr) > ep);  // NaN: near
                 cand = near || ((D >> lane) & 1ull);
+                if (cand) exact[j] = 2;
             }
             const uint64_t mk = __ballot(cand);
             if (mk) {
@@ -721,6 +731,22 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
         o.thr = thr_cur;
         o.reserved = 0;
         out_state[s] = o;
+    }
+}
+
+// the states entering the segments before a scan: segment 0 gets the shard's entry state.
+// reset 1: every other segment starts clean (speculative), all active; 2 (thresholds refined):
+// every segment re-scans from its fixed-point entry state; 0 (the shard's entry changed): the
+// others keep their states and only segment 0 is active
+__global__ void scan_entry_kernel(SState *__restrict__ in_state, int32_t *__restrict__ active, int64_t nseg,
+                                  SState entry, double thr0, int32_t reset) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < nseg) {
+        if (s == 0) in_state[0] = entry;
+        else if (reset == 1) in_state[s] = SState{-1, -2, thr0, 0};
+        active[s] = (s == 0 || reset) ? 1 : 0;
+    } else if (s < nseg + 2) {
+        active[s] = 0;  // change counter, overflow flag
     }
 }
 
@@ -1092,22 +1118,13 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
         if (rounds) *rounds = 0;
         return MSD_OK;
     }
-    if (reset || !p->scanned) {
-        std::vector<SState> init(p->nseg);
-        for (auto &s : init) s = SState{-1, -2, thr0, 0};
-        std::memcpy(&init[0], entry, sizeof(SState));
-        MSD_HIP(hipMemcpyAsync(st_in(p), init.data(), sizeof(SState) * p->nseg, hipMemcpyHostToDevice, st));
-        std::vector<int32_t> act(p->nseg + 2, 1);
-        act[p->nseg] = 0;
-        act[p->nseg + 1] = 0;
-        MSD_HIP(hipMemcpyAsync(p->d_active, act.data(), sizeof(int32_t) * act.size(), hipMemcpyHostToDevice, st));
-        MSD_HIP(hipStreamSynchronize(st));
-    } else {
-        MSD_HIP(hipMemcpyAsync(st_in(p), entry, sizeof(SState), hipMemcpyHostToDevice, st));
-        int32_t one = 1;
-        MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));
-        MSD_HIP(hipMemcpyAsync(p->d_active, &one, sizeof(int32_t), hipMemcpyHostToDevice, st));
-        MSD_HIP(hipStreamSynchronize(st));
+    {  // entry states and active flags set on the device (kernel arguments: no host staging, no sync)
+        SState e0;
+        std::memcpy(&e0, entry, sizeof(SState));
+        const int32_t mode = !p->scanned ? 1 : (reset == 1 || reset == 2 ? reset : 0);
+        hipLaunchKernelGGL(scan_entry_kernel, dim3((unsigned)((p->nseg + 2 + 255) / 256)), dim3(256), 0, st, st_in(p),
+                           p->d_active, p->nseg, e0, thr0, mode);
+        MSD_HIP(hipGetLastError());
     }
     p->thr0 = thr0;
     ScanParams P;
@@ -1133,7 +1150,8 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
                 KernelTimer timer(p->ctx, K_SSCAN);
                 hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
                                    p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
-                                   p->d_margin, p->d_thr, overflow, nullptr, nullptr, nullptr, nullptr, nullptr);
+                                   p->d_margin, p->d_thr, overflow, nullptr, p->d_eps, p->d_exact,
+                                   p->decide ? p->d_list : nullptr, p->d_done + p->ntiles);
             }
             MSD_HIP(hipGetLastError());
             ++nround;
@@ -1150,19 +1168,19 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
         if (hc[0] == 0) break;
         if (nround > p->nseg + 2 + R) return fail(MSD_ERR_INVALID, "msd_stream_scan: no fixed point");
     }
-    if (p->cfg.adaptive) {
+    if (p->cfg.adaptive && !p->decide) {
         // the tiles whose fresh thresholds the fixed point reads: one more pass over every segment
         // from its final entry state (same results), marking them -- the speculative rounds above
-        // would also mark tiles that only a wrong entry state reads.  Decisions-only mode lists the
-        // frames instead (near ties and triggers on predicted thresholds), appended at the counter
-        // after d_done, which msd_stream_refine consumes and clears
+        // would also mark tiles that only a wrong entry state reads.  Decisions-only mode lists
+        // frames (near ties and triggers on predicted thresholds) in every round instead, appended at
+        // the counter after d_done, which msd_stream_refine consumes and clears: a speculative
+        // round lists a few frames more, each once, and no extra pass is needed
         MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_active), 1, p->nseg, st));
         {
             KernelTimer timer(p->ctx, K_SSCAN);
             hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail, p->d_fresh, P,
                                st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns, p->d_margin, p->d_thr,
-                               overflow, p->decide ? nullptr : p->d_need, p->d_eps, p->d_exact,
-                               p->decide ? p->d_list : nullptr, p->d_done + p->ntiles);
+                               overflow, p->d_need, nullptr, nullptr, nullptr, nullptr);
         }
         MSD_HIP(hipGetLastError());
         MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));

@@ -661,10 +661,11 @@ class StreamPlan:
         check(self.ctx.lib.msd_stream_refine(self.h, C.byref(n)))
         return n.value
 
-    def scan(self, thr0: float, entry: MsdStreamState, reset: bool) -> tuple[MsdStreamState, int]:
+    def scan(self, thr0: float, entry: MsdStreamState, reset: int) -> tuple[MsdStreamState, int]:
+        """reset 1: clean restart; 2: re-scan every segment (thresholds refined); 0: entry changed"""
         ex = MsdStreamState()
         rounds = C.c_int32(0)
-        check(self.ctx.lib.msd_stream_scan(self.h, float(thr0), C.byref(entry), 1 if reset else 0, C.byref(ex),
+        check(self.ctx.lib.msd_stream_scan(self.h, float(thr0), C.byref(entry), int(reset), C.byref(ex),
                                            C.byref(rounds)))
         return ex, rounds.value
 

@@ -204,11 +204,13 @@ class StreamDetector:
         return mean + self.k * std
 
     # 3. the state at the shard edges
-    def scan(self, thr0: float) -> int:
+    def scan(self, thr0: float, refined: bool = False) -> int:
+        """refined: thresholds changed since the last fixed point -- every segment re-scans from its
+        converged entry state instead of a clean restart"""
         ops, comm, r = self.ops, self.comm, self.comm.rank
         F0 = self.F0 if self.adaptive else ops.n_total
-        entry = clean_state(thr0)
-        exit_, _ = ops.scan(thr0, entry, True)
+        entry = self._entry if refined else clean_state(thr0)
+        exit_, _ = ops.scan(thr0, entry, 2 if refined else 1)
         rounds = 1
         while True:
             # one exchange per round: every rank's exit and entry state and first frame, so each
@@ -218,11 +220,12 @@ class StreamDetector:
             changed = [q > 0 and not same_state(exits[q - 1], _unpack(got[q][3:6]), int(got[q][6]), F0)
                        for q in range(comm.world)]
             if not any(changed):
+                self._entry = entry
                 return rounds
             rounds += 1
             if changed[r]:
                 entry = exits[r - 1]
-                exit_, _ = ops.scan(thr0, entry, False)
+                exit_, _ = ops.scan(thr0, entry, 0)
 
     def run(self, thresholds: bool = True) -> StreamResult:
         ops, comm = self.ops, self.comm
@@ -244,7 +247,7 @@ class StreamDetector:
             refined += n
             if not any(int(f[0]) for f in comm.allgather_fixed(np.array([n], np.int64))):
                 break
-            rounds += self.scan(thr0)
+            rounds += self.scan(thr0, refined=True)
         # runs of every shard, merged in stream order (a run continued across an edge has start -1)
         local, margin = ops.runs()
         got = comm.allgather(np.concatenate([np.array([margin], np.float64).view(np.int64),
