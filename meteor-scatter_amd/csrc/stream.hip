@@ -434,19 +434,27 @@ __global__ __launch_bounds__(FR_THREADS) void fresh_kernel(const double *__restr
 
 // ---- the predictor: mean + k*std of every window from prefix sums of x and x^2 (not numpy's
 // rounding; it only tells the first scan which tiles need exact thresholds)
-constexpr int PB = 64;  // elements per prefix block
+constexpr int PB = 256;  // elements per prefix block
+// one wave per prefix block: each lane sums 4 elements, then an xor-shuffle tree (<= 10 additions
+// per element, within the predictor's error bound)
 __global__ __launch_bounds__(256) void blocksum_kernel(const double *__restrict__ x, int64_t x_len, int64_t nblk,
                                                        double2 *__restrict__ blk) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= nblk) return;
     double s = 0.0, q = 0.0;
-    const int64_t e = (b + 1) * PB < x_len ? (b + 1) * PB : x_len;
-    for (int64_t i = b * PB; i < e; ++i) {
-        const double v = x[i];
+#pragma unroll
+    for (int r = 0; r < PB / 64; ++r) {
+        const int64_t i = b * PB + r * 64 + lane;
+        const double v = i < x_len ? x[i] : 0.0;
         s += v;
         q += v * v;
     }
-    blk[b] = make_double2(s, q);
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        q += __shfl_xor(q, o, 64);
+    }
+    if (lane == 0) blk[b] = make_double2(s, q);
 }
 
 // exclusive prefix over the blocks, in place, one workgroup
@@ -473,18 +481,6 @@ __global__ __launch_bounds__(1024) void blockscan_kernel(double2 *__restrict__ b
     }
 }
 
-__device__ __forceinline__ double2 prefix_at(const double *__restrict__ x, const double2 *__restrict__ pre,
-                                             int64_t e) {  // sums of x[0..e)
-    const int64_t b = e / PB;
-    double2 r = pre[b];
-    for (int64_t i = b * PB; i < e; ++i) {
-        const double v = x[i];
-        r.x += v;
-        r.y += v * v;
-    }
-    return r;
-}
-
 // eps (decisions-only mode): a bound on |predicted - numpy's threshold| from the rounding-error
 // bounds of both (u = 2^-53; an element passes through at most d additions: |error of a sum| <=
 // d u sum|x|, with sum|x| <= sqrt(len sum x^2)), times 4.  Frames whose |delta - predicted| exceeds it
@@ -495,16 +491,67 @@ __device__ __forceinline__ double sd_err(double e, double sig_lo) {  // |sqrt(a)
     return sig_lo > 0.0 ? fmin(r, e / sig_lo) : r;
 }
 
+__device__ __forceinline__ double2 d2add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+
+// exclusive block scan (256 threads, Hillis-Steele in LDS) of (x, x^2), plus base
+__device__ __forceinline__ double2 block_exscan(double2 v, double2 base, double2 *sh) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const double2 w = t >= o ? sh[t - o] : make_double2(0.0, 0.0);
+        __syncthreads();
+        sh[t] = d2add(sh[t], w);
+        __syncthreads();
+    }
+    const double2 r = t > 0 ? d2add(base, sh[t - 1]) : base;
+    __syncthreads();
+    return r;
+}
+
+// prefix sums of (x, x^2) over x[0 .. e): the block prefix plus the <= PB - 1 elements after the
+// block start, summed by the workgroup as a tree (every thread gets it)
+__device__ __forceinline__ double2 block_prefix(const double *__restrict__ x, const double2 *__restrict__ pre,
+                                                int64_t e, double2 *sh) {
+    const int t = threadIdx.x;
+    const int64_t b = e / PB, q = b * PB + t;
+    const double v = q < e ? x[q] : 0.0;
+    sh[t] = make_double2(v, v * v);
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) sh[t] = d2add(sh[t], sh[t + o]);
+        __syncthreads();
+    }
+    const double2 r = d2add(pre[b], sh[0]);
+    __syncthreads();
+    return r;
+}
+
+// a workgroup predicts 256 consecutive frames: the prefix sums at their window ends (and, for
+// full windows, starts) are contiguous, so one block_prefix per range plus a block scan gives them
 __global__ __launch_bounds__(256) void approx_kernel(const double *__restrict__ x, const double2 *__restrict__ pre,
                                                      FreshParams P, int64_t jbeg, double *__restrict__ fresh,
                                                      double *__restrict__ eps) {
-    const int64_t j = jbeg + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    static_assert(PB == 256, "block_prefix: one element per thread of a 256-thread workgroup");
+    __shared__ double2 sh[256];
+    const int t = threadIdx.x;
+    const int64_t j0 = jbeg + (int64_t)blockIdx.x * 256;
+    const int64_t e0 = P.n_tail + j0, l0 = e0 - P.W;  // window end / start of a full window
+    const double2 base_hi = block_prefix(x, pre, e0, sh);
+    const double2 base_lo = l0 > 0 ? block_prefix(x, pre, l0, sh) : make_double2(0.0, 0.0);
+    auto val = [&](int64_t q) {
+        const double v = q >= 0 && q < P.x_len ? x[q] : 0.0;
+        return make_double2(v, v * v);
+    };
+    const double2 hi = block_exscan(val(e0 + t), base_hi, sh);
+    double2 lo = block_exscan(val(l0 + t), base_lo, sh);  // zeros before index 0
+    const int64_t j = j0 + t;
     if (j >= P.n_local) return;
     const int64_t i = P.frame0 + j;
     if (i < P.F0) return;
-    const int64_t e = P.n_tail + j;
+    const int64_t e = e0 + t;
     const int64_t len = i < P.W ? i : P.W;  // windows before frame W are delta[0:i] (x index 0 = frame 0)
-    const double2 hi = prefix_at(x, pre, e), lo = prefix_at(x, pre, e - len);
+    if (len < P.W) lo = make_double2(0.0, 0.0);
     const double fl = (double)len;
     const double m = (hi.x - lo.x) / fl;
     double v = (hi.y - lo.y) / fl - m * m;
@@ -514,8 +561,9 @@ __global__ __launch_bounds__(256) void approx_kernel(const double *__restrict__ 
     fresh[j] = thr;
     if (!eps) return;
     const double u = 0x1p-53, ak = fabs(P.k);
-    // predictor: prefix sums through <= 63 + per + 10 + per + 63 additions (+1 for x*x)
-    const double d2 = 140.0 + 2.0 * (double)P.pre_per;
+    // predictor: prefix sums through <= PB (block sums) + per + 10 + per (block scan) + 8 + 1
+    // (block_prefix) + 8 + 1 (block_exscan) additions, +1 rounding of x*x (2 PB + 20 + 2 per: ample)
+    const double d2 = 2.0 * PB + 20.0 + 2.0 * (double)P.pre_per;
     const double S1 = hi.x - lo.x, S2 = hi.y - lo.y;
     const double eS1 = 1.01 * d2 * u * (sqrt((double)e * hi.y) + sqrt((double)(e - len) * lo.y)) + u * fabs(S1);
     const double eS2 = 1.01 * (d2 + 1.0) * u * (hi.y + lo.y) + u * fabs(S2);
@@ -1063,7 +1111,7 @@ int msd_stream_fresh(msd_stream_plan *p) {
                            st, p->d_x, P, jshort, p->d_fresh);
     if (jshort < p->n_local) {  // the predictor for full windows
         const int64_t nb = P.x_len / PB + 1;
-        hipLaunchKernelGGL(blocksum_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, p->d_x, P.x_len,
+        hipLaunchKernelGGL(blocksum_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, st, p->d_x, P.x_len,
                            nb, p->d_pre);
         hipLaunchKernelGGL(blockscan_kernel, dim3(1), dim3(1024), 0, st, p->d_pre, nb);
         const int64_t m = p->n_local - jshort;
