@@ -661,9 +661,11 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
             ex = exact[j];
         }
     };
-    double dv_n, fr_n, ep_n = 0.0;
-    uint8_t ex_n = 1;
+    // two steps in flight: the loads of step k + 128 are issued while step k is walked
+    double dv_n, fr_n, ep_n = 0.0, dv_m, fr_m, ep_m = 0.0;
+    uint8_t ex_n = 1, ex_m = 1;
     ld(a, dv_n, fr_n, ep_n, ex_n);
+    ld(a + 64, dv_m, fr_m, ep_m, ex_m);
     for (int64_t k = a; k < b; k += 64) {
         const int nvalid = (int)(b - k < 64 ? b - k : 64);
         const bool valid = lane < nvalid;
@@ -672,7 +674,11 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
         const int64_t pos = P.frame0 + k;
         const double dv = dv_n, fr = fr_n, ep = ep_n;
         const uint8_t ex = ex_n;
-        ld(k + 64, dv_n, fr_n, ep_n, ex_n);
+        dv_n = dv_m;
+        fr_n = fr_m;
+        ep_n = ep_m;
+        ex_n = ex_m;
+        ld(k + 128, dv_m, fr_m, ep_m, ex_m);
         const bool init = gi < P.F0;
         const double t_unf = init ? thr0 : fr;
         const uint64_t A_unf = __ballot(valid && dv > t_unf);
@@ -1184,7 +1190,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
     P.F0 = p->cfg.adaptive ? p->cfg.fixed_init_blocks : p->n_total;  // global mode: thr0 everywhere
     P.Fa = p->cfg.adaptive ? p->cfg.freeze_after_blocks : 0;
     P.thr0 = thr0;
-    P.write_thr = 1;
+    P.write_thr = p->decide ? 0 : 1;  // decisions only: the thresholds buffer is not an output
     int32_t *changed = p->d_active + p->nseg;
     int32_t *overflow = p->d_active + p->nseg + 1;
     // rounds are enqueued three at a time (a round with no active segment costs two empty
