@@ -257,6 +257,9 @@ int msd_stream_chunk_sums(msd_stream_plan *plan, int32_t use_mean, double mean, 
  * is not the reference's list.  Call before msd_stream_fresh. */
 int msd_stream_set_exact_thresholds(msd_stream_plan *plan, int32_t on);
 int msd_stream_fresh(msd_stream_plan *plan); /* async; needs the tail halo */
+/* decisions-only mode, after msd_stream_fresh and before any refine: the predicted thresholds
+ * and their error bounds (n_local each, host; either may be NULL) -- for checking the bound */
+int msd_stream_predicted(msd_stream_plan *plan, double *fresh, double *eps);
 /* synchronous; *computed = tiles (decisions only: frames) made exact now (0: the previous scan
  * read exact values only where they decide) */
 int msd_stream_refine(msd_stream_plan *plan, int32_t *computed);

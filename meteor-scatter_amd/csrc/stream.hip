@@ -1088,6 +1088,18 @@ int msd_stream_set_exact_thresholds(msd_stream_plan *p, int32_t on) {
     return MSD_OK;
 }
 
+int msd_stream_predicted(msd_stream_plan *p, double *fresh, double *eps) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_predicted: null plan");
+    if (!p->decide) return fail(MSD_ERR_INVALID, "msd_stream_predicted: plan not in decisions-only mode");
+    if (p->n_local == 0) return MSD_OK;
+    DeviceGuard g(p->ctx->device);
+    hipStream_t st = p->ctx->stream;
+    if (fresh) MSD_HIP(hipMemcpyAsync(fresh, p->d_fresh, sizeof(double) * p->n_local, hipMemcpyDeviceToHost, st));
+    if (eps) MSD_HIP(hipMemcpyAsync(eps, p->d_eps, sizeof(double) * p->n_local, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
+    return MSD_OK;
+}
+
 int msd_stream_fresh(msd_stream_plan *p) {
     if (!p) return fail(MSD_ERR_INVALID, "msd_stream_fresh: null plan");
     if (!p->cfg.adaptive || p->n_local == 0) return MSD_OK;

@@ -211,6 +211,7 @@ _SIGS = [
      [_P, C.c_int32, C.c_double, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("msd_stream_set_exact_thresholds", C.c_int, [_P, C.c_int32]),
     ("msd_stream_fresh", C.c_int, [_P]),
+    ("msd_stream_predicted", C.c_int, [_P, _P, _P]),
     ("msd_stream_refine", C.c_int, [_P, C.POINTER(C.c_int32)]),
     ("msd_stream_scan", C.c_int,
      [_P, C.c_double, C.POINTER(MsdStreamState), C.c_int32, C.POINTER(MsdStreamState), C.POINTER(C.c_int32)]),
@@ -655,6 +656,13 @@ class StreamPlan:
 
     def fresh(self):
         check(self.ctx.lib.msd_stream_fresh(self.h))
+
+    def predicted(self) -> tuple[np.ndarray, np.ndarray]:
+        """decisions-only mode, after fresh(): (predicted thresholds, error bounds)"""
+        f = np.empty(self.n_local, np.float64)
+        e = np.empty(self.n_local, np.float64)
+        check(self.ctx.lib.msd_stream_predicted(self.h, ptr(f), ptr(e)))
+        return f, e
 
     def refine(self) -> int:
         n = C.c_int32(0)

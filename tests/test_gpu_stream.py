@@ -439,3 +439,53 @@ def test_fresh_all_option_agrees():
     assert np.array_equal(a.detections, b.detections)
     assert np.array_equal(a.thresholds, b.thresholds, equal_nan=True)
     _check(a, d, True, 4.0, 2000, 500, 100)
+
+
+def _bound_case(d, W, k, f0, nl):
+    """predicted thresholds and bounds of the shard [f0, f0 + nl) vs numpy's thresholds"""
+    from meteorgpu import _lib
+    n = d.size
+    ctx = _ctx()
+    plan = _lib.StreamPlan(ctx, _lib.det_cfg(True, k, W, 0, 100, 0), n, f0, nl, seg_len=1024, head_frames=8192)
+    try:
+        plan.set_delta(d[f0: f0 + nl])
+        plan.set_halos(d[f0 - plan.n_tail: f0], d[f0 + nl: f0 + nl + plan.n_head])
+        plan.set_exact_thresholds(False)
+        plan.fresh()
+        pred, eps = plan.predicted()
+    finally:
+        plan.close()
+    worst = 0.0
+    for j in range(nl):
+        i = f0 + j
+        if i == 0:
+            assert np.isnan(pred[j]) or np.isnan(eps[j])  # empty window: NaN, decided exactly
+            continue
+        win = d[max(0, i - W): i]
+        t = np.mean(win) + k * np.std(win)
+        err = abs(pred[j] - t)
+        assert err <= eps[j], (i, pred[j], t, eps[j])
+        worst = max(worst, err / eps[j] if eps[j] > 0 else 0.0)
+    return worst
+
+
+@pytest.mark.parametrize("kind", ["bursts", "dc_offset", "dynamic_range", "steps", "large"])
+def test_prediction_error_bound(kind):
+    """the decisions-only bound on |predicted - numpy| holds frame by frame (first shard with
+    short windows, and a later shard over its halo), on streams chosen to stress it: a large DC
+    offset over a tiny spread, values over 16 decades, constant stretches with jumps"""
+    rng = np.random.default_rng({"bursts": 1, "dc_offset": 2, "dynamic_range": 3, "steps": 4, "large": 5}[kind])
+    n, W = 20000, 3000
+    if kind == "bursts":
+        d = make_delta(n, 91)
+    elif kind == "dc_offset":
+        d = 1e4 + 1e-3 * rng.normal(size=n)
+    elif kind == "dynamic_range":
+        d = rng.normal(size=n) * 10.0 ** rng.uniform(-8, 8, n)
+    elif kind == "steps":
+        d = np.repeat(rng.choice([0.0, 1.0, 1e6, -3.5], n // 500), 500).astype(np.float64)
+    else:
+        d = 1e12 + rng.normal(size=n) * 1e3
+    worst = max(_bound_case(d, W, 4.0, 0, 8000), _bound_case(d, W, 2.5, 9000, 6000))
+    print(f"{kind}: max |predicted - numpy| / bound = {worst:.3g}")
+    assert worst <= 1.0  # |error| <= eps (the bound carries a factor 4 of margin)
