@@ -12,9 +12,10 @@
 // nfft only sets the bin spacing).  Segment powers are averaged in scipy's order (sequential
 // over segments, / nseg) and the band sums use numpy's pairwise order.
 //
-// live_detect_kernel: one workgroup per file.  The history thresholds mean + k*std of the
-// previous W over-noise values do not depend on the state, so they are computed in
-// parallel (one thread per block); one thread then runs the state machine.
+// live_over_kernel, live_history_kernel: the over-noise values, then the history thresholds
+// mean + k*std of the previous W of them -- state-free, one thread per block of every file
+// (the whole GPU, not one workgroup per file);
+// live_detect_kernel: one workgroup per file runs the state machine (one wave, ballots).
 #include <cmath>
 
 #include "msd_internal.h"
@@ -249,6 +250,35 @@ __device__ __noinline__ void live_close(LiveScan &sc, const double *ov, const do
     sc.until = t0 + C.after_tracking_wait_sec;
 }
 
+// processor.py:391: block_db_2_ms = block_db_ms - np.mean([n1, n2])
+__global__ __launch_bounds__(WL_THREADS) void live_over_kernel(const double *__restrict__ band_db,
+                                                                const int64_t *__restrict__ nblocks, LiveArgs A,
+                                                                double *__restrict__ over) {
+    const int64_t f = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * WL_THREADS + threadIdx.x;
+    if (i >= A.ld || i >= nblocks[f]) return;
+    const double *sig = band_db + (f * 3 + 0) * A.ld;
+    const double *n1 = band_db + (f * 3 + 1) * A.ld;
+    const double *n2 = band_db + (f * 3 + 2) * A.ld;
+    const double m = (-0.0 + n1[i] + n2[i]) / 2.0;
+    over[f * A.ld + i] = sig[i] - m;
+}
+
+// processor.py:392-402: history = the previous min(W, b) values (W = 0 → all of them)
+__global__ __launch_bounds__(WL_THREADS) void live_history_kernel(const int64_t *__restrict__ nblocks, LiveArgs A,
+                                                                   const double *__restrict__ over,
+                                                                   double *__restrict__ thr) {
+    const int64_t f = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * WL_THREADS + threadIdx.x;
+    if (i >= A.ld || i >= nblocks[f]) return;
+    const int64_t W = A.cfg.avg_win_blocks;
+    const int64_t h0 = W > 0 ? (i - W > 0 ? i - W : 0) : 0;
+    const int64_t hn = i - h0;
+    double mean = NAN, sd = NAN;
+    if (hn > 0) np_mean_std(over + f * A.ld, h0, hn, mean, sd);
+    thr[f * A.ld + i] = mean + A.cfg.k_std * sd;
+}
+
 __global__ __launch_bounds__(WL_THREADS) void live_detect_kernel(const double *__restrict__ band_db,
                                                                   const int64_t *__restrict__ nblocks, LiveArgs A,
                                                                   double *__restrict__ over, double *__restrict__ thr,
@@ -259,28 +289,9 @@ __global__ __launch_bounds__(WL_THREADS) void live_detect_kernel(const double *_
     if (f >= A.nfiles) return;
     const int64_t nb = nblocks[f];
     const int tid = threadIdx.x;
-    const double *sig = band_db + (f * 3 + 0) * A.ld;
-    const double *n1 = band_db + (f * 3 + 1) * A.ld;
-    const double *n2 = band_db + (f * 3 + 2) * A.ld;
-    double *ov = over + f * A.ld;
+    double *ov = over + f * A.ld;  // over-noise values and history thresholds: the two kernels above
     double *th = thr + f * A.ld;
     const msd_live_cfg &C = A.cfg;
-    // processor.py:391: block_db_2_ms = block_db_ms - np.mean([n1, n2])
-    for (int64_t i = tid; i < nb; i += WL_THREADS) {
-        const double m = (-0.0 + n1[i] + n2[i]) / 2.0;
-        ov[i] = sig[i] - m;
-    }
-    __syncthreads();
-    // processor.py:392-402: history = the previous min(W, b) values (W = 0 → all of them)
-    for (int64_t i = tid; i < nb; i += WL_THREADS) {
-        const int64_t W = C.avg_win_blocks;
-        const int64_t h0 = W > 0 ? (i - W > 0 ? i - W : 0) : 0;
-        const int64_t hn = i - h0;
-        double mean = NAN, sd = NAN;
-        if (hn > 0) np_mean_std(ov, h0, hn, mean, sd);
-        th[i] = mean + C.k_std * sd;
-    }
-    __syncthreads();
     // the state machine (processor.py:404-507): wave 0 scans chunks of the over-noise values,
     // fresh thresholds and block times staged in LDS by the whole workgroup; the thresholds
     // used go back the same way.  History statistics at triggers / detections read the staged chunk when the
@@ -421,6 +432,11 @@ int launch_live(msd_ctx *ctx, const double *band_db, const int64_t *nblocks, int
     A.ld = ld;
     A.cap = cap;
     KernelTimer timer(ctx, K_LIVE);
+    if (ld > 0) {  // grid width: the leading dimension bounds every file's block count
+        const dim3 grid((unsigned)((ld + WL_THREADS - 1) / WL_THREADS), (unsigned)nfiles);
+        hipLaunchKernelGGL(live_over_kernel, grid, dim3(WL_THREADS), 0, ctx->stream, band_db, nblocks, A, over);
+        hipLaunchKernelGGL(live_history_kernel, grid, dim3(WL_THREADS), 0, ctx->stream, nblocks, A, over, thr);
+    }
     hipLaunchKernelGGL(live_detect_kernel, dim3((unsigned)nfiles), dim3(WL_THREADS), 0, ctx->stream, band_db, nblocks,
                        A, over, thr, out, counts, status);
     MSD_HIP(hipGetLastError());

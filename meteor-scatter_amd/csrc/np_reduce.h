@@ -154,9 +154,18 @@ struct SqDevRef {
     }
 };
 
-// numpy mean/std of p[base .. base+n)
+// numpy mean/std of p[base .. base+n).  n <= 128 (one pairwise leaf) stays inline: the general
+// np_sum is a large out-of-line function whose call and instruction-cache misses cost more
+// than the sum itself in the event handlers of the live scan (live.hip)
 __device__ __forceinline__ void np_mean_std(const double *p, int64_t base, int64_t n, double &mean, double &std) {
 #pragma clang fp contract(off)
+    if (n <= 128) {
+        const double s = np_sum_small(ArrRef{p}, base, n);
+        mean = s / (double)n;
+        const double v = np_sum_small(SqDevRef{p, mean}, base, n);
+        std = sqrt(v / (double)n);
+        return;
+    }
     const double s = np_sum(ArrRef{p}, base, n);
     mean = s / (double)n;
     const double v = np_sum(SqDevRef{p, mean}, base, n);
