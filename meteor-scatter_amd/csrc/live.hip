@@ -27,7 +27,6 @@ namespace msd {
 namespace {
 
 constexpr int WL_THREADS = 256;
-constexpr int LV_CHUNK = 2048;  // blocks per LDS-staged chunk of the state-machine scan
 
 // np.sum over LDS: numpy's exact order up to 128 elements (one pairwise leaf); longer runs
 // (bands wider than 128 bins, nperseg != 256 above 128) use the same 8-accumulator leaf
@@ -279,86 +278,146 @@ __global__ __launch_bounds__(WL_THREADS) void live_history_kernel(const int64_t 
     thr[f * A.ld + i] = mean + A.cfg.k_std * sd;
 }
 
-__global__ __launch_bounds__(WL_THREADS) void live_detect_kernel(const double *__restrict__ band_db,
-                                                                  const int64_t *__restrict__ nblocks, LiveArgs A,
-                                                                  double *__restrict__ over, double *__restrict__ thr,
-                                                                  msd_meteor *__restrict__ out,
-                                                                  int64_t *__restrict__ counts,
-                                                                  int32_t *__restrict__ status) {
+// the state machine of one file, time-segmented: wave w of the file's workgroup scans blocks
+// [a_w, b_w).  Segment 0 starts from the true initial state (Init); the others start from the
+// memoryless Detection state (no lock), which is where a file spends most of its time.  After
+// each round every segment whose entry differs from its predecessor's exit re-scans from that
+// exit, until no entry changes (normally 2 rounds); the final entries are then exact, and a
+// last pass per segment writes the thresholds used and the meteors at offsets from the
+// segments' meteor counts.  A segment's scan: at position k lane j evaluates block k+j under
+// the current state; the first block whose event condition holds (ballot) is where the state
+// changes, so a 64-block span without events is one step.
+constexpr int LV_SEGS = 16;  // segments (waves) per file
+
+__device__ __forceinline__ bool live_same_entry(const LiveScan &x, const LiveScan &y, double t1_first) {
+    if (x.state != y.state) return false;
+    if (x.state == 2)
+        return __builtin_bit_cast(long long, x.lock) == __builtin_bit_cast(long long, y.lock) &&
+               __builtin_bit_cast(long long, x.t_start) == __builtin_bit_cast(long long, y.t_start) && x.trig == y.trig;
+    if (x.state == 1) {  // a lock that has run out before the first block's end is no lock
+        const bool lx = x.until > t1_first, ly = y.until > t1_first;
+        if (lx != ly) return false;
+        return !lx || (__builtin_bit_cast(long long, x.lock) == __builtin_bit_cast(long long, y.lock) &&
+                       __builtin_bit_cast(long long, x.until) == __builtin_bit_cast(long long, y.until));
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(LV_SEGS * 64) void live_detect_kernel(const double *__restrict__ band_db,
+                                                                   const int64_t *__restrict__ nblocks, LiveArgs A,
+                                                                   double *__restrict__ over, double *__restrict__ thr,
+                                                                   msd_meteor *__restrict__ out,
+                                                                   int64_t *__restrict__ counts,
+                                                                   int32_t *__restrict__ status) {
     const int64_t f = blockIdx.x;
     if (f >= A.nfiles) return;
     const int64_t nb = nblocks[f];
-    const int tid = threadIdx.x;
-    double *ov = over + f * A.ld;  // over-noise values and history thresholds: the two kernels above
-    double *th = thr + f * A.ld;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const double *ov = over + f * A.ld;  // over-noise values and fresh history thresholds: the two
+    double *th = thr + f * A.ld;         // kernels above; th is overwritten with the thresholds used
     const msd_live_cfg &C = A.cfg;
-    // the state machine (processor.py:404-507): wave 0 scans chunks of the over-noise values,
-    // fresh thresholds and block times staged in LDS by the whole workgroup; the thresholds
-    // used go back the same way.  History statistics at triggers / detections read the staged chunk when the
-    // history lies inside it, the global copy otherwise.
-    __shared__ double s_ov[LV_CHUNK], s_th[LV_CHUNK], s_t[LV_CHUNK + 1];
-    LiveScan sc;
-    for (int64_t c0 = 0; c0 < nb; c0 += LV_CHUNK) {
-        const int cn = nb - c0 < LV_CHUNK ? (int)(nb - c0) : LV_CHUNK;
-        for (int k = tid; k < cn; k += WL_THREADS) {
-            s_ov[k] = ov[c0 + k];
-            s_th[k] = th[c0 + k];
+    const int64_t seg = (nb + LV_SEGS - 1) / LV_SEGS;
+    const int64_t a = w * seg < nb ? w * seg : nb;
+    const int64_t b = a + seg < nb ? a + seg : nb;
+    auto tblk = [&](int64_t i) { return (double)(i * (int64_t)C.block_size) / C.fs; };
+    // (LiveScan has default member initialisers, which __shared__ variables may not have)
+    __shared__ __attribute__((aligned(16))) char s_state[2 * LV_SEGS * sizeof(LiveScan)];
+    LiveScan *s_in = reinterpret_cast<LiveScan *>(s_state), *s_out = s_in + LV_SEGS;
+    __shared__ int64_t s_cnt[LV_SEGS];
+    __shared__ int s_active[LV_SEGS], s_changed;
+
+    // one pass over the segment from sc; emit: write the thresholds used and the meteors
+    auto scan = [&](LiveScan &sc, bool emit) {
+        int64_t k = a;
+        while (k < b) {
+            const int64_t kk = k + lane;
+            const bool valid = kk < b;
+            const int64_t kc = valid ? kk : b - 1;
+            const double v = ov[kc], fresh = th[kc], t0 = tblk(kc), t1 = tblk(kc + 1);
+            double t;
+            bool cand;
+            if (sc.state == 0) {
+                t = fresh;
+                cand = t0 >= C.init_wait_sec;
+            } else if (sc.state == 1) {
+                t = sc.until > t1 ? sc.lock : fresh;
+                cand = v > t;
+            } else {
+                t = sc.lock;
+                cand = v < t;
+            }
+            const uint64_t mask = __ballot(valid && cand);
+            const int first = mask ? __builtin_ctzll(mask) : 64;
+            if (emit && valid && lane <= first) th[kk] = t;  // thresholds used (processor.py:395-412)
+            if (!mask) {
+                k += 64;
+                continue;
+            }
+            const int64_t e = k + first;  // event block
+            const double te = __shfl(t, first), t0e = __shfl(t0, first);
+            if (sc.state == 0) {
+                sc.state = 1;
+                sc.lock = -1.0;
+                sc.until = -1.0;
+            } else if (sc.state == 1) {
+                live_trigger(sc, ov, ov, 0, e, te, t0e, C);
+            } else {
+                live_close(sc, ov, ov, 0, e, t0e, C, out + f * A.cap, A.cap, emit && lane == 0);
+            }
+            k = e + 1;
         }
-        // block start times (i*B)/fs, i = c0 .. c0+cn (the last one is the chunk's end)
-        for (int k = tid; k <= cn; k += WL_THREADS) s_t[k] = (double)((c0 + k) * (int64_t)C.block_size) / C.fs;
-        __syncthreads();
-        if (tid < 64) {
-            // wave 0 scans: at position k, lane j evaluates block k+j under the current state;
-            // the first block whose event condition holds (ballot) is where the state changes.
-            // Blocks before it keep the state, so a 64-block span without events is one step;
-            // each event is one more.  All lanes carry identical copies of the scan state and
-            // run the (rare) event handlers redundantly; lane 0 writes the detection.
-            const int lane = tid;
-            int k = 0;
-            while (k < cn) {
-                const int kk = k + lane;
-                const bool valid = kk < cn;
-                const int kc = valid ? kk : cn - 1;
-                const double v = s_ov[kc], fresh = s_th[kc], t0 = s_t[kc], t1 = s_t[kc + 1];
-                double t;
-                bool cand;
-                if (sc.state == 0) {
-                    t = fresh;
-                    cand = t0 >= C.init_wait_sec;
-                } else if (sc.state == 1) {
-                    t = sc.until > t1 ? sc.lock : fresh;
-                    cand = v > t;
-                } else {
-                    t = sc.lock;
-                    cand = v < t;
-                }
-                const uint64_t mask = __ballot(valid && cand);
-                const int first = mask ? __builtin_ctzll(mask) : 64;
-                if (valid && lane <= first) s_th[kk] = t;  // thresholds used (processor.py:395-412)
-                if (!mask) {
-                    k += 64;
-                    continue;
-                }
-                const int e = k + first;  // event block (chunk-relative)
-                const double te = __shfl(t, first), t0e = __shfl(t0, first);
-                if (sc.state == 0) {
-                    sc.state = 1;
-                    sc.lock = -1.0;
-                    sc.until = -1.0;
-                } else if (sc.state == 1) {
-                    live_trigger(sc, ov, s_ov, c0, c0 + e, te, t0e, C);
-                } else {
-                    live_close(sc, ov, s_ov, c0, c0 + e, t0e, C, out + f * A.cap, A.cap, lane == 0);
-                }
-                k = e + 1;
+    };
+
+    if (lane == 0) {
+        LiveScan e0;  // Init at the file start, memoryless Detection elsewhere (speculative)
+        if (w > 0) {
+            e0.state = 1;
+            e0.lock = -1.0;
+            e0.until = -1.0;
+        }
+        s_in[w] = e0;
+        s_active[w] = 1;
+    }
+    __syncthreads();
+    for (;;) {
+        if (s_active[w]) {
+            LiveScan sc = s_in[w];
+            sc.cnt = 0;
+            scan(sc, false);
+            if (lane == 0) {
+                s_out[w] = sc;
+                s_cnt[w] = sc.cnt;
             }
         }
+        if (tid == 0) s_changed = 0;
         __syncthreads();
-        for (int k = tid; k < cn; k += WL_THREADS) th[c0 + k] = s_th[k];
+        if (lane == 0) {  // (an empty segment's exit is its entry: the scan does nothing)
+            int act = 0;
+            if (w > 0) {
+                const LiveScan nw = s_out[w - 1];
+                if (!live_same_entry(nw, s_in[w], tblk(a + 1))) {
+                    s_in[w] = nw;
+                    act = 1;
+                    atomicOr(&s_changed, 1);
+                }
+            }
+            s_active[w] = act;
+        }
         __syncthreads();
+        if (!s_changed) break;
+        __syncthreads();  // everyone has read s_changed before the next round resets it
+    }
+    // final pass: exact entries, meteors at the offsets of the earlier segments' counts
+    int64_t off = 0;
+    for (int j = 0; j < w; ++j) off += s_cnt[j];
+    {
+        LiveScan sc = s_in[w];
+        sc.cnt = off;
+        scan(sc, true);
     }
     if (tid != 0) return;
-    const int64_t cnt = sc.cnt;
+    int64_t cnt = 0;
+    for (int j = 0; j < LV_SEGS; ++j) cnt += s_cnt[j];
     counts[f] = cnt;
     if (status) status[f] = cnt > A.cap ? 3 : 0;
 }
@@ -437,7 +496,7 @@ int launch_live(msd_ctx *ctx, const double *band_db, const int64_t *nblocks, int
         hipLaunchKernelGGL(live_over_kernel, grid, dim3(WL_THREADS), 0, ctx->stream, band_db, nblocks, A, over);
         hipLaunchKernelGGL(live_history_kernel, grid, dim3(WL_THREADS), 0, ctx->stream, nblocks, A, over, thr);
     }
-    hipLaunchKernelGGL(live_detect_kernel, dim3((unsigned)nfiles), dim3(WL_THREADS), 0, ctx->stream, band_db, nblocks,
+    hipLaunchKernelGGL(live_detect_kernel, dim3((unsigned)nfiles), dim3(LV_SEGS * 64), 0, ctx->stream, band_db, nblocks,
                        A, over, thr, out, counts, status);
     MSD_HIP(hipGetLastError());
     return MSD_OK;

@@ -200,3 +200,27 @@ def test_proc_wav_file_exports_detection_figures(tmp_path):
     pngs = sorted(out.glob("x/*/spec_and_psd_*.png"))
     assert len(res.detections) > 0 and len(pngs) == len(res.detections)
     assert all(q.stat().st_size > 10000 for q in pngs)
+
+
+@pytest.mark.parametrize("nb", [17, 100, 1601, 20000])
+@pytest.mark.parametrize("kw", [dict(), dict(after_tracking_wait_sec=30.0), dict(init_detection_wait_sec=0.0),
+                                dict(avg_win_sec=0.4, detection_dur_min_sec=0.2)])
+def test_state_machine_segments(live, nb, kw):
+    """the kernel splits each file into 16 time segments scanned in parallel to a fixed point:
+    bursts and long plateaus on and across the segment edges (tracking and post-tracking locks
+    carried over one or several edges), bit-exact with the oracle"""
+    rng = np.random.default_rng(nb)
+    sig = rng.normal(0, 1, nb)
+    seg = -(-nb // 16)
+    for e in range(seg, nb, seg):  # a burst straddling every edge, some long enough to span segments
+        L_ = int(rng.choice([1, 3, seg // 2 + 1, 2 * seg + 1]))
+        sig[max(0, e - 2): e - 2 + L_] += rng.uniform(8, 30)
+    for s in rng.integers(0, nb, max(1, nb // 50)):
+        sig[s: s + rng.integers(1, 10)] += rng.uniform(5, 30)
+    rows = np.stack([sig, rng.normal(0, 0.5, nb), rng.normal(0, 0.5, nb)])
+    cfg = live.ConfigDetection(**kw)
+    m, thr, over = live.live_detect(rows, 4000, cfg)
+    rm, rthr, rover = L.live_detect_ref(rows, 4000, 800, _ref_cfg(cfg))
+    np.testing.assert_array_equal(thr, rthr)
+    assert [(a.time_start, a.time_stop, a.db_min, a.db_max, a.db_mean, a.db_std) for a in m] == \
+           [(b.time_start, b.time_stop, b.db_min, b.db_max, b.db_mean, b.db_std) for b in rm]
