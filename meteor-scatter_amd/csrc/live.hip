@@ -15,7 +15,8 @@
 // live_over_kernel, live_history_kernel: the over-noise values, then the history thresholds
 // mean + k*std of the previous W of them -- state-free, one thread per block of every file
 // (the whole GPU, not one workgroup per file);
-// live_detect_kernel: one workgroup per file runs the state machine (one wave, ballots).
+// live_detect_kernel: one workgroup per file runs the state machine, 16 time segments in
+// parallel (one wave each, ballots) to a fixed point over their entry states.
 #include <cmath>
 
 #include "msd_internal.h"
