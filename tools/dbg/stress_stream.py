@@ -1,5 +1,6 @@
 """Debug (GPU box): run the randomised sharded-device parity case of tests/test_gpu_stream.py for
-many more seeds (argv[1], default 80) and report failures."""
+many more seeds (argv[1], default 80), with the thresholds output and in decisions-only mode,
+and report failures."""
 import os
 import sys
 
@@ -12,11 +13,12 @@ import test_gpu_stream as T  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 80
 bad = []
 for seed in range(100, 100 + n):
-    try:
-        T.test_random_sharded_device(seed)
-    except pytest.skip.Exception:
-        pass
-    except Exception as e:  # noqa: BLE001
-        bad.append((seed, repr(e)[:200]))
-        print("FAIL", seed, repr(e)[:200], flush=True)
+    for thresholds in (True, False):
+        try:
+            T._random_case(seed, thresholds)
+        except pytest.skip.Exception:
+            pass
+        except Exception as e:  # noqa: BLE001
+            bad.append((seed, thresholds, repr(e)[:200]))
+            print("FAIL", seed, thresholds, repr(e)[:200], flush=True)
 print(f"{n} seeds, {len(bad)} failures", flush=True)
