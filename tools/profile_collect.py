@@ -45,4 +45,19 @@ for sub, name, kernel, match in ((tag, "stft", "stft1024_kernel<short, 0>", {"fi
         b = last_json(f"{src}/kt_c5.log")
         rec.update({"frames": b["config"]["frames_per_gpu"], "nperseg": 4096})
     json.dump(rec, open(f"{dst}/{name}_pmc.json", "w"), indent=1)
+# per-dispatch durations of each workload's roofline kernel from the kernel trace: the stats
+# average includes the cold first (warm-up) dispatch; the timed steps' average is the figure
+# the bench line's live HIP-event timing reports under the profiler
+lines = ["roofline kernel, per-dispatch durations (ms) from rocprofv3 --kernel-trace; the run is "
+         "bench.py --steps 5 --warmup 1, so dispatch 1 is the warm-up"]
+for wl, key in (("", "stft1024_kernel"), ("_live", "welch_bands_kernel"), ("_c5", "cstft4096_kernel")):
+    import csv
+    rows = list(csv.DictReader(open(f"{src}/kt{wl}/kt_kernel_trace.csv")))
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if key in r["Kernel_Name"]]
+    b = last_json(f"{src}/kt{wl}.log")
+    live = b["roofline"].get("kernel_ms")
+    lines.append(f"{key} ({wl[1:] or 'c3'}): " + " ".join(f"{x:.3f}" for x in d) +
+                 f" | all {sum(d) / len(d):.3f} | timed (after warm-up) {sum(d[1:]) / max(1, len(d) - 1):.3f}"
+                 f" | bench live HIP events {live}")
+open(f"{dst}/{tag}_dispatches.txt", "w").write("\n".join(lines) + "\n")
 print("profiles updated for", tag)
