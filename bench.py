@@ -41,7 +41,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10, help="untimed steps (the GPU clock ramps up over the first few)")
     ap.add_argument("--files", type=int, default=1440, help="one-minute files per GPU")
     ap.add_argument("--cpu-files", type=int, default=150, help="files in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
