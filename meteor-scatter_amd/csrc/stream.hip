@@ -72,6 +72,7 @@ struct msd_stream_plan {
     double thr0 = 0;
     bool scanned = false;
     bool want_exact = true;  // msd_stream_set_exact_thresholds
+    int32_t listed = -1;     // decisions only: frames listed by the last msd_stream_scan (host copy)
 };
 
 namespace msd {
@@ -1149,7 +1150,8 @@ int msd_stream_refine(msd_stream_plan *p, int32_t *computed) {
     FreshParams P;
     fresh_params(p, P);
     int32_t *count = p->d_done + p->ntiles;
-    if (p->decide) {  // the frames the last marking pass listed
+    if (p->decide && p->listed == 0) return MSD_OK;  // the last scan listed nothing
+    if (p->decide) {  // the frames the scan rounds listed
         {
             KernelTimer timer(p->ctx, K_FRESH);
             hipLaunchKernelGGL(fresh_list_kernel, dim3(1024), dim3(256), 0, st, p->d_x, P, p->d_list, count,
@@ -1229,6 +1231,8 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
         int32_t hc[2];
         MSD_HIP(hipMemcpyAsync(hc, changed, sizeof(hc), hipMemcpyDeviceToHost, st));
         MSD_HIP(hipMemcpyAsync(&ex, st_out(p) + (p->nseg - 1), sizeof(SState), hipMemcpyDeviceToHost, st));
+        if (p->decide)  // frames listed so far: a refine with none to compute needs no GPU round trip
+            MSD_HIP(hipMemcpyAsync(&p->listed, p->d_done + p->ntiles, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         MSD_HIP(hipStreamSynchronize(st));
         if (hc[1]) return fail(MSD_ERR_CAPACITY, "msd_stream_scan: more runs in a segment than cap_per_seg");
         if (hc[0] == 0) break;
