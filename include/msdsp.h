@@ -273,6 +273,14 @@ int msd_stream_scan(msd_stream_plan *plan, double thr0, const msd_stream_state *
 int msd_stream_runs(msd_stream_plan *plan, msd_det *runs, int64_t cap, int64_t *count, double *margin);
 /* dets[j].db = np.mean(delta[start:stop]) for global [start, stop) inside the halos + shard */
 int msd_stream_db(msd_stream_plan *plan, msd_det *dets, int64_t n);
+/* One process holding the whole stream (frame0 = 0, n_local = n_total): the sequence above in
+ * one call -- fresh, global threshold, scan / refine to the fixed point, runs (the global
+ * mode's end quirk applied), dB means.  out: cap runs, *count of them; *thr0_out = mean +
+ * k*std of the stream; *margin = min |delta - threshold read|; *rounds = scans; *refined =
+ * exact-threshold work units (tiles, or frames with exact_thresholds = 0).  Errors as the
+ * reference: MSD_ERR_INDEX (empty global input), MSD_ERR_ASSERT (zero-duration last run). */
+int msd_stream_detect_local(msd_stream_plan *plan, int32_t exact_thresholds, msd_det *out, int64_t cap,
+                            int64_t *count, double *thr0_out, double *margin, int32_t *rounds, int32_t *refined);
 
 /* ------------------------------------------- a10: legacy spectrogram noise floor
  * prime_detection.py:65-91: band_power = np.sum(Pxx[noise_band]) sums the spectrogram over

@@ -1308,4 +1308,89 @@ int msd_stream_db(msd_stream_plan *p, msd_det *dets, int64_t n) {
     return MSD_OK;
 }
 
+// The whole protocol for one process holding the whole stream (meteorgpu/stream.py
+// StreamDetector.run at world size 1, same results), natively: no halos, the chunk sums added
+// in order on the host, the scan / refine loop, the runs, the global-mode end quirk and the dB
+// means computed on the plan's own run buffer -- two host round trips fewer than the call
+// sequence, and no interpreter between the calls.
+int msd_stream_detect_local(msd_stream_plan *p, int32_t exact_thresholds, msd_det *out, int64_t cap, int64_t *count,
+                            double *thr0_out, double *margin, int32_t *rounds, int32_t *refined) {
+    if (!p || !count || !thr0_out || !margin || !rounds || !refined)
+        return fail(MSD_ERR_INVALID, "msd_stream_detect_local: null");
+    if (p->frame0 != 0 || p->n_local != p->n_total)
+        return fail(MSD_ERR_UNSUPPORTED, "msd_stream_detect_local: the plan must hold the whole stream");
+    *count = 0;
+    *margin = __builtin_inf();
+    *rounds = 0;
+    *refined = 0;
+    const int64_t n = p->n_total;
+    const bool adaptive = p->cfg.adaptive != 0;
+    if (n == 0) {
+        *thr0_out = NAN;
+        if (!adaptive) return fail(MSD_ERR_INDEX, "index 0 is out of bounds for axis 0 with size 0");  // main.py:412
+        return MSD_OK;
+    }
+    int rc;
+    if (adaptive) {
+        if ((rc = msd_stream_set_exact_thresholds(p, exact_thresholds))) return rc;
+        if ((rc = msd_stream_fresh(p))) return rc;
+    }
+    // np.mean / np.std of the whole stream (main.py:464-466, :399-400): s = 0.0; s += chunk sums
+    std::vector<double> sums((size_t)(n / CHUNK + 2));
+    int64_t nc = 0, c0 = 0;
+    if ((rc = msd_stream_chunk_sums(p, 0, 0.0, sums.data(), (int64_t)sums.size(), &nc, &c0))) return rc;
+    double s = 0.0;
+    for (int64_t i = 0; i < nc; ++i) s += sums[(size_t)i];
+    const double mean = s / (double)n;
+    if ((rc = msd_stream_chunk_sums(p, 1, mean, sums.data(), (int64_t)sums.size(), &nc, &c0))) return rc;
+    double s2 = 0.0;
+    for (int64_t i = 0; i < nc; ++i) s2 += sums[(size_t)i];
+    const double thr0 = mean + p->cfg.k_std * std::sqrt(s2 / (double)n);
+    *thr0_out = thr0;
+    // the freeze / run scan to its fixed point, refined until it reads exact thresholds only
+    const msd_stream_state clean{-1, -2, thr0, 0};
+    msd_stream_state ex{};
+    int32_t r = 0;
+    if ((rc = msd_stream_scan(p, thr0, &clean, 1, &ex, &r))) return rc;
+    *rounds = 1;
+    while (adaptive) {
+        int32_t c = 0;
+        if ((rc = msd_stream_refine(p, &c))) return rc;
+        *refined += c;
+        if (c == 0) break;
+        if ((rc = msd_stream_scan(p, thr0, &clean, 2, &ex, &r))) return rc;
+        ++*rounds;
+    }
+    // runs of the shard, compacted on the device
+    DeviceGuard g(p->ctx->device);
+    hipStream_t st = p->ctx->stream;
+    hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(1024), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
+                       p->d_count, p->d_pos);
+    MSD_HIP(hipGetLastError());
+    int64_t nr = 0;
+    std::vector<double> mg((size_t)p->nseg);
+    MSD_HIP(hipMemcpyAsync(&nr, p->d_count, sizeof(nr), hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(mg.data(), p->d_margin, sizeof(double) * p->nseg, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
+    for (double v : mg) *margin = v < *margin ? v : *margin;
+    *count = nr;
+    if (nr > cap) return fail(MSD_ERR_CAPACITY, "msd_stream_detect_local: more runs than capacity");
+    if (nr == 0) return MSD_OK;
+    if (!out) return fail(MSD_ERR_INVALID, "msd_stream_detect_local: null out");
+    MSD_HIP(hipMemcpy(out, p->d_out, sizeof(msd_det) * nr, hipMemcpyDeviceToHost));
+    if (!adaptive && out[nr - 1].stop == n) {  // burst_stops gets len-1 (main.py:414-415)
+        out[nr - 1].stop = n - 1;
+        if (out[nr - 1].stop - out[nr - 1].start <= 0)
+            return fail(MSD_ERR_ASSERT, "Detection duration must be greater than 0");  // main.py:437
+        MSD_HIP(hipMemcpyAsync(p->d_out + (nr - 1), out + (nr - 1), sizeof(msd_det), hipMemcpyHostToDevice, st));
+    }
+    // np.mean dB of every run (main.py:422-423, :501-502) on the run buffer itself
+    hipLaunchKernelGGL(db_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, st, p->d_x, (int64_t)0, p->d_out,
+                       nr);
+    MSD_HIP(hipGetLastError());
+    MSD_HIP(hipMemcpyAsync(out, p->d_out, sizeof(msd_det) * nr, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
+    return MSD_OK;
+}
+
 }  // extern "C"

@@ -210,6 +210,9 @@ _SIGS = [
     ("msd_stream_chunk_sums", C.c_int,
      [_P, C.c_int32, C.c_double, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("msd_stream_set_exact_thresholds", C.c_int, [_P, C.c_int32]),
+    ("msd_stream_detect_local", C.c_int, [_P, C.c_int32, _P, C.c_int64, C.POINTER(C.c_int64),
+                                          C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_int32)]),
     ("msd_stream_fresh", C.c_int, [_P]),
     ("msd_stream_predicted", C.c_int, [_P, _P, _P]),
     ("msd_stream_refine", C.c_int, [_P, C.POINTER(C.c_int32)]),
@@ -684,6 +687,18 @@ class StreamPlan:
         mg = C.c_double(0)
         check(self.ctx.lib.msd_stream_runs(self.h, ptr(out), cap, C.byref(n), C.byref(mg)))
         return out[: n.value].copy(), mg.value
+
+    def detect_local(self, exact_thresholds: bool = True):
+        """msd_stream_detect_local (the plan holds the whole stream): (detections, thr0, margin,
+        rounds, refined)"""
+        cap = max(1, self.nseg * self.cap_per_seg)
+        out = np.zeros(cap, dtype=DET_DTYPE)
+        n, thr0, mg = C.c_int64(0), C.c_double(0), C.c_double(0)
+        rounds, refined = C.c_int32(0), C.c_int32(0)
+        check(self.ctx.lib.msd_stream_detect_local(self.h, 1 if exact_thresholds else 0, ptr(out), cap, C.byref(n),
+                                                   C.byref(thr0), C.byref(mg), C.byref(rounds), C.byref(refined)))
+        self.exact_thresholds = bool(exact_thresholds)
+        return out[: n.value].copy(), thr0.value, mg.value, rounds.value, refined.value
 
     def db(self, dets: np.ndarray) -> np.ndarray:
         d = np.ascontiguousarray(dets, dtype=DET_DTYPE).copy()

@@ -233,6 +233,11 @@ class StreamDetector:
             if not self.adaptive:  # above_thresh[0] on an empty array (main.py:412)
                 raise IndexError("index 0 is out of bounds for axis 0 with size 0")
             return StreamResult(np.zeros(0, _lib.DET_DTYPE), float("nan"), np.zeros(0), math.inf, 0)
+        if isinstance(comm, LocalComm) and hasattr(ops, "detect_local"):  # one native call, same results
+            # (a one-rank RCCL or gloo group keeps the exchange protocol below)
+            dets, thr0, margin, rounds, refined = ops.detect_local(thresholds if self.adaptive else True)
+            thr = None if not thresholds else (ops.thresholds() if self.adaptive else np.array([thr0]))
+            return StreamResult(dets, thr0, thr, margin, rounds, refined)
         self.exchange_halos()
         if self.adaptive:  # state-free, independent of thr0: queued before the chunk-sum round trips
             # without the thresholds output only the decisions need exact thresholds: predicted
@@ -300,6 +305,16 @@ class DeviceStreamOps:
 
     def set_exact_thresholds(self, on):
         self.plan.set_exact_thresholds(on)
+
+    def detect_local(self, exact_thresholds=True):
+        try:
+            return self.plan.detect_local(exact_thresholds)
+        except _lib.MsdError as e:  # the reference's exceptions, as the Python protocol raises them
+            if e.code == _lib.MSD_ERR_INDEX:
+                raise IndexError("index 0 is out of bounds for axis 0 with size 0") from None
+            if e.code == _lib.MSD_ERR_ASSERT:
+                raise AssertionError("Detection duration must be greater than 0") from None
+            raise
 
     def fresh(self):
         self.plan.fresh()

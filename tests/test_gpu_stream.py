@@ -489,3 +489,45 @@ def test_prediction_error_bound(kind):
     worst = max(_bound_case(d, W, 4.0, 0, 8000), _bound_case(d, W, 2.5, 9000, 6000))
     print(f"{kind}: max |predicted - numpy| / bound = {worst:.3g}")
     assert worst <= 1.0  # |error| <= eps (the bound carries a factor 4 of margin)
+
+
+@pytest.mark.parametrize("adaptive,thresholds", [(True, True), (True, False), (False, True)])
+def test_native_local_path_equals_protocol(adaptive, thresholds):
+    """msd_stream_detect_local (one native call, taken with LocalComm) and the Python protocol
+    over a one-rank group give identical results"""
+    from meteorgpu import _lib, stream
+    d = make_delta(30000, 61, rate=0.01)
+    k, W, Fa, F0 = 3.0, 2000, 300, 100
+
+    def one(comm):
+        ctx = _lib.Context(0)
+        try:
+            plan = _lib.StreamPlan(ctx, _lib.det_cfg(adaptive, k, W, 0, Fa, F0), d.size, 0, d.size, seg_len=1024)
+            try:
+                plan.set_delta(d)
+                return stream.StreamDetector(stream.DeviceStreamOps(plan), comm, adaptive, k, W, F0).run(thresholds)
+            finally:
+                plan.close()
+        finally:
+            ctx.close()
+
+    a = one(stream.LocalComm())
+    b = run_threads(1, lambda r, comm: one(comm))[0]
+    assert np.array_equal(a.detections, b.detections) and len(a.detections) > 10
+    assert a.thr0 == b.thr0 and a.margin == b.margin and a.refined == b.refined
+    if thresholds:
+        assert np.array_equal(a.thresholds, b.thresholds, equal_nan=True)
+    _check(a, d, adaptive, k, W, Fa, F0) if thresholds else None
+
+
+def test_native_local_path_errors():
+    """the reference's exceptions through the native path: empty global input, zero-duration
+    last global run"""
+    from meteorgpu import _lib, stream
+    ctx = _ctx()
+    with pytest.raises(IndexError):
+        stream.detect_stream(ctx, np.zeros(0), 0, 0, adaptive=False, k_std=4.0)
+    d = make_delta(5000, 62)
+    d[-2], d[-1] = -50.0, 50.0  # one block above at the end: t_dur == 0 (main.py:437)
+    with pytest.raises(AssertionError):
+        stream.detect_stream(ctx, d, d.size, 0, adaptive=False, k_std=4.0)
