@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--files", type=int, default=1440, help="one-minute files per GPU")
     ap.add_argument("--cpu-files", type=int, default=150, help="files in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--concurrent-stages", action="store_true",
+                    help="C3: run block_delta -> detect on a second stream beside the STFT (A/B; no gain measured)")
     ap.add_argument("--cpu-procs", type=int, default=16, help="processes of the multi-core CPU baseline "
                     "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
@@ -423,7 +425,7 @@ def main():
         lo, hi = 0, a.files
     F = hi - lo
     bp = BatchPipeline(ctx, F, n, FS, nperseg=NPERSEG, noverlap=NOVERLAP, freq_band=BAND, noise_band=NOISE,
-                       with_spectrogram=not a.no_spectrogram)
+                       with_spectrogram=not a.no_spectrogram, concurrent=a.concurrent_stages)
     for i in range(F):
         bp.upload_file(i, pool[(lo + i + (0 if a.shard_day else rank)) % POOL])
     # file i starts at minute i of the day: 2025-06-01 (one day sharded) or 2025-06-(1+r) (a day per rank)
@@ -457,8 +459,9 @@ def main():
     # the (all-reduced) hour histogram holds every detection of every rank
     _, counts, status, _ = bp.detections()
     assert (status == 0).all(), "detector status"
-    ctx.timing(True)
-    ctx.timing_reset()
+    for c in bp.contexts:
+        c.timing(True)
+        c.timing_reset()
     sync_all()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -478,8 +481,8 @@ def main():
     hist = bp.hour_counts()
     assert int(hist.sum()) == total_dets, "hour histogram != detections"
     stft_ms, stft_launches = ctx.timing_get(_lib.K_STFT)
-    blk_ms, blk_launches = ctx.timing_get(_lib.K_BLOCK)
-    det_ms, det_launches = ctx.timing_get(_lib.K_DSCAN)
+    blk_ms, blk_launches = bp.stage_ctx.timing_get(_lib.K_BLOCK)
+    det_ms, det_launches = bp.stage_ctx.timing_get(_lib.K_DSCAN)
 
     samples = (a.files if a.shard_day else world * F) * n
     value = samples * a.steps / elapsed / 1e6

@@ -387,6 +387,10 @@ int msd_memcpy_h2d_async(msd_ctx *ctx, void *dst, const void *src, size_t bytes)
  * so far; 1: uploads enqueued from now on wait for the compute enqueued so far */
 int msd_fence(msd_ctx *ctx, int direction);
 int msd_copy_synchronize(msd_ctx *ctx);
+/* work enqueued on waiter's stream from now on waits for the work enqueued on signaler's
+ * stream so far (two contexts of one device: independent stages of a step run concurrently,
+ * e.g. the STFT beside block_delta -> detect in BatchPipeline; no reference counterpart) */
+int msd_stream_wait(msd_ctx *waiter, msd_ctx *signaler);
 
 /* ------------------------------------------ multi-GPU: per-hour count reduction
  * RCCL (loaded at run time from librccl.so.1), one communicator per (process, GPU). */

@@ -164,6 +164,7 @@ void msd_destroy(msd_ctx *ctx) {
         hipStreamDestroy(ctx->copy_stream);
     }
     if (ctx->fence_ev) hipEventDestroy(ctx->fence_ev);
+    if (ctx->join_ev) hipEventDestroy(ctx->join_ev);
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }

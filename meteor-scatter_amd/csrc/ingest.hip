@@ -196,6 +196,16 @@ int msd_fence(msd_ctx *ctx, int direction) {
     return MSD_OK;
 }
 
+int msd_stream_wait(msd_ctx *waiter, msd_ctx *signaler) {
+    if (!waiter || !signaler || waiter == signaler) return fail(MSD_ERR_INVALID, "msd_stream_wait: bad args");
+    if (waiter->device != signaler->device) return fail(MSD_ERR_INVALID, "msd_stream_wait: contexts on different devices");
+    DeviceGuard g(signaler->device);
+    if (!signaler->join_ev) MSD_HIP(hipEventCreateWithFlags(&signaler->join_ev, hipEventDisableTiming));
+    MSD_HIP(hipEventRecord(signaler->join_ev, signaler->stream));
+    MSD_HIP(hipStreamWaitEvent(waiter->stream, signaler->join_ev, 0));
+    return MSD_OK;
+}
+
 int msd_copy_synchronize(msd_ctx *ctx) {
     if (!ctx) return fail(MSD_ERR_INVALID, "msd_copy_synchronize: null");
     if (!ctx->copy_stream) return MSD_OK;

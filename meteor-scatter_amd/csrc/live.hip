@@ -96,6 +96,55 @@ __device__ __forceinline__ double wave_np_sum(const double *seg, int n, int lane
     return readlane_f64(v, 0);
 }
 
+// Goertzel power of NB band bins per lane (bins j, j + 64, ...) over the staged, windowed
+// segment, added into the wave's psd in segment order.  The arithmetic per bin is the same
+// for any NB (bit-identical results).
+template <int NB>
+__device__ __forceinline__ void goertzel_bins(const double *seg, int L, const double *__restrict__ g_bins, int j,
+                                              int nslots, double scale, double *psd, int s) {
+    double cw[NB], sw[NB], c2[NB], dbl[NB], s1[NB], s2[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int jb = j + 64 * b;
+        const double *bc = g_bins + 4 * (jb < nslots ? jb : 0);
+        cw[b] = bc[0], sw[b] = bc[1], c2[b] = bc[2], dbl[b] = bc[3];
+        s1[b] = 0.0, s2[b] = 0.0;
+    }
+    const double2 *y2 = reinterpret_cast<const double2 *>(seg);
+    int m = 0;
+#pragma unroll 4
+    for (; m + 2 <= L; m += 2) {
+        const double2 y = y2[m >> 1];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            double s0 = __builtin_fma(c2[b], s1[b], y.x - s2[b]);
+            s2[b] = s1[b];
+            s1[b] = s0;
+            s0 = __builtin_fma(c2[b], s1[b], y.y - s2[b]);
+            s2[b] = s1[b];
+            s1[b] = s0;
+        }
+    }
+    if (m < L) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const double s0 = __builtin_fma(c2[b], s1[b], seg[m] - s2[b]);
+            s2[b] = s1[b];
+            s1[b] = s0;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int jb = j + 64 * b;
+        // X e^{i w (L-1)} = s1 - e^{-i w} s2: |X|^2 = re^2 + im^2
+        const double re = s1[b] - cw[b] * s2[b], im = sw[b] * s2[b];
+        double p = re * re + im * im;  // conj(X) * X (real part)
+        p = p * scale;                 // result *= scale
+        p = p * dbl[b];                // result[..., 1:-1] *= 2 (onesided psd)
+        if (jb < nslots) psd[jb] = s == 0 ? p : psd[jb] + p;  // Pxy.mean(axis=-1): segments in order
+    }
+}
+
 // One wave per processing block: per Welch segment, stage + detrend + window the samples in
 // the wave's LDS, then Goertzel over the segment for every band bin (lane = bin, broadcast
 // LDS reads of the samples, two per ds_read_b128), accumulating the segment powers in the
@@ -133,36 +182,11 @@ __global__ __launch_bounds__(WL_THREADS) void welch_bands_kernel(const T *__rest
         wave_sync();
         for (int i = lane; i < L; i += 64) seg[i] = g_win[i] * (seg[i] - mean);  // win * detrended
         wave_sync();
-        for (int j0 = 0; j0 < A.nslots; j0 += 64) {
-            const int j = j0 + lane;
-            const bool act = j < A.nslots;
-            const double *bc = g_bins + 4 * (act ? j : 0);
-            const double cw = bc[0], sw = bc[1], c2 = bc[2], dbl = bc[3];
-            double s1 = 0.0, s2 = 0.0;
-            const double2 *y2 = reinterpret_cast<const double2 *>(seg);
-            int m = 0;
-#pragma unroll 4
-            for (; m + 2 <= L; m += 2) {
-                const double2 y = y2[m >> 1];
-                double s0 = __builtin_fma(c2, s1, y.x - s2);
-                s2 = s1;
-                s1 = s0;
-                s0 = __builtin_fma(c2, s1, y.y - s2);
-                s2 = s1;
-                s1 = s0;
-            }
-            if (m < L) {
-                const double s0 = __builtin_fma(c2, s1, seg[m] - s2);
-                s2 = s1;
-                s1 = s0;
-            }
-            // X e^{i w (L-1)} = s1 - e^{-i w} s2: |X|^2 = re^2 + im^2
-            const double re = s1 - cw * s2, im = sw * s2;
-            double p = re * re + im * im;  // conj(X) * X (real part)
-            p = p * A.scale;               // result *= scale
-            p = p * dbl;                   // result[..., 1:-1] *= 2 (onesided psd)
-            if (act) psd[j] = s == 0 ? p : psd[j] + p;  // Pxy.mean(axis=-1): segments in order
-        }
+        // two bins per lane while 128 remain (one broadcast LDS read feeds both recurrences:
+        // half the LDS reads per flop, two independent FMA chains), then one per lane
+        int j0 = 0;
+        for (; j0 + 128 <= A.nslots; j0 += 128) goertzel_bins<2>(seg, L, g_bins, j0 + lane, A.nslots, A.scale, psd, s);
+        for (; j0 < A.nslots; j0 += 64) goertzel_bins<1>(seg, L, g_bins, j0 + lane, A.nslots, A.scale, psd, s);
         wave_sync();
     }
     for (int j = lane; j < A.nslots; j += 64) {

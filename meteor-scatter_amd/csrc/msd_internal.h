@@ -37,6 +37,7 @@ struct msd_ctx {
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;  // host → HBM uploads (msd_memcpy_h2d_async), created on first use
     hipEvent_t fence_ev = nullptr;      // cross-stream ordering (msd_fence)
+    hipEvent_t join_ev = nullptr;       // cross-context ordering (msd_stream_wait), this ctx signalling
     bool timing = false;
     bool force_generic = false;  // MSD_OPT_GENERIC_STFT
     bool fresh_all = false;      // MSD_OPT_FRESH_ALL

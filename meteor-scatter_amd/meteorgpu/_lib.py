@@ -193,6 +193,7 @@ _SIGS = [
     ("msd_memcpy_h2d_async", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("msd_fence", C.c_int, [_P, C.c_int]),
     ("msd_copy_synchronize", C.c_int, [_P]),
+    ("msd_stream_wait", C.c_int, [_P, _P]),
     ("msd_comm_get_unique_id", C.c_int, [_P]),
     ("msd_comm_init", C.c_int, [_P, C.c_int, _P, C.c_int, C.POINTER(_P)]),
     ("msd_comm_destroy", None, [_P]),
@@ -292,6 +293,10 @@ class Context:
 
     def synchronize(self):
         check(self.lib.msd_synchronize(self.h))
+
+    def wait_for(self, other: "Context"):
+        """Work enqueued on this context from now on waits for ``other``'s work so far."""
+        check(self.lib.msd_stream_wait(self.h, other.h))
 
     # ---- device memory
     def alloc(self, nbytes: int) -> "DeviceBuffer":

@@ -30,8 +30,14 @@ class BatchPipeline:
                  threshold_estimation_window_sec: float = 120, threshold_freeze_before_detection_sec: float = 3,
                  threshold_freeze_after_detection_sec: float = 20, threshold_fixed_init_duration_sec: float = 10,
                  with_spectrogram: bool = True, nbuckets: int = 24, bucket_us: int = 3600 * 10 ** 6,
-                 dtype=np.int16):
+                 dtype=np.int16, concurrent: bool = False):
         self.ctx = ctx
+        # concurrent: block_delta -> detect run on a second context's stream beside the STFT
+        # (they only share the read-only samples); run() forks from and joins back into ctx.
+        # Off by default: on MI355X the step is no faster (7.19-7.21 ms either way)
+        # -- the persistent VALU-bound STFT leaves no idle issue slots for them to fill
+        self.side = _lib.Context(ctx.device) if concurrent and with_spectrogram else None
+        self.stage_ctx = self.side if self.side is not None else ctx
         self.nfiles, self.n, self.fs = int(nfiles), int(n_per_file), float(fs)
         self.dtype = np.dtype(dtype)
         self.with_spectrogram = with_spectrogram
@@ -51,7 +57,7 @@ class BatchPipeline:
         self.block_size = int(fs * block_duration_sec)
         self.block_sec = block_duration_sec
         L = min(self.block_size, nfft)
-        self.blocks = _lib.BlockPlan(ctx, self.block_size, nfft, hanning_sym(self.block_size)[:L],
+        self.blocks = _lib.BlockPlan(self.stage_ctx, self.block_size, nfft, hanning_sym(self.block_size)[:L],
                                      band_bins(nfft, fs, freq_band), band_bins(nfft, fs, noise_band))
         self.nb = self.n // self.block_size
         self.ld_b = max(1, self.nb)
@@ -102,9 +108,11 @@ class BatchPipeline:
         """Enqueue one pass over the batch (no host synchronisation).  ``x`` / ``start_us``:
         alternative device buffers of the same layout as ``d_x`` / ``d_start_us`` (double-buffered
         ingest); ``clear_hist=False`` accumulates the hour histogram across batches."""
-        lib, h = self.ctx.lib, self.ctx.h
+        lib, h = self.ctx.lib, self.stage_ctx.h
         x = self.d_x if x is None else x
         self.hist.file_start_us = (self.d_start_us if start_us is None else start_us).ptr
+        if self.side is not None:
+            self.side.wait_for(self.ctx)  # fork: uploads and earlier readers of the outputs first
         if clear_hist:
             _lib.check(lib.msd_memset_dev(h, self.d_hist.ptr, 0, self.d_hist.nbytes))
         if self.with_spectrogram:
@@ -114,6 +122,12 @@ class BatchPipeline:
         _lib.check(lib.msd_detect_dev(h, self.d_delta.ptr, self.d_nb.ptr, self.nfiles, self.ld_b, self.cfg,
                                       self.d_dets.ptr, self.cap, self.d_counts.ptr, self.d_thr.ptr,
                                       self.d_margin.ptr, self.d_status.ptr, self.hist))
+        if self.side is not None:
+            self.ctx.wait_for(self.side)  # join: everything after run() on ctx sees the detections
+
+    @property
+    def contexts(self):
+        return [self.ctx] if self.side is None else [self.ctx, self.side]
 
     # ------------------------------------------------------------------ outputs
     def spectrogram(self, i: int) -> np.ndarray:

@@ -280,6 +280,37 @@ def test_batch_pipeline_matches_single_file_path():
         assert hist[h] == ref_hours.get(h, 0)
 
 
+def test_batch_concurrent_stages_identical():
+    """BatchPipeline(concurrent=True): block_delta -> detect on a second context's stream beside
+    the STFT (msd_stream_wait fork/join) gives the serial pipeline's outputs bit for bit, over
+    back-to-back steps without host synchronisation (the next step's histogram memset must wait
+    for the previous step's readers)."""
+    ctx = dsp.context(0)
+    fs, n, F = 48000, 48000 * 60, 8
+    xs = [synth.synth_real(seed=3100 + i, fs=fs, duration_s=60, f0=1000.0, rate_per_min=6)[0] for i in range(F)]
+    out = []
+    for conc in (False, True):
+        bp = BatchPipeline(ctx, F, n, fs, noise_band=(2950.0, 3050.0), concurrent=conc)
+        assert (bp.side is not None) == conc
+        for i, x in enumerate(xs):
+            bp.upload_file(i, x)
+        bp.set_start_times(np.arange(F, dtype=np.int64) * 60 * 10 ** 6, 0)
+        for _ in range(3):
+            bp.run()
+        ctx.synchronize()
+        dets, counts, status, margin = bp.detections()
+        assert (status == 0).all()
+        out.append((bp.delta(), bp.thresholds(), counts, [d.tobytes() for d in dets], bp.hour_counts(),
+                    [bp.spectrogram(i) for i in (0, F - 1)]))
+    a, b = out
+    for u, v in zip(a[:3] + (a[4],), b[:3] + (b[4],)):
+        np.testing.assert_array_equal(u, v)
+    assert a[3] == b[3]
+    for u, v in zip(a[5], b[5]):
+        np.testing.assert_array_equal(u, v)
+    assert a[4].sum() == a[2].sum()
+
+
 def test_full_day_batch_properties():
     """C3 at full size (1440 x 60 s @ 48 kHz, 8.3 GB in, 16.6 GB spectrogram) through
     size-independent properties: replicated files give identical outputs at every offset
