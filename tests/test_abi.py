@@ -50,3 +50,5 @@ def test_invalid_args_fail_without_gpu():
     lib = _lib.load()
     assert lib.msd_create(0, None) == _lib.MSD_ERR_INVALID
     assert b"null" in lib.msd_last_error()
+    assert lib.msd_stream_wait(None, None) == _lib.MSD_ERR_INVALID
+    assert b"msd_stream_wait" in lib.msd_last_error()
