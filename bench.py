@@ -14,6 +14,11 @@ STFT, timed live with HIP events on the stream it runs on) and the CPU baseline
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+With --gpus N > 1 and no launcher environment (WORLD_SIZE unset) bench.py starts the N ranks
+itself (meteorgpu.launch.spawn) before anything touches a GPU.  No PyTorch anywhere: the ranks
+share the RCCL unique id through a rendezvous file, and the barrier, the rank count and the
+max-over-ranks time go through libmsdsp's RCCL wrappers (meteorgpu.launch.Group).
 """
 import argparse
 import datetime
@@ -33,16 +38,24 @@ SECONDS = 60
 BAND = (950.0, 1050.0)
 NOISE = (2950.0, 3050.0)  # far from the ping: the 48 kHz crop leaks into near bands
 NPERSEG, NOVERLAP = 1024, 512
+C5_FS, C5_N, C5_HOP, C5_SECONDS = 192000, 4096, 1024, 3 * 3600
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 POOL = 16              # distinct synthetic recordings, replicated over the batch
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU); spawned here unless "
+                    "an external launcher set WORLD_SIZE, which must then equal --gpus")
+    ap.add_argument("--spawn", action="store_true", help="start the ranks through the launcher even at "
+                    "--gpus 1 (the N>1 code path: rendezvous file + RCCL communicator on one GPU)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher self-test without a GPU: the ranks "
+                    "rendezvous a random id and rank 0 prints what every rank saw")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps (the GPU clock ramps up over the first few)")
     ap.add_argument("--files", type=int, default=1440, help="one-minute files per GPU")
+    ap.add_argument("--c5-seconds", type=float, default=C5_SECONDS, help="c5: seconds of the stream per GPU "
+                    "(default 3 h: 24 h over 8 GPUs)")
     ap.add_argument("--cpu-files", type=int, default=150, help="files in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--concurrent-stages", action="store_true",
@@ -143,11 +156,12 @@ def cpu_baseline_live(pool, seconds):
     return len(x) / dt / 1e6, dt
 
 
-def main_live(a, world, rank, local, dist):
+def main_live(a, world, rank, local, job_of):
     """Phase-2 live detector over a day of 4 kHz audio per GPU: 24 x 1 h int16 files."""
     from meteorgpu import _lib, synth
     from meteorgpu import live as LV
     ctx = _lib.Context(local)
+    job = job_of(ctx)
     cfg = LV.ConfigDetection(proc_block_sec=0.2, n_fft=4096, signal_freq=1000,
                              detection_db_over_noise_mean_min=1, detection_dur_min_sec=0.5)
     n = LIVE_FS * LIVE_FILE_S
@@ -160,10 +174,8 @@ def main_live(a, world, rank, local, dist):
 
     def sync_all():
         ctx.synchronize()
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        if job is not None:
+            job.barrier()
 
     for _ in range(a.warmup):
         lb.run()
@@ -177,11 +189,8 @@ def main_live(a, world, rank, local, dist):
         lb.run()
     sync_all()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if job is not None:
+        elapsed = job.max_f64(elapsed)
     w_ms, w_n = ctx.timing_get(_lib.K_WELCH)
     l_ms, l_n = ctx.timing_get(_lib.K_LIVE)
     wc = lb.plan.cfg
@@ -207,30 +216,32 @@ def main_live(a, world, rank, local, dist):
                      "algorithmic_flops_per_launch": flops},
         "kernel_ms_per_step": {"welch": round(avg_s * 1e3, 4), "live_detect": round(l_ms / max(l_n, 1), 4)},
     }
-    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
         secs = 1800
         v, dt = cpu_baseline_live(pool, secs)
         out["cpu_baseline"] = {"value": round(v, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
                                "sample": f"{secs} s of one 4 kHz file ({dt:.1f} s): scipy welch per block + "
                                          f"band sums + state machine (oracle/live_oracle.py), 1 thread"}
+    out["ranks_seen"] = job.ranks_seen() if job is not None else 1
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if job is not None:
+        job.close()
 
 
-C5_FS, C5_N, C5_HOP, C5_SECONDS = 192000, 4096, 1024, 3 * 3600
 C5_BAND, C5_NOISE = (950.0, 1050.0), (-3050.0, -2950.0)  # Hz from the SDR centre (two-sided spectrum)
 
 
-def main_c5(a, world, rank, local, dist):
+def main_c5(a, world, rank, local, job_of):
     """BASELINE config C5: a 24 h 192 kHz I/Q stream time-sharded over the GPUs (3 h of it per
     GPU; weak scaling: the stream is 3 h x N long).  A step = the whole path on every rank:
     two-sided 4096-point power spectrogram at 75 % overlap (frame-major float32, kept in HBM),
     the per-frame band / noise dB delta, and the reference's adaptive detector over the WHOLE
     stream (meteorgpu.stream: halo, chunk-sum and shard-edge state exchanges over RCCL)."""
     from meteorgpu import _lib, iq, stream, synth
-    from meteorgpu.batch import Communicator
     ctx = _lib.Context(local)
-    shard = C5_FS * C5_SECONDS
+    job = job_of(ctx)
+    shard = int(C5_FS * a.c5_seconds)
     n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
                              rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")))
@@ -249,13 +260,7 @@ def main_c5(a, world, rank, local, dist):
         det.upload(pool[k % len(pool)][: 2 * m], sample_offset=pos)
         pos += m
         k += 1
-    comm = stream.LocalComm()
-    rccl = None
-    if dist is not None:
-        obj = [Communicator.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        rccl = Communicator(ctx, world, obj[0], rank)
-        comm = stream.RcclComm(rccl, rank, world)
+    comm = job.comm if job is not None else stream.LocalComm()
 
     def step():
         det.spectrogram_and_delta()
@@ -263,10 +268,8 @@ def main_c5(a, world, rank, local, dist):
 
     def sync_all():
         ctx.synchronize()
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        if job is not None:
+            job.barrier()
 
     res = None
     for _ in range(a.warmup):
@@ -280,11 +283,8 @@ def main_c5(a, world, rank, local, dist):
         res = step()
     sync_all()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if job is not None:
+        elapsed = job.max_f64(elapsed)
     kms = {}
     for name, kid in (("cstft", _lib.K_CSTFT), ("band_delta", _lib.K_IQDELTA), ("fresh_thresholds", _lib.K_FRESH),
                       ("scan", _lib.K_SSCAN)):
@@ -294,6 +294,7 @@ def main_c5(a, world, rank, local, dist):
     avg_s = k_ms / max(k_n, 1) / 1e3
     T = det.f1 - det.f0
     samples = shard  # per rank: its 3 h (the 3072-sample frame tail is read, not counted)
+    hrs = f"{a.c5_seconds / 3600:g} h"
     alg_bytes = (det.s1 - det.s0) * 4 + T * C5_N * 4
     out = {
         "metric": "Msamples/s processed (192 kHz I/Q: 4096-pt two-sided spectrogram, 75% overlap, band delta, "
@@ -302,8 +303,8 @@ def main_c5(a, world, rank, local, dist):
         "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32 spectrogram / f64 detector",
-        "data": "synthetic: 4 seeded 1-minute 192 kHz int16 I/Q chunks (noise + pings) tiled into 3 h per GPU",
-        "config": {"workload": "C5: 192 kHz I/Q stream time-sharded 3 h per GPU (3 h x N long), spectrogram "
+        "data": f"synthetic: 4 seeded 1-minute 192 kHz int16 I/Q chunks (noise + pings) tiled into {hrs} per GPU",
+        "config": {"workload": f"C5: 192 kHz I/Q stream time-sharded {hrs} per GPU ({hrs} x N long), spectrogram "
                                "4096/1024 float32 [T][4096] frame-major + per-frame band dB (950..1050 Hz vs "
                                "-3050..-2950 Hz) + adaptive detector over the whole stream (k 4, window 120 s = "
                                f"{det.W} frames, freeze 20 s, fixed init 10 s)",
@@ -319,7 +320,7 @@ def main_c5(a, world, rank, local, dist):
                      "algorithmic_bytes_per_launch": alg_bytes},
         "kernel_ms_per_step": kms,
     }
-    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
         from oracle import iq_oracle as Q
         m = C5_FS * 60  # one minute of the stream
         z = pool[0]
@@ -330,14 +331,15 @@ def main_c5(a, world, rank, local, dist):
                                "sample": f"60 s of the 192 kHz I/Q stream ({dt:.1f} s): scipy.signal.spectrogram "
                                          f"(complex input, 4096/3072) + per-frame band sums + adaptive detector "
                                          f"(oracle/iq_oracle.py), 1 thread"}
+    out["ranks_seen"] = job.ranks_seen() if job is not None else 1
     det.close()
-    if rccl is not None:
-        rccl.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if job is not None:
+        job.close()
 
 
-def main_files(a, world, rank, local, dist):
+def main_files(a, world, rank, local, job_of):
     """End to end from disk: `--files` one-minute 48 kHz WAVs written to a temp dir, then
     meteorgpu.ingest.WavDay (native reader threads → pinned memory → copy stream → the C3
     pipeline, double-buffered batches of 120).  The page cache is warm (files just written):
@@ -346,6 +348,7 @@ def main_files(a, world, rank, local, dist):
     import tempfile
     from meteorgpu import _lib, ingest, synth, wav
     ctx = _lib.Context(local)
+    job = job_of(ctx)
     F = min(a.files, 480)
     pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
     d = tempfile.mkdtemp(prefix=f"msd_wav_{rank}_", dir=os.environ.get("TMPDIR", "/tmp"))
@@ -366,6 +369,8 @@ def main_files(a, world, rank, local, dist):
             dets, hist, info = wd.run()
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
+        if job is not None:
+            best = job.max_f64(best)
         n = FS * SECONDS
         out = {
             "metric": "Msamples/s end to end from WAV files (48 kHz, C3 pipeline)",
@@ -378,38 +383,61 @@ def main_files(a, world, rank, local, dist):
                        "files_per_gpu": F, "read_s": round(info["read_s"], 3),
                        "detections": int(sum(len(x) for x in dets)), "hour_total": int(hist.sum())},
         }
+        out["ranks_seen"] = job.ranks_seen() if job is not None else 1
         if rank == 0:
             print(json.dumps(out), flush=True)
     finally:
         shutil.rmtree(d, ignore_errors=True)
+        if job is not None:
+            job.close()
+
+
+def dry_run(rank, world):
+    """Launcher self-test without a GPU: the ranks share a random 128-byte id through the
+    rendezvous file, each publishes the digest it saw, and rank 0 checks they all agree."""
+    import hashlib
+    from meteorgpu import launch
+    uid = launch.share_bytes(rank, lambda: os.urandom(128))
+    launch.share_bytes(0, lambda: hashlib.sha1(uid).digest(), tag=f"seen{rank}")
+    if rank != 0:
+        return
+    seen = [launch.share_bytes(1, lambda: b"", tag=f"seen{r}") for r in range(world)]
+    for r in range(world):
+        launch.release(0, tag=f"seen{r}")
+    launch.release(0)
+    ok = all(d == hashlib.sha1(uid).digest() for d in seen)
+    print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": len(seen), "id_agreed": ok}), flush=True)
+    if not ok:
+        sys.exit(1)
 
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # MSD_BENCH_FORCE_DIST=1 takes the N>1 path (nccl process group + RCCL communicator) at
-    # world size 1, so the distributed code runs on a one-GPU box too
-    use_dist = world > 1 or os.environ.get("MSD_BENCH_FORCE_DIST", "0") not in ("", "0")
-    if use_dist:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from meteorgpu import launch
+    if not launch.launched() and (a.gpus > 1 or a.spawn):
+        # start the ranks before anything here touches a GPU; each is this script again
+        sys.exit(launch.spawn([os.path.abspath(__file__)] + sys.argv[1:], a.gpus))
+    rank, world, local = launch.env_world()
+    if world != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)")
+    if a.dry_run:
+        return dry_run(rank, world)
+    from meteorgpu import _lib
+    ndev = _lib.device_count()
+    if local >= ndev:
+        sys.exit(f"bench.py: rank {rank} wants device {local} but only {ndev} GPU(s) are visible")
+    # the job's RCCL group: every launched rank (N > 1, or --spawn at N = 1) joins it
+    job_of = (lambda ctx: launch.Group(ctx, rank, world)) if launch.launched() else (lambda ctx: None)
     if a.workload in ("live", "c5", "files"):
-        {"live": main_live, "c5": main_c5, "files": main_files}[a.workload](a, world, rank, local, dist)
-        if dist is not None:
-            dist.destroy_process_group()
+        {"live": main_live, "c5": main_c5, "files": main_files}[a.workload](a, world, rank, local, job_of)
         return
 
-    from meteorgpu import _lib, synth
-    from meteorgpu.batch import BatchPipeline, Communicator
+    from meteorgpu import synth
+    from meteorgpu.batch import BatchPipeline
 
     pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
     mp_base = None
-    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
         # before any GPU call: the workers are forked from this process
         mp_files = a.cpu_files * a.cpu_procs // 4
         v, dt = cpu_baseline_mp(pool, mp_files, a.cpu_procs)
@@ -434,23 +462,17 @@ def main():
     us = lambda t: (t - epoch) // datetime.timedelta(microseconds=1)  # noqa: E731
     bp.set_start_times(np.array([us(day0 + datetime.timedelta(minutes=lo + i)) for i in range(F)], np.int64),
                        us(day0))
-    comm = None
-    if dist is not None:
-        obj = [Communicator.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm = Communicator(ctx, world, obj[0], rank)
+    job = job_of(ctx)
 
     def step():
         bp.run()
-        if comm is not None:
-            comm.allreduce_i64(bp.d_hist, bp.nbuckets)
+        if job is not None:
+            job.rccl.allreduce_i64(bp.d_hist, bp.nbuckets)
 
     def sync_all():
         ctx.synchronize()
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        if job is not None:
+            job.barrier()
 
     for _ in range(a.warmup):
         step()
@@ -468,14 +490,9 @@ def main():
         step()
     sync_all()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([int(counts.sum())], dtype=torch.int64, device="cuda")
-        dist.all_reduce(tot)
-        total_dets = int(tot.item())
+    if job is not None:
+        elapsed = job.max_f64(elapsed)
+        total_dets = int(job.sum_i64([int(counts.sum())])[0])
     else:
         total_dets = int(counts.sum())
     hist = bp.hour_counts()
@@ -534,7 +551,7 @@ def main():
         "block_delta": round(blk_ms / max(blk_launches, 1), 4),
         "detect": round(det_ms / max(det_launches, 1), 4),
     }
-    if rank == 0 and dist is None and not a.no_cpu_baseline and a.cpu_files > 0:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
         v, dt = cpu_baseline(pool, a.cpu_files)
         out["cpu_baseline"] = {
             "value": round(v, 2),
@@ -546,12 +563,11 @@ def main():
         }
     if mp_base is not None:
         out["cpu_baseline_multicore"] = mp_base
+    out["ranks_seen"] = job.ranks_seen() if job is not None else 1
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if comm is not None:
-        comm.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if job is not None:
+        job.close()
 
 
 if __name__ == "__main__":

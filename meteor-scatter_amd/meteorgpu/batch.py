@@ -165,7 +165,7 @@ class BatchPipeline:
 class Communicator:
     """RCCL communicator over the ranks of one job (one process per GPU).  The
     128-byte unique id is created by rank 0 and distributed by the caller
-    (bench.py uses torch.distributed's object broadcast for that rendezvous)."""
+    (meteorgpu.launch.Group shares it through a rendezvous file)."""
 
     @staticmethod
     def unique_id() -> bytes:

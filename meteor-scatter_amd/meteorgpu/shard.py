@@ -5,9 +5,9 @@ The reference processes files one by one in a single process (main.py:865-935 lo
 per-hour aggregation main.py:687-716).  Files are independent: each file's global
 threshold, adaptive window and freeze state are file-local (main.py:464-466, 450-522),
 so a batch shards as contiguous file ranges with no data-path collective; only the
-per-hour histogram (a few dozen int64) is all-reduced.  On GPUs that is one RCCL
-all-reduce on the device histogram (``batch.Communicator``); on the CPU (tests, gloo)
-``allreduce_counts`` does the same over torch.distributed.
+per-hour histogram (a few dozen int64) is all-reduced: one RCCL all-reduce on the device
+histogram (``batch.Communicator``, set up by ``launch.Group``).  The CPU tests stand in
+for it with a gloo all-reduce (tests/torch_comm.py).
 """
 from __future__ import annotations
 
@@ -51,18 +51,3 @@ def hour_histogram(start_blocks, file_start_us, block_sec: float, base_us: int, 
             if 0 <= b < nbuckets:
                 out[b] += 1
     return out
-
-
-def allreduce_counts(counts: np.ndarray, group=None) -> np.ndarray:
-    """Sum an int64 count vector over the ranks of a torch.distributed process group
-    (gloo on the host; the GPU path all-reduces the device histogram with RCCL instead).
-    Returns the reduced copy; a no-op without an initialised process group."""
-    import torch
-    import torch.distributed as dist
-
-    a = np.ascontiguousarray(counts, dtype=np.int64)
-    if not (dist.is_available() and dist.is_initialized()):
-        return a.copy()
-    t = torch.from_numpy(a.copy())
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return t.numpy()

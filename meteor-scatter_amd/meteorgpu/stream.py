@@ -53,36 +53,6 @@ class LocalComm:
     allgather_fixed = allgather  # every rank sends the same number of elements
 
 
-class TorchComm:
-    """torch.distributed process group (gloo on the host; tests and CPU runs)."""
-
-    def __init__(self, group=None):
-        import torch.distributed as dist
-        self.dist, self.group = dist, group
-        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
-
-    def allgather(self, a: np.ndarray) -> list[np.ndarray]:
-        import torch
-        a = np.ascontiguousarray(a)
-        n = torch.tensor([a.size], dtype=torch.int64)
-        ns = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
-        self.dist.all_gather(ns, n, group=self.group)
-        m = max(int(t.item()) for t in ns)
-        buf = np.zeros(max(m, 1), a.dtype)
-        buf[: a.size] = a
-        t = torch.from_numpy(buf)
-        outs = [torch.zeros_like(t) for _ in range(self.world)]
-        self.dist.all_gather(outs, t, group=self.group)
-        return [o.numpy()[: int(k.item())].copy() for o, k in zip(outs, ns)]
-
-    def allgather_fixed(self, a: np.ndarray) -> list[np.ndarray]:
-        import torch
-        t = torch.from_numpy(np.ascontiguousarray(a).copy())
-        outs = [torch.zeros_like(t) for _ in range(self.world)]
-        self.dist.all_gather(outs, t, group=self.group)
-        return [o.numpy().copy() for o in outs]
-
-
 class RcclComm:
     """RCCL over the GPUs of one job (msd_comm_allgather on device buffers)."""
 

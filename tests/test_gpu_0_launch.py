@@ -1,0 +1,45 @@
+"""GPU: bench.py through the torch-free launcher (--spawn at --gpus 1: rendezvous file, RCCL
+communicator, barrier / max / rank count through libmsdsp) for the three workloads the
+multi-GPU configs use -- C3 (a day per GPU), C4 (--shard-day) and C5 (the I/Q stream with its
+RCCL exchanges).  Named to run first in `-m gpu`, so the pytest process has not opened the
+GPU when it starts the child."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=240):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "MSD_RDZV_KEY"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--spawn", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", *args], capture_output=True, text=True,
+                       timeout=timeout, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["ranks_seen"] == 1 and d["value"] > 0
+    return d
+
+
+def test_spawn_c3():
+    d = _bench("--files", "16")
+    assert d["scaling"] == "weak" and d["config"]["files_per_gpu"] == 16 and d["roofline"]["frac"] > 0
+
+
+def test_spawn_c4_shard_day():
+    d = _bench("--files", "24", "--shard-day")
+    assert d["scaling"] == "strong" and d["config"]["files_per_gpu"] == 24
+
+
+def test_spawn_c5():
+    d = _bench("--workload", "c5", "--c5-seconds", "300")
+    assert d["config"]["samples_per_gpu"] == 192000 * 300 and d["detections_per_step"] > 0

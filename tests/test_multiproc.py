@@ -36,16 +36,17 @@ def _dets(i):
 
 
 def _rank_main(rank, world, port, out_dir):
-    sys.path[:0] = [ROOT, os.path.join(ROOT, "meteor-scatter_amd")]
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "meteor-scatter_amd"), os.path.join(ROOT, "tests")]
     import torch.distributed as dist
     from meteorgpu import shard
+    from torch_comm import allreduce_counts
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         lo, hi = shard.shard_range(NFILES, rank, world)
         starts = [[round(d[0] / 0.2) for d in _dets(i)] for i in range(lo, hi)]
         file_us = [shard.to_us(DAY0 + i * STEP) for i in range(lo, hi)]
         local = shard.hour_histogram(starts, file_us, 0.2, shard.to_us(DAY0), 24)
-        total = shard.allreduce_counts(local)
+        total = allreduce_counts(local)
         np.save(os.path.join(out_dir, f"r{rank}.npy"), np.stack([local, total]))
     finally:
         dist.destroy_process_group()

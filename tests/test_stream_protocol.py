@@ -114,12 +114,13 @@ def _gloo_rank(rank, world, port, out):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "meteor-scatter_amd"), os.path.join(ROOT, "tests")]
     import torch.distributed as dist
     from stream_np_ops import NumpyStreamOps as Ops
+    from torch_comm import TorchComm
     from meteorgpu import stream as S
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         d = make_delta(25000, 15, rate=0.01)
         lo, hi = shard_bounds(d.size, world, rank)
-        res = S.StreamDetector(Ops(d[lo:hi], d.size, lo, True, 4.0, 600, 100, 50), S.TorchComm(), True, 4.0,
+        res = S.StreamDetector(Ops(d[lo:hi], d.size, lo, True, 4.0, 600, 100, 50), TorchComm(), True, 4.0,
                                600, 50).run()
         np.save(os.path.join(out, f"r{rank}.npy"), np.stack([res.detections["start"], res.detections["stop"]]))
         np.save(os.path.join(out, f"db{rank}.npy"), res.detections["db"])
