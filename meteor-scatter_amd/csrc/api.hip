@@ -7,6 +7,8 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <set>
+#include <tuple>
 
 #include "msd_internal.h"
 
@@ -21,6 +23,18 @@ int fail(int code, const std::string &msg) {
 }
 int hip_fail(hipError_t e, const char *what) {
     return fail(MSD_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure_dyn_lds(const void *kernel, int bytes) {
+    static std::mutex mu;
+    static std::set<std::tuple<const void *, int, int>> done;  // (kernel, device, bytes)
+    int dev = 0;
+    MSD_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({kernel, dev, bytes})) return MSD_OK;
+    MSD_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.insert({kernel, dev, bytes});
+    return MSD_OK;
 }
 
 KernelTimer::KernelTimer(msd_ctx *c, int k) : ctx(c), kernel(k) {

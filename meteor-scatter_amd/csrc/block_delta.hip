@@ -15,11 +15,7 @@
 #include "msd_internal.h"
 #include "np_reduce.h"
 
-#ifdef BD2_OLDFORM
-#define BD2_STEP(c, a, b, w) ((w) + (c) * (a) - (b))
-#else
 #define BD2_STEP(c, a, b, w) fma((c), (a), (w) - (b))
-#endif
 
 namespace msd {
 namespace {
@@ -203,12 +199,8 @@ __device__ __forceinline__ void bd2_sweep(const T *__restrict__ xb, const double
         const double re = row_sum_d(fma(yr, rot.x, -yi * rot.y));
         const double im = row_sum_d(fma(yr, rot.y, yi * rot.x));
         if (sub == 0) {
-#ifdef MSD_BD_HYPOT
-            const double h = hypot(re, im);  // np.abs(complex) then **2
-            pb[j0 + t] = h * h;
-#else  // re^2 + im^2: within 2 ulp of np.abs(X)**2 (the bar is 1e-9 dB), without hypot's scaling code
+            // re^2 + im^2: within 2 ulp of np.abs(X)**2 (the bar is 1e-9 dB), without hypot's scaling code
             pb[j0 + t] = re * re + im * im;
-#endif
         }
     }
 }
@@ -314,12 +306,9 @@ int launch_bd(msd_block_plan *p, const void *x, const int64_t *off, const int64_
     const int64_t grid = (waves + BD_WAVES - 1) / BD_WAVES;
     if (grid > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "block_delta: grid too large");
     const size_t lds = sizeof(double) * BD_WAVES * (size_t)(p->nbins > 0 ? p->nbins : 1);
-    static bool attr_set = false;
-    if (!attr_set) {
-        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(block_delta_kernel<T, SPL>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(double) * BD_WAVES * BD_MAXBINS)));
-        attr_set = true;
-    }
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(block_delta_kernel<T, SPL>),
+                                (int)(sizeof(double) * BD_WAVES * BD_MAXBINS)))
+        return rc;
     hipLaunchKernelGGL((block_delta_kernel<T, SPL>), dim3((unsigned)grid), dim3(BD_WAVES * 64), lds, p->ctx->stream,
                        static_cast<const T *>(x), off, len, nfiles, max_blocks, p->block_size, p->L, p->nfft,
                        p->d_window, p->d_tw, p->d_bins, p->band_hi - p->band_lo + 1 > 0 ? p->band_hi - p->band_lo + 1 : 0,

@@ -214,11 +214,8 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
 #pragma unroll
             for (int k2b = 0; k2b < 16; ++k2b) {
                 const float pw = v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y;
-#ifndef MSD_NO_NT_STORE  // streaming (non-temporal) stores: the output is written once, never re-read here (A/B: -1 to -2 %)
+                // streaming (non-temporal) stores: written once, never re-read here (A/B: -1 to -2 %)
                 __builtin_nontemporal_store(pw, of + tid + 256 * k2b);
-#else
-                of[tid + 256 * k2b] = pw;
-#endif
             }
             // no barrier at the end: the next frame writes buf / red only after its first
             // barrier, which every wave reaches after its pass-3 reads of this frame
@@ -313,10 +310,7 @@ int msd_cstft_psd_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
     DeviceGuard g(p->ctx->device);
     const int64_t total = nstreams * max_frames;
-#ifndef MSD_CS_WG_PER_CU
-#define MSD_CS_WG_PER_CU 3
-#endif
-    int64_t wgs = (int64_t)p->ctx->num_cu * MSD_CS_WG_PER_CU;  // persistent: LDS (37 KB) allows 4 per CU
+    int64_t wgs = (int64_t)p->ctx->num_cu * 3;  // persistent: LDS (37 KB) allows 4 per CU
     if (wgs > total) wgs = total;
     const int64_t per = (total + wgs - 1) / wgs;
     wgs = (total + per - 1) / per;

@@ -478,12 +478,7 @@ int launch_welch_t(msd_welch_plan *p, const void *x, const int64_t *off, const i
     const int nw = (int)std::min<size_t>(WL_THREADS / 64, (160 * 1024) / wave_bytes);
     if (nw < 1) return fail(MSD_ERR_UNSUPPORTED, "welch: nperseg + band bins exceed the LDS budget");
     const size_t lds = wave_bytes * nw;
-    static bool attr = false;
-    if (!attr) {
-        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(welch_bands_kernel<T>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(welch_bands_kernel<T>), 160 * 1024)) return rc;
     const int64_t grid = (nfiles * max_blocks + nw - 1) / nw;  // a wave per block
     if (grid > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "welch: grid too large");
     KernelTimer timer(p->ctx, K_WELCH);

@@ -14,6 +14,9 @@ namespace msd {
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
 int hip_fail(hipError_t e, const char *what);
+// hipFuncAttributeMaxDynamicSharedMemorySize = bytes for `kernel` on the CURRENT device, once
+// per (kernel, device); thread-safe (several contexts may launch from several threads)
+int ensure_dyn_lds(const void *kernel, int bytes);
 
 #define MSD_HIP(call)                                   \
     do {                                                \

@@ -266,12 +266,7 @@ int launch_t(msd_stft_plan *p, const void *x, const int64_t *off, const int64_t 
              int64_t ld) {
     using G = StftGeom<M, NW, TT>;
     auto kern = stft_psd_kernel<M, NW, TT, T>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES));
-        attr_set = true;
-    }
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(kern), G::LDS_BYTES)) return rc;
     const int64_t tiles = ld / TT;
     const int64_t blocks = tiles * nfiles;
     if (blocks > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "stft: grid too large");

@@ -14,7 +14,7 @@
 //           pi(0)=0, pi(1)=32), so it holds Z[pi(l) + 64 r] and the conjugate partner
 //           Z[512 - k] lives in lane l^1 (one DPP quad_perm per value);
 //   post    real-spectrum split, |X|^2 * scale (x2 off DC / Nyquist) → LDS tile
-//           [513][32] (row pitch 34: conflict-free 8-B writes of the frame pair).
+//           [513][32] (row pitch 34, tile_at()).
 // One workgroup = 16 waves (4 per SIMD: one wave alone issues a VALU op only every
 // ~4 cycles, so the SIMD needs several) = one tile of 32 consecutive frames, one
 // frame pair per wave.  The tile leaves as 128-B row segments.  Workgroups are
@@ -90,59 +90,6 @@ __device__ __forceinline__ void dft8_windowed(float2 *v, const float2 *d, const 
     dft8_tail(v, a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]);
 }
 
-#ifdef MSD_STFT_PK
-// ---- frame-pair packed arithmetic (experiment MSD_STFT_PK, off by default): the wave's two frames A, B ride in the two halves of
-// 64-bit register pairs, {A.re, B.re} and {A.im, B.im}, so every butterfly is one v_pk_add_f32 /
-// v_pk_mul_f32 / v_pk_fma_f32 for both frames; twiddles and window values, shared by the frames,
-// are broadcast.  Half the VALU instructions of the scalar path, but no faster (A/B +1 %): in
-// isolation v_pk_add_f32 issues in 5.0 cycles vs 2.9 for v_add_f32 and v_pk_fma_f32 in 5.1 vs 4.2
-// (tools/ubench/pk_rate2.hip), in this kernel's mix a packed op costs about two scalar ones.
-typedef float f2 __attribute__((ext_vector_type(2)));
-struct C2 {
-    f2 re, im;
-};
-__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
-__device__ __forceinline__ C2 padd(C2 a, C2 b) { return {a.re + b.re, a.im + b.im}; }
-__device__ __forceinline__ C2 psub(C2 a, C2 b) { return {a.re - b.re, a.im - b.im}; }
-__device__ __forceinline__ C2 pmi(C2 a) { return {a.im, -a.re}; }  // a * (-i)
-__device__ __forceinline__ C2 ptw(C2 a, float2 w) {               // a * w, w shared by both frames
-    const f2 wx = splat(w.x), wy = splat(w.y);
-    return {a.re * wx - a.im * wy, a.re * wy + a.im * wx};
-}
-__device__ __forceinline__ void pdft4(C2 &a0, C2 &a1, C2 &a2, C2 &a3) {
-    const C2 t0 = padd(a0, a2), t1 = psub(a0, a2), t2 = padd(a1, a3), t3 = pmi(psub(a1, a3));
-    a0 = padd(t0, t2);
-    a1 = padd(t1, t3);
-    a2 = psub(t0, t2);
-    a3 = psub(t1, t3);
-}
-__device__ __forceinline__ void pdft8_tail(C2 *v, C2 a0, C2 a1, C2 a2, C2 a3, C2 b0, C2 b1, C2 b2, C2 b3) {
-    const f2 s = splat(0.70710678118654752440f);
-    b1 = {(b1.re + b1.im) * s, (b1.im - b1.re) * s};
-    b2 = pmi(b2);
-    b3 = {(b3.im - b3.re) * s, -(b3.re + b3.im) * s};
-    pdft4(a0, a1, a2, a3);
-    pdft4(b0, b1, b2, b3);
-    v[0] = a0; v[2] = a1; v[4] = a2; v[6] = a3;
-    v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
-}
-__device__ __forceinline__ void pdft8(C2 *v) {
-    pdft8_tail(v, padd(v[0], v[4]), padd(v[1], v[5]), padd(v[2], v[6]), padd(v[3], v[7]), psub(v[0], v[4]),
-               psub(v[1], v[5]), psub(v[2], v[6]), psub(v[3], v[7]));
-}
-// dft8 of the windowed points (window pair w = (w_even, w_odd) per point, shared by the frames)
-__device__ __forceinline__ void pdft8_windowed(C2 *v, const float2 *w) {
-    C2 a[4], b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const f2 px = v[j + 4].re * splat(w[j + 4].x), py = v[j + 4].im * splat(w[j + 4].y);
-        const f2 qx = splat(w[j].x), qy = splat(w[j].y);
-        a[j] = {__builtin_elementwise_fma(v[j].re, qx, px), __builtin_elementwise_fma(v[j].im, qy, py)};
-        b[j] = {__builtin_elementwise_fma(v[j].re, qx, -px), __builtin_elementwise_fma(v[j].im, qy, -py)};
-    }
-    pdft8_tail(v, a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]);
-}
-#endif
 
 // Transpose-scratch layout (float2 index): bit 4 of n flips bits 1 and 3, plus 4 float2 of
 // padding per 32.  Together with the pass-3 lane table below it makes all four transpose
@@ -156,6 +103,10 @@ __constant__ int8_t k_pass3_lane[64] = {0,  32, 1,  63, 3,  61, 5,  59, 6,  58, 
                                         13, 51, 15, 49, 16, 48, 18, 46, 25, 39, 26, 38, 27, 37, 28, 36,
                                         2,  62, 4,  60, 8,  56, 9,  55, 10, 54, 11, 53, 17, 47, 19, 45,
                                         20, 44, 21, 43, 22, 42, 23, 41, 24, 40, 29, 35, 30, 34, 31, 33};
+
+// Output tile: bin k, frame column c at k * 34 + c (pitch 34 keeps rows 8-B aligned; an
+// XOR-swizzled pitch-32 tile read by conflict-free ds_read_b128 measured 1.5 % slower)
+__device__ __forceinline__ int tile_at(int k, int c) { return k * F_PITCH + c; }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -282,145 +233,32 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     // transform and the prefetched samples waited for at the top of the loop are never younger
     // than a tile's stores.
     auto write_out = [&](const FileCur &wc) {
-        // scalar base + lane offsets, 8 lanes x 16 B per row: two 8-B LDS reads (pitch 34 keeps
-        // rows 8-B aligned) → one 16-B store.  WIDE = 0: 32-bit offsets (K*ld*4 < 2^32, i.e.
-        // ld < 2^21 frames); WIDE = 1: 64-bit (longer files)
+        // scalar base + lane offsets, 8 lanes x 16 B per row: two 8-B LDS reads → one 16-B
+        // store.  WIDE = 0: 32-bit offsets (K*ld*4 < 2^32, i.e. ld < 2^21 frames); WIDE = 1:
+        // 64-bit (longer files)
         char *of = reinterpret_cast<char *>(out + wc.f * (int64_t)F_K * ld + wc.ti * F_TT);
         const int qq = tid & 7;
 #pragma unroll
         for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 8) {
             const int k = k0 + (tid >> 3);
             if (k < F_K) {
-                const float2 a = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq]);
-                const float2 b = *reinterpret_cast<const float2 *>(&tile[k * F_PITCH + 4 * qq + 2]);
+                const float2 a = *reinterpret_cast<const float2 *>(&tile[tile_at(k, 4 * qq)]);
+                const float2 b = *reinterpret_cast<const float2 *>(&tile[tile_at(k, 4 * qq + 2)]);
                 const float4 v = make_float4(a.x, a.y, b.x, b.y);
                 float4 *dst;
                 if constexpr (WIDE)
                     dst = reinterpret_cast<float4 *>(of + ((int64_t)k * ld * 4 + 16 * qq));
                 else
                     dst = reinterpret_cast<float4 *>(of + ((uint32_t)k * ((uint32_t)ld * 4u) + 16u * (uint32_t)qq));
-#ifndef MSD_NO_NT_STORE  // streaming (non-temporal) stores: the output is written once, never re-read here (A/B: -1 to -2 %)
+                // streaming (non-temporal) stores: written once, never re-read here (A/B: -1 to -2 %)
                 typedef float f4v __attribute__((ext_vector_type(4)));
                 __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v *>(dst));
-#else
-                *dst = v;
-#endif
             }
         }
     };
     FileCur prev = cur;
     bool have_prev = false;
 
-#ifdef MSD_STFT_PK  // experiment (off): frame-pair packed math; A/B +1 % — the v_pk ops cost about two scalar ops here
-    f2 *scr2 = reinterpret_cast<f2 *>(scr);  // the scratch as {A, B} pairs: re round, then im round
-    for (int64_t tl = tb; tl < te; ++tl) {
-        const bool has_next = tl + 1 < te;
-        const FileCur nxt = has_next ? advance(cur) : cur;
-        C2 P[8];
-        float2 wv[8];
-        // ---- detrend (consumes raw); the window is applied inside pass 1
-        {
-            float mean[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                if constexpr (IO::kInt) {
-                    int s = 0;
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) s = IO::sum2(raw[q][r], s);
-                    s = row_sum_i(s);
-                    const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
-                                    __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
-                    mean[q] = detrend ? (float)((double)tot * (1.0 / 1024.0)) : 0.f;
-                } else {
-                    float s = 0.f;
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) s += IO::lo(raw[q][r]) + IO::hi(raw[q][r]);
-                    s = row_sum_f(s);
-                    auto rl = [](float a, int lane) {
-                        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), lane));
-                    };
-                    const float tot = (rl(s, 0) + rl(s, 16)) + (rl(s, 32) + rl(s, 48));
-                    mean[q] = detrend ? tot * (1.0f / 1024.0f) : 0.f;
-                }
-            }
-            const f2 mv = {mean[0], mean[1]};
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                wv[r] = t_win[r * 64 + l];
-                P[r].re = f2{IO::lo(raw[0][r]), IO::lo(raw[1][r])} - mv;
-                P[r].im = f2{IO::hi(raw[0][r]), IO::hi(raw[1][r])} - mv;
-            }
-        }
-        if (have_prev) write_out(prev);
-        // ---- prefetch the next tile's frame pair into the (now free) sample registers
-        if (has_next) load_pair<T>(x, nxt, nxt.ti * F_TT + wcol, hop, l, raw);
-
-        // ---- pass 1 (Ns = 1): out[8 l + r]; transposed in two rounds (re pairs, im pairs)
-        pdft8_windowed(P, wv);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) scr2[phys(8 * l + r)] = h ? P[r].im : P[r].re;
-            wave_sync();
-#pragma unroll
-            for (int r = 0; r < 8; ++r) (h ? P[r].im : P[r].re) = scr2[phys(l + 64 * r)];
-            wave_sync();
-        }
-        // ---- pass 2 (Ns = 8): out[64 (l>>3) + (l&7) + 8 r]
-        const int o2 = 64 * (l >> 3) + (l & 7);
-#pragma unroll
-        for (int r = 1; r < 8; ++r) P[r] = ptw(P[r], t_tw2[r * 64 + l]);
-        pdft8(P);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) scr2[phys(o2 + 8 * r)] = h ? P[r].im : P[r].re;
-            wave_sync();
-#pragma unroll
-            for (int r = 0; r < 8; ++r) (h ? P[r].im : P[r].re) = scr2[phys(pi + 64 * r)];
-            wave_sync();
-        }
-        // ---- pass 3 (Ns = 64): butterfly pi(l) → lane holds Z[pi(l) + 64 r]
-#pragma unroll
-        for (int r = 1; r < 8; ++r) P[r] = ptw(P[r], t_tw3[r * 64 + l]);
-        pdft8(P);
-        // ---- post (see the unpacked branch below for the algebra), both frames at once
-        f2 pa[4], pb[4];
-        const f2 sc0 = splat(l == 0 ? 0.5f : 1.0f);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float2 wk = t_post[r * 64 + l];
-            const C2 sv = P[7 - r];
-            C2 m;
-            m.re = f2{dpp_f<0xB1>(sv.re.x), dpp_f<0xB1>(sv.re.y)};
-            m.im = f2{dpp_f<0xB1>(sv.im.x), dpp_f<0xB1>(sv.im.y)};
-            if (l < 2) m = (l == 0) ? P[(8 - r) & 7] : sv;
-            const C2 z = P[r];
-            const C2 e = {z.re + m.re, z.im - m.im};
-            const C2 o = {z.im + m.im, m.re - z.re};  // -i (z - conj m)
-            const C2 t = ptw(o, wk);
-            const C2 X1 = padd(e, t), X2 = psub(e, t);
-            pa[r] = X1.re * X1.re + X1.im * X1.im;
-            pb[r] = X2.re * X2.re + X2.im * X2.im;
-            if (r == 0) {
-                pa[r] *= sc0;
-                pb[r] *= sc0;
-            }
-        }
-        const f2 p256 = (P[4].re * P[4].re + P[4].im * P[4].im) * splat(4.0f);  // lane 0: bin 256
-        lds_barrier();  // the previous tile's write-out has finished reading the tile
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            *reinterpret_cast<f2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = pa[r];
-            *reinterpret_cast<f2 *>(&tile[(512 - pi - 64 * r) * F_PITCH + wcol]) = pb[r];
-        }
-        if (l == 0) *reinterpret_cast<f2 *>(&tile[256 * F_PITCH + wcol]) = p256;
-        lds_barrier();  // tile complete
-        prev = cur;
-        have_prev = true;
-        cur = nxt;
-    }
-#else
     for (int64_t tl = tb; tl < te; ++tl) {
         const bool has_next = tl + 1 < te;
         const FileCur nxt = has_next ? advance(cur) : cur;
@@ -543,28 +381,18 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             const float2 z = v[q][4];
             p256[q] = (z.x * z.x + z.y * z.y) * 4.0f;
         }
-#ifdef MSD_EXP_PAD  // experiment: extra VALU per frame pair
-        {
-            float dmy = pa[0][0];
-#pragma unroll
-            for (int i = 0; i < MSD_EXP_PAD; ++i) asm volatile("v_add_f32 %0, %0, %1" : "+v"(dmy) : "v"(pb[0][1]));
-            pa[0][0] = dmy;
-        }
-#endif
         lds_barrier();  // the previous tile's write-out has finished reading the tile
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            *reinterpret_cast<float2 *>(&tile[(pi + 64 * r) * F_PITCH + wcol]) = make_float2(pa[0][r], pa[1][r]);
-            *reinterpret_cast<float2 *>(&tile[(512 - pi - 64 * r) * F_PITCH + wcol]) =
-                make_float2(pb[0][r], pb[1][r]);
+            *reinterpret_cast<float2 *>(&tile[tile_at(pi + 64 * r, wcol)]) = make_float2(pa[0][r], pa[1][r]);
+            *reinterpret_cast<float2 *>(&tile[tile_at(512 - pi - 64 * r, wcol)]) = make_float2(pb[0][r], pb[1][r]);
         }
-        if (l == 0) *reinterpret_cast<float2 *>(&tile[256 * F_PITCH + wcol]) = make_float2(p256[0], p256[1]);
+        if (l == 0) *reinterpret_cast<float2 *>(&tile[tile_at(256, wcol)]) = make_float2(p256[0], p256[1]);
         lds_barrier();  // tile complete
         prev = cur;
         have_prev = true;
         cur = nxt;
     }
-#endif
     write_out(prev);  // the last tile (complete since the loop's final barrier)
 }
 
@@ -573,14 +401,7 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
                   int64_t ld) {
     const bool wide = (uint64_t)F_K * (uint64_t)ld * 4u >= (1ull << 32);
     auto kern = wide ? stft1024_kernel<T, 1> : stft1024_kernel<T, 0>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(stft1024_kernel<T, 0>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
-        MSD_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(stft1024_kernel<T, 1>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
-        attr_set = true;
-    }
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(kern), F_LDS)) return rc;
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->ctx->device);
     const int64_t tiles_per_file = ld / F_TT;

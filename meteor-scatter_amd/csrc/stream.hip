@@ -180,22 +180,16 @@ __global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restric
 // {offset, length (<= 128), adds that follow it, 1 if a chunk ends after them}
 constexpr int FR_MAXREC_LDS = 512;  // records kept in LDS (W up to ~32K); more are read from HBM
 
-#ifndef MSD_FR_THREADS
-#define MSD_FR_THREADS 64
-#endif
-#ifndef MSD_FR_F
-#define MSD_FR_F 8
-#endif
-constexpr int FR_THREADS = MSD_FR_THREADS;       // a workgroup computes one tile
-constexpr int FR_F = MSD_FR_F;                   // frames per lane
+constexpr int FR_THREADS = 64;                   // a workgroup computes one tile
+constexpr int FR_F = 8;                          // frames per lane
 constexpr int FR_FRAMES = FR_THREADS * FR_F;     // frames per tile
 constexpr int FR_STAGE = FR_FRAMES + 128;        // staged elements per leaf (leaf <= 128)
-// pad (conflict-free LDS reads): F = 8: 2 doubles per 8 (16-B reads); F = 4: 1 per 4 (8-B reads)
+// pad (conflict-free 16-B LDS reads): 2 doubles per 8
 constexpr int FR_PADDED = FR_STAGE + FR_STAGE / 4;
 constexpr int FR_LOADS = (FR_STAGE + FR_THREADS - 1) / FR_THREADS;
 constexpr int FR_DEPTH = 7;
 
-__device__ __forceinline__ int padded(int q) { return FR_F == 8 ? q + 2 * (q >> 3) : q + (q >> 2); }
+__device__ __forceinline__ int padded(int q) { return q + 2 * (q >> 3); }
 
 struct FreshParams {
     int64_t n_local, frame0, n_tail, x_len, W, F0;
@@ -212,7 +206,6 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
                                            const int4 *recs, int nleaf, double *stage,
                                            const double (&mean)[FR_F], double (&out)[FR_F]) {
     const int tid = threadIdx.x;
-#if MSD_FR_F == 8
     // 8 frames: the pending partial sums live in scratch (a runtime-indexed array; 8 x 7 doubles
     // would not fit beside the 64 accumulators), touched once per leaf / add
     double stk_[FR_DEPTH + 1][FR_F];
@@ -231,32 +224,6 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
         for (int f = 0; f < FR_F; ++f) top(1, f) = top(1, f) + top(0, f);
         pop();
     };
-#else
-    // the tree's pending partial sums, top at stk[0]: a push shifts the stack down, an add pops
-    // the top into the next entry and shifts up -- static register indices only (a runtime-indexed
-    // array would live in scratch); depth <= 7 for numpy's trees of <= 8192 elements
-    double stk[FR_DEPTH][FR_F];
-    auto top = [&](int d, int f) -> double & { return stk[d][f]; };
-    auto push = [&](const double (&v)[FR_F]) {
-#pragma unroll
-        for (int d = FR_DEPTH - 1; d > 0; --d)
-#pragma unroll
-            for (int f = 0; f < FR_F; ++f) stk[d][f] = stk[d - 1][f];
-#pragma unroll
-        for (int f = 0; f < FR_F; ++f) stk[0][f] = v[f];
-    };
-    auto pop = [&]() {
-#pragma unroll
-        for (int d = 0; d < FR_DEPTH - 1; ++d)
-#pragma unroll
-            for (int f = 0; f < FR_F; ++f) stk[d][f] = stk[d + 1][f];
-    };
-    auto add_top = [&]() {
-#pragma unroll
-        for (int f = 0; f < FR_F; ++f) stk[1][f] = stk[1][f] + stk[0][f];
-        pop();
-    };
-#endif
     double acc[FR_F];
 #pragma unroll
     for (int f = 0; f < FR_F; ++f) acc[f] = 0.0;
@@ -338,9 +305,6 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
             using T_ = std::integral_constant<bool, true>;
             using F_ = std::integral_constant<bool, false>;
             group(0, T_{}, F_{});
-#ifdef MSD_FR_UNROLL
-#pragma unroll MSD_FR_UNROLL
-#endif
             for (int g = 1; g < G; ++g) group(g, F_{}, F_{});
             group(G, F_{}, T_{});
 #pragma unroll
