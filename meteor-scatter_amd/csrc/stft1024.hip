@@ -229,9 +229,9 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     raw_t raw[2][8];
     load_pair<T>(x, cur, cur.ti * F_TT + wcol, hop, l, raw);
     // ---- tile → HBM: 513 rows x 32 floats (128 B), 8 lanes x 16 B per row.  Issued one
-    // iteration late (after the next tile's detrend), so the stores drain during that tile's
-    // transform and the prefetched samples waited for at the top of the loop are never younger
-    // than a tile's stores.
+    // iteration late (in the middle of the next tile's transform), so the stores drain while
+    // that tile computes; the next prefetch is issued before them, so the wait for it at the top
+    // of the loop never waits for a tile's stores.
     auto write_out = [&](const FileCur &wc) {
         // scalar base + lane offsets, 8 lanes x 16 B per row: two 8-B LDS reads → one 16-B
         // store.  WIDE = 0: 32-bit offsets (K*ld*4 < 2^32, i.e. ld < 2^21 frames); WIDE = 1:
@@ -275,7 +275,9 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                     s = row_sum_i(s);
                     const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
                                     __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
-                    mean[q] = detrend ? (float)((double)tot * (1.0 / 1024.0)) : 0.f;
+                    // float(tot) rounds tot to 24 bits exactly as rounding tot / 1024 would (a
+                    // power-of-two scale), so this equals float((double)tot / 1024) without FP64
+                    mean[q] = detrend ? (float)tot * (1.0f / 1024.0f) : 0.f;
                 } else {
                     float s = 0.f;
 #pragma unroll
@@ -296,7 +298,6 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                     v[q][r] = make_float2(IO::lo(raw[q][r]) - mean[q], IO::hi(raw[q][r]) - mean[q]);
             }
         }
-        if (have_prev) write_out(prev);
         // ---- prefetch the next tile's frame pair into the (now free) sample registers
         if (has_next) load_pair<T>(x, nxt, nxt.ti * F_TT + wcol, hop, l, raw);
 
@@ -315,6 +316,9 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             for (int r = 0; r < 8; ++r) v[q][r] = scr[phys(l + 64 * r)];
             wave_sync();
         }
+        // the previous tile's write-out, between the first transposes and pass 2: its LDS reads
+        // and stores then overlap the other waves' arithmetic (A/B: -2 % against the loop top)
+        if (have_prev) write_out(prev);
         // ---- pass 2 (Ns = 8): out[64 (l>>3) + (l&7) + 8 r]
         const int o2 = 64 * (l >> 3) + (l & 7);
 #pragma unroll

@@ -8,6 +8,8 @@
 //   2: registers, 2 frames per wave: float2 per row, 16 waves per tile
 //   3: mode 1 with nontemporal stores
 //   4: registers, 8 frames per wave (two float4 per row), 4 waves per tile
+//   5: LDS-tile pattern with 16-frame tiles: 64-B row segments, 4 lanes x 16 B per row
+//   6: LDS-tile pattern with 64-frame tiles: 256-B row segments, 16 lanes x 16 B per row
 // Prints GB/s for each mode; the byte count is the spectrogram (16.6 GB).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -46,6 +48,23 @@ __global__ __launch_bounds__(1024) void wr(float *out, int64_t ld, int64_t tiles
                 const int k = l + 64 * r;
                 if (k < K) *reinterpret_cast<float2 *>(of + (int64_t)k * ld + 2 * w) = make_float2(k, tl);
             }
+        } else if (mode == 5) {  // tile tl covers 16 frames: two per 32-frame "tile" index
+            for (int h = 0; h < 2; ++h) {
+                const int q = tid & 3;
+                for (int k0 = 0; k0 < K; k0 += 256) {
+                    const int k = k0 + (tid >> 2);
+                    if (k < K)
+                        *reinterpret_cast<float4 *>(of + (int64_t)k * ld + 16 * h + 4 * q) = make_float4(k, tl, 1.f, 2.f);
+                }
+            }
+        } else if (mode == 6) {  // pairs of 32-frame tiles as one 64-frame tile
+            if (it & 1) continue;
+            const int q = tid & 15;
+            for (int k0 = 0; k0 < K; k0 += 64) {
+                const int k = k0 + (tid >> 4);
+                if (k < K && ti + 1 < tiles_per_file)
+                    *reinterpret_cast<float4 *>(of + (int64_t)k * ld + 4 * q) = make_float4(k, tl, 1.f, 2.f);
+            }
         } else if (mode == 4) {
             if (w >= 4) continue;
             for (int r = 0; r < 9; ++r) {
@@ -70,7 +89,7 @@ int main() {
     hipEventCreate(&b);
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-    for (int mode = 0; mode <= 4; ++mode) {
+    for (int mode : {0, 5, 6}) {
         for (int wpc = 1; wpc <= 2; ++wpc) {
             const int64_t wgs = (int64_t)cus * wpc;
             const int64_t per = (ntiles + wgs - 1) / wgs;
