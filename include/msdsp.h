@@ -92,10 +92,23 @@ int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches
  * window: N float32 values of the periodic Hann (scipy get_window, cast to
  * complex64 by _spectral_helper, i.e. float32); scale = 1/(fs*sum(w^2)) as
  * scipy computes it.  Output: float32 [K = N/2+1][T], T = (n-N)/hop + 1, with
- * bins 1..N/2-1 doubled (one-sided, even N). */
+ * bins 1..N/2-1 doubled (one-sided, even N).  N: a power of two in [16, 16384]
+ * (1024: stft1024.hip; 256..2048: stft.hip's tiled kernel; others: stft_any.hip). */
 int msd_stft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float *window, double scale,
                          msd_stft_plan **out);
+/* The general form: segments of nperseg samples (any length >= 1) zero-padded to an nfft-point
+ * transform (nfft a power of two in [16, 16384], nfft >= nperseg), K = nfft/2 + 1 bins, in
+ * float32 (precision MSD_F32, output float) or float64 (MSD_F64, output double; the
+ * msd_stft_psd_f64 entry points).  Covers scipy.signal.spectrogram(..., nfft=) and its
+ * shrinking of nperseg to a short input (dsp/src/main.py:127-133 with n_fft = 1024*4,
+ * :278-300; scipy _spectral_py.py _triage_segments) and matplotlib.mlab.specgram in float64
+ * (prime_detection.py:70, window_hanning, detrend_none, pad_to = NFFT).  window: nperseg
+ * float64 values (cast to float32 by a float32 plan). */
+int msd_stft_plan_create_ex(msd_ctx *ctx, int32_t nperseg, int32_t nfft, int32_t hop, const double *window,
+                            double scale, int precision, msd_stft_plan **out);
 void msd_stft_plan_destroy(msd_stft_plan *plan);
+/* K = nfft/2 + 1, the rows of the plan's spectrogram */
+int32_t msd_stft_bins(const msd_stft_plan *plan);
 /* detrend: 1 = 'constant' (scipy's default, the plan's initial setting), 0 = none
  * (matplotlib.mlab.specgram's detrend_none, prime_detection.py:70) */
 int msd_stft_plan_set_detrend(msd_stft_plan *plan, int detrend);
@@ -108,6 +121,10 @@ int msd_stft_psd_dev(msd_stft_plan *plan, const void *x, int dtype, const int64_
                      int64_t nfiles, int64_t max_frames, float *out, int64_t ld);
 /* single signal, host buffers: out is dense float32 [K][T] */
 int msd_stft_psd(msd_stft_plan *plan, const void *x, int dtype, int64_t n, float *out, int64_t *frames);
+/* the same two for a float64 plan (msd_stft_plan_create_ex with MSD_F64): out is double */
+int msd_stft_psd_f64_dev(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                         int64_t nfiles, int64_t max_frames, double *out, int64_t ld);
+int msd_stft_psd_f64(msd_stft_plan *plan, const void *x, int dtype, int64_t n, double *out, int64_t *frames);
 
 /* --------------------------------------- a2/a3: block band energies → delta
  * Replaces the per-block loop of dsp/src/main.py:352-393:
@@ -288,6 +305,10 @@ int msd_stream_detect_local(msd_stream_plan *plan, int32_t exact_thresholds, msd
  * writes it; out[f] (device) = sum over k in [lo, hi], t < frames of spec, float64. */
 int msd_spec_band_sum_dev(msd_ctx *ctx, const float *spec, int64_t nfiles, int32_t K, int64_t frames, int64_t ld,
                           int32_t lo, int32_t hi, double *out);
+/* the same over a float64 spectrogram (msd_stft_psd_f64_dev: the legacy specgram in mlab's
+ * float64) */
+int msd_spec_band_sum_f64_dev(msd_ctx *ctx, const double *spec, int64_t nfiles, int32_t K, int64_t frames,
+                              int64_t ld, int32_t lo, int32_t hi, double *out);
 
 /* ------------------------------------------------ a8: Welch band powers (phase 2)
  * Replaces, per processing block of dsp/src/live/backend/processor.py:177-206 and :349-369:

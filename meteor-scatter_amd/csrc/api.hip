@@ -286,36 +286,61 @@ int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches
 }
 
 // ------------------------------------------------------------------ STFT plan
-int msd_stft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float *window, double scale,
-                         msd_stft_plan **out) {
-    if (!ctx || !window || !out) return fail(MSD_ERR_INVALID, "msd_stft_plan_create: null");
+}  // extern "C"
+namespace {
+bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
+
+// shared by the float32 and float64 plan constructors: window (nperseg values) and the
+// twiddles of an nfft-point real FFT, in the plan's precision
+int stft_plan_make(msd_ctx *ctx, int32_t nperseg, int32_t nfft, int32_t hop, const float *w32, const double *w64,
+                   double scale, int precision, msd_stft_plan **out) {
     *out = nullptr;
-    if (nperseg != 256 && nperseg != 512 && nperseg != 1024 && nperseg != 2048)
-        return fail(MSD_ERR_UNSUPPORTED, "stft: nperseg must be 256, 512, 1024 or 2048");
-    if (hop <= 0 || hop > nperseg) return fail(MSD_ERR_INVALID, "stft: need 0 < hop <= nperseg (noverlap < nperseg)");
+    if (nperseg < 1 || !pow2_in(nfft, 16, 16384) || nfft < nperseg)
+        return fail(MSD_ERR_UNSUPPORTED, "stft: need 1 <= nperseg <= nfft, nfft a power of two in [16, 16384]");
+    if (hop <= 0) return fail(MSD_ERR_INVALID, "stft: need hop = nperseg - noverlap > 0");
+    if (precision != MSD_F32 && precision != MSD_F64) return fail(MSD_ERR_INVALID, "stft: precision must be F32 or F64");
     DeviceGuard g(ctx->device);
     auto *p = new msd_stft_plan();
     p->ctx = ctx;
     p->nperseg = nperseg;
+    p->nfft = nfft;
     p->hop = hop;
-    p->M = nperseg / 2;
+    p->M = nfft / 2;
+    p->precision = precision;
     p->scale = scale;
     const int M = p->M;
-    std::vector<float2> tw(M), post(M + 1);
+    std::vector<double2> tw(M), post(M + 1);
     for (int m = 0; m < M; ++m) {
         const double a = -2.0 * M_PI * (double)m / (double)M;
-        tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+        tw[m] = make_double2(std::cos(a), std::sin(a));
     }
     for (int k = 0; k <= M; ++k) {
         const double a = -M_PI * (double)k / (double)M;
-        post[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+        post[k] = make_double2(std::cos(a), std::sin(a));
     }
-    hipError_t e = hipMalloc(&p->d_window, sizeof(float) * nperseg);
-    if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(float2) * M);
-    if (e == hipSuccess) e = hipMalloc(&p->d_post, sizeof(float2) * (M + 1));
-    if (e == hipSuccess) e = hipMemcpy(p->d_window, window, sizeof(float) * nperseg, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(float2) * M, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_post, post.data(), sizeof(float2) * (M + 1), hipMemcpyHostToDevice);
+    hipError_t e = hipSuccess;
+    if (precision == MSD_F32) {
+        std::vector<float2> tw32(M), post32(M + 1);
+        for (int m = 0; m < M; ++m) tw32[m] = make_float2((float)tw[m].x, (float)tw[m].y);
+        for (int k = 0; k <= M; ++k) post32[k] = make_float2((float)post[k].x, (float)post[k].y);
+        std::vector<float> win(nperseg);
+        for (int i = 0; i < nperseg; ++i) win[i] = w32 ? w32[i] : (float)w64[i];
+        e = hipMalloc(&p->d_window, sizeof(float) * nperseg);
+        if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(float2) * M);
+        if (e == hipSuccess) e = hipMalloc(&p->d_post, sizeof(float2) * (M + 1));
+        if (e == hipSuccess) e = hipMemcpy(p->d_window, win.data(), sizeof(float) * nperseg, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw32.data(), sizeof(float2) * M, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_post, post32.data(), sizeof(float2) * (M + 1), hipMemcpyHostToDevice);
+    } else {
+        std::vector<double> win(nperseg);
+        for (int i = 0; i < nperseg; ++i) win[i] = w64 ? w64[i] : (double)w32[i];
+        e = hipMalloc(&p->d_window64, sizeof(double) * nperseg);
+        if (e == hipSuccess) e = hipMalloc(&p->d_tw64, sizeof(double2) * M);
+        if (e == hipSuccess) e = hipMalloc(&p->d_post64, sizeof(double2) * (M + 1));
+        if (e == hipSuccess) e = hipMemcpy(p->d_window64, win.data(), sizeof(double) * nperseg, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_tw64, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p->d_post64, post.data(), sizeof(double2) * (M + 1), hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
         msd_stft_plan_destroy(p);
         return hip_fail(e, "stft plan upload");
@@ -324,37 +349,8 @@ int msd_stft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float
     return MSD_OK;
 }
 
-void msd_stft_plan_destroy(msd_stft_plan *p) {
-    if (!p) return;
-    DeviceGuard g(p->ctx->device);
-    hipStreamSynchronize(p->ctx->stream);
-    hipFree(p->d_window);
-    hipFree(p->d_tw);
-    hipFree(p->d_post);
-    delete p;
-}
-
-int64_t msd_stft_frames(const msd_stft_plan *p, int64_t n) {
-    if (!p || n < p->nperseg) return 0;
-    return (n - p->nperseg) / p->hop + 1;
-}
-
-int msd_stft_psd_dev(msd_stft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len,
-                     int64_t nfiles, int64_t max_frames, float *out, int64_t ld) {
-    if (!p || (nfiles > 0 && (!x || !off || !len || !out))) return fail(MSD_ERR_INVALID, "msd_stft_psd_dev: null");
-    if (ld % 32 != 0 || ld < max_frames || ld <= 0) return fail(MSD_ERR_INVALID, "stft: ld must be >= max_frames, a positive multiple of 32");
-    DeviceGuard g(p->ctx->device);
-    return launch_stft(p, x, dtype, off, len, nfiles, max_frames, out, ld);
-}
-
-int msd_stft_plan_set_detrend(msd_stft_plan *p, int detrend) {
-    if (!p || (detrend != 0 && detrend != 1)) return fail(MSD_ERR_INVALID, "msd_stft_plan_set_detrend: bad args");
-    p->detrend = detrend;
-    return MSD_OK;
-}
-
-int msd_stft_psd(msd_stft_plan *p, const void *x, int dtype, int64_t n, float *out, int64_t *frames) {
-    if (!p || !x || !out) return fail(MSD_ERR_INVALID, "msd_stft_psd: null");
+// host-buffer convenience path shared by msd_stft_psd / msd_stft_psd_f64: out dense [K][T]
+int stft_psd_host(msd_stft_plan *p, const void *x, int dtype, int64_t n, void *out, size_t out_es, int64_t *frames) {
     const size_t es = dtype_size(dtype);
     if (!es) return fail(MSD_ERR_INVALID, "msd_stft_psd: unknown dtype");
     const int64_t T = msd_stft_frames(p, n);
@@ -369,17 +365,90 @@ int msd_stft_psd(msd_stft_plan *p, const void *x, int dtype, int64_t n, float *o
     int rc;
     if ((rc = ctx_scratch(ctx, 0, xin, &dx))) return rc;
     if ((rc = ctx_scratch(ctx, 1, 64, &dmeta))) return rc;
-    if ((rc = ctx_scratch(ctx, 2, sizeof(float) * K * ld, &dout))) return rc;
+    if ((rc = ctx_scratch(ctx, 2, out_es * K * ld, &dout))) return rc;
     int64_t meta[2] = {0, n};
     MSD_HIP(hipMemcpyAsync(dx, x, (size_t)n * es, hipMemcpyHostToDevice, ctx->stream));
     MSD_HIP(hipMemcpyAsync(dmeta, meta, sizeof(meta), hipMemcpyHostToDevice, ctx->stream));
     const int64_t *doff = static_cast<const int64_t *>(dmeta);
-    rc = launch_stft(p, dx, dtype, doff, doff + 1, 1, T, static_cast<float *>(dout), ld);
+    rc = launch_stft(p, dx, dtype, doff, doff + 1, 1, T, dout, ld);
     if (rc) return rc;
-    MSD_HIP(hipMemcpy2DAsync(out, sizeof(float) * T, dout, sizeof(float) * ld, sizeof(float) * T, K,
-                             hipMemcpyDeviceToHost, ctx->stream));
+    MSD_HIP(hipMemcpy2DAsync(out, out_es * T, dout, out_es * ld, out_es * T, K, hipMemcpyDeviceToHost, ctx->stream));
     MSD_HIP(hipStreamSynchronize(ctx->stream));
     return MSD_OK;
+}
+}  // namespace
+extern "C" {
+
+int msd_stft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const float *window, double scale,
+                         msd_stft_plan **out) {
+    if (!ctx || !window || !out) return fail(MSD_ERR_INVALID, "msd_stft_plan_create: null");
+    *out = nullptr;
+    if (!pow2_in(nperseg, 16, 16384))
+        return fail(MSD_ERR_UNSUPPORTED, "stft: nperseg must be a power of two in [16, 16384] (nfft = nperseg)");
+    if (hop <= 0 || hop > nperseg) return fail(MSD_ERR_INVALID, "stft: need 0 < hop <= nperseg (noverlap < nperseg)");
+    return stft_plan_make(ctx, nperseg, nperseg, hop, window, nullptr, scale, MSD_F32, out);
+}
+
+int msd_stft_plan_create_ex(msd_ctx *ctx, int32_t nperseg, int32_t nfft, int32_t hop, const double *window,
+                            double scale, int precision, msd_stft_plan **out) {
+    if (!ctx || !window || !out) return fail(MSD_ERR_INVALID, "msd_stft_plan_create_ex: null");
+    return stft_plan_make(ctx, nperseg, nfft, hop, nullptr, window, scale, precision, out);
+}
+
+void msd_stft_plan_destroy(msd_stft_plan *p) {
+    if (!p) return;
+    DeviceGuard g(p->ctx->device);
+    hipStreamSynchronize(p->ctx->stream);
+    hipFree(p->d_window);
+    hipFree(p->d_tw);
+    hipFree(p->d_post);
+    hipFree(p->d_window64);
+    hipFree(p->d_tw64);
+    hipFree(p->d_post64);
+    delete p;
+}
+
+int64_t msd_stft_frames(const msd_stft_plan *p, int64_t n) {
+    if (!p || n < p->nperseg) return 0;
+    return (n - p->nperseg) / p->hop + 1;
+}
+
+int32_t msd_stft_bins(const msd_stft_plan *p) { return p ? p->M + 1 : 0; }
+
+int msd_stft_psd_dev(msd_stft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                     int64_t nfiles, int64_t max_frames, float *out, int64_t ld) {
+    if (!p || (nfiles > 0 && (!x || !off || !len || !out))) return fail(MSD_ERR_INVALID, "msd_stft_psd_dev: null");
+    if (p->precision != MSD_F32) return fail(MSD_ERR_INVALID, "msd_stft_psd_dev: float64 plan (use msd_stft_psd_f64_dev)");
+    if (ld % 32 != 0 || ld < max_frames || ld <= 0) return fail(MSD_ERR_INVALID, "stft: ld must be >= max_frames, a positive multiple of 32");
+    DeviceGuard g(p->ctx->device);
+    return launch_stft(p, x, dtype, off, len, nfiles, max_frames, out, ld);
+}
+
+int msd_stft_psd_f64_dev(msd_stft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                         int64_t nfiles, int64_t max_frames, double *out, int64_t ld) {
+    if (!p || (nfiles > 0 && (!x || !off || !len || !out))) return fail(MSD_ERR_INVALID, "msd_stft_psd_f64_dev: null");
+    if (p->precision != MSD_F64) return fail(MSD_ERR_INVALID, "msd_stft_psd_f64_dev: float32 plan (use msd_stft_psd_dev)");
+    if (ld % 32 != 0 || ld < max_frames || ld <= 0) return fail(MSD_ERR_INVALID, "stft: ld must be >= max_frames, a positive multiple of 32");
+    DeviceGuard g(p->ctx->device);
+    return launch_stft(p, x, dtype, off, len, nfiles, max_frames, out, ld);
+}
+
+int msd_stft_plan_set_detrend(msd_stft_plan *p, int detrend) {
+    if (!p || (detrend != 0 && detrend != 1)) return fail(MSD_ERR_INVALID, "msd_stft_plan_set_detrend: bad args");
+    p->detrend = detrend;
+    return MSD_OK;
+}
+
+int msd_stft_psd(msd_stft_plan *p, const void *x, int dtype, int64_t n, float *out, int64_t *frames) {
+    if (!p || !x || !out) return fail(MSD_ERR_INVALID, "msd_stft_psd: null");
+    if (p->precision != MSD_F32) return fail(MSD_ERR_INVALID, "msd_stft_psd: float64 plan (use msd_stft_psd_f64)");
+    return stft_psd_host(p, x, dtype, n, out, sizeof(float), frames);
+}
+
+int msd_stft_psd_f64(msd_stft_plan *p, const void *x, int dtype, int64_t n, double *out, int64_t *frames) {
+    if (!p || !x || !out) return fail(MSD_ERR_INVALID, "msd_stft_psd_f64: null");
+    if (p->precision != MSD_F64) return fail(MSD_ERR_INVALID, "msd_stft_psd_f64: float32 plan (use msd_stft_psd)");
+    return stft_psd_host(p, x, dtype, n, out, sizeof(double), frames);
 }
 
 // ------------------------------------------------------------- block-delta plan

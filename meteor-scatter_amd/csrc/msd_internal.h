@@ -55,12 +55,16 @@ struct msd_ctx {
 
 struct msd_stft_plan {
     msd_ctx *ctx = nullptr;
-    int nperseg = 0, hop = 0, M = 0;  // M = nperseg/2 complex points
-    int detrend = 1;                   // 1 constant (scipy), 0 none (matplotlib mlab)
+    int nperseg = 0, nfft = 0, hop = 0, M = 0;  // M = nfft/2 complex points, K = M + 1 bins
+    int detrend = 1;                             // 1 constant (scipy), 0 none (matplotlib mlab)
+    int precision = MSD_F32;                     // arithmetic and output type: MSD_F32 or MSD_F64
     double scale = 0;
-    float *d_window = nullptr;   // [nperseg]
+    float *d_window = nullptr;   // [nperseg]  (MSD_F32 plans)
     float2 *d_tw = nullptr;      // [M]    exp(-2*pi*i*m/M)
     float2 *d_post = nullptr;    // [M+1]  exp(-2*pi*i*k/(2M))
+    double *d_window64 = nullptr;  // the same three in float64 (MSD_F64 plans)
+    double2 *d_tw64 = nullptr;
+    double2 *d_post64 = nullptr;
 };
 
 struct msd_block_plan {
@@ -181,8 +185,11 @@ struct KernelTimer {
 int ctx_scratch(msd_ctx *ctx, int slot, size_t bytes, void **out);
 
 // launchers (defined in the kernel translation units)
+// out: float32 or float64 [nfiles][K][ld] by the plan's precision
 int launch_stft(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len, int64_t nfiles,
-                int64_t max_frames, float *out, int64_t ld);
+                int64_t max_frames, void *out, int64_t ld);
+int launch_stft_any(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                    int64_t nfiles, void *out, int64_t ld);
 int launch_stft1024(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                     int64_t nfiles, float *out, int64_t ld);
 int launch_block_delta(msd_block_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,

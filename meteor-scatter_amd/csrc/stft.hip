@@ -291,21 +291,27 @@ int launch_m(msd_stft_plan *p, const void *x, int dtype, const int64_t *off, con
 }  // namespace
 
 int launch_stft(msd_stft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len, int64_t nfiles,
-                int64_t max_frames, float *out, int64_t ld) {
+                int64_t max_frames, void *out, int64_t ld) {
     (void)max_frames;
     if (nfiles == 0) return MSD_OK;
     KernelTimer timer(p->ctx, K_STFT);
+    // the tiled float32 kernels cover nperseg = nfft in {256, ..., 2048} for u8 / i16 / f32;
+    // every other shape (and every float64 plan) goes to stft_any.hip
+    const bool tiled_dtype = dtype == MSD_U8 || dtype == MSD_I16 || dtype == MSD_F32;
+    if (p->precision != MSD_F32 || p->nfft != p->nperseg || !tiled_dtype)
+        return launch_stft_any(p, x, dtype, off, len, nfiles, out, ld);
     if (!p->ctx->force_generic) {
-        const int fast = launch_stft1024(p, x, dtype, off, len, nfiles, out, ld);
+        const int fast = launch_stft1024(p, x, dtype, off, len, nfiles, static_cast<float *>(out), ld);
         if (fast < 0) return fast;
         if (fast == 1) return MSD_OK;
     }
+    float *o = static_cast<float *>(out);
     switch (p->nperseg) {
-        case 256: return launch_m<128, 8, 32>(p, x, dtype, off, len, nfiles, out, ld);
-        case 512: return launch_m<256, 8, 32>(p, x, dtype, off, len, nfiles, out, ld);
-        case 1024: return launch_m<512, 8, 32>(p, x, dtype, off, len, nfiles, out, ld);
-        case 2048: return launch_m<1024, 4, 16>(p, x, dtype, off, len, nfiles, out, ld);
-        default: return fail(MSD_ERR_UNSUPPORTED, "stft: nperseg must be 256, 512, 1024 or 2048");
+        case 256: return launch_m<128, 8, 32>(p, x, dtype, off, len, nfiles, o, ld);
+        case 512: return launch_m<256, 8, 32>(p, x, dtype, off, len, nfiles, o, ld);
+        case 1024: return launch_m<512, 8, 32>(p, x, dtype, off, len, nfiles, o, ld);
+        case 2048: return launch_m<1024, 4, 16>(p, x, dtype, off, len, nfiles, o, ld);
+        default: return launch_stft_any(p, x, dtype, off, len, nfiles, out, ld);
     }
 }
 

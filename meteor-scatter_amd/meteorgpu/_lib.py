@@ -154,11 +154,16 @@ _SIGS = [
     ("msd_timing_reset", C.c_int, [_P]),
     ("msd_timing_get", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     ("msd_stft_plan_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_double, C.POINTER(_P)]),
+    ("msd_stft_plan_create_ex", C.c_int,
+     [_P, C.c_int32, C.c_int32, C.c_int32, _P, C.c_double, C.c_int, C.POINTER(_P)]),
     ("msd_stft_plan_destroy", None, [_P]),
+    ("msd_stft_bins", C.c_int32, [_P]),
     ("msd_stft_plan_set_detrend", C.c_int, [_P, C.c_int]),
     ("msd_stft_frames", C.c_int64, [_P, C.c_int64]),
     ("msd_stft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64]),
     ("msd_stft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
+    ("msd_stft_psd_f64_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64]),
+    ("msd_stft_psd_f64", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
     ("msd_block_plan_create", C.c_int,
      [_P, C.c_int64, C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
     ("msd_block_plan_destroy", None, [_P]),
@@ -177,6 +182,8 @@ _SIGS = [
     ("msd_cstft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P]),
     ("msd_cstft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
     ("msd_spec_band_sum_dev", C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
+    ("msd_spec_band_sum_f64_dev", C.c_int,
+     [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
     ("msd_welch_plan_create", C.c_int, [_P, C.POINTER(MsdWelchCfg), _P, C.POINTER(_P)]),
     ("msd_welch_plan_destroy", None, [_P]),
     ("msd_welch_bands_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64, _P]),
@@ -360,16 +367,32 @@ class DeviceBuffer:
 
 
 class StftPlan:
-    def __init__(self, ctx: Context, nperseg: int, hop: int, window: np.ndarray, scale: float):
+    """msd_stft_plan: nperseg-sample segments (hop apart) zero-padded to nfft (default nperseg),
+    float32 (``precision=np.float32``) or float64 arithmetic and output [K = nfft/2 + 1][T]."""
+
+    def __init__(self, ctx: Context, nperseg: int, hop: int, window: np.ndarray, scale: float, nfft: int | None = None,
+                 precision=np.float32):
         self.ctx = ctx
-        w = np.ascontiguousarray(window, dtype=np.float32)
-        if w.shape != (nperseg,):
-            raise ValueError("window length must equal nperseg")
+        nfft = int(nperseg) if nfft is None else int(nfft)
+        self.dtype = np.dtype(precision)
+        if self.dtype not in (np.float32, np.float64):
+            raise ValueError("precision must be float32 or float64")
         h = C.c_void_p()
-        check(ctx.lib.msd_stft_plan_create(ctx.h, int(nperseg), int(hop), ptr(w), float(scale), C.byref(h)))
+        if nfft == nperseg and self.dtype == np.float32:
+            w = np.ascontiguousarray(window, dtype=np.float32)
+            if w.shape != (nperseg,):
+                raise ValueError("window length must equal nperseg")
+            check(ctx.lib.msd_stft_plan_create(ctx.h, int(nperseg), int(hop), ptr(w), float(scale), C.byref(h)))
+        else:
+            w = np.ascontiguousarray(window, dtype=np.float64)
+            if w.shape != (nperseg,):
+                raise ValueError("window length must equal nperseg")
+            prec = MSD_F64 if self.dtype == np.float64 else MSD_F32
+            check(ctx.lib.msd_stft_plan_create_ex(ctx.h, int(nperseg), nfft, int(hop), ptr(w), float(scale), prec,
+                                                  C.byref(h)))
         self.h = h
-        self.nperseg, self.hop = int(nperseg), int(hop)
-        self.nbins = nperseg // 2 + 1
+        self.nperseg, self.hop, self.nfft = int(nperseg), int(hop), nfft
+        self.nbins = int(ctx.lib.msd_stft_bins(h))
 
     def close(self):
         if getattr(self, "h", None) and self.ctx.h:  # a plan outliving its context leaks, never crashes
@@ -392,16 +415,17 @@ class StftPlan:
     def run(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x)
         T = self.frames(x.shape[0])
-        out = np.empty((self.nbins, T), dtype=np.float32)
+        out = np.empty((self.nbins, T), dtype=self.dtype)
         t = C.c_int64(0)
-        check(self.ctx.lib.msd_stft_psd(self.h, ptr(x), dtype_code(x.dtype), int(x.shape[0]), ptr(out),
-                                        C.byref(t)))
+        fn = self.ctx.lib.msd_stft_psd_f64 if self.dtype == np.float64 else self.ctx.lib.msd_stft_psd
+        check(fn(self.h, ptr(x), dtype_code(x.dtype), int(x.shape[0]), ptr(out), C.byref(t)))
         return out
 
     def run_dev(self, x: DeviceBuffer, dtype, off: DeviceBuffer, length: DeviceBuffer, nfiles: int,
                 max_frames: int, out: DeviceBuffer, ld: int):
-        check(self.ctx.lib.msd_stft_psd_dev(self.h, x.ptr, dtype_code(dtype), off.ptr, length.ptr, int(nfiles),
-                                            int(max_frames), out.ptr, int(ld)))
+        fn = self.ctx.lib.msd_stft_psd_f64_dev if self.dtype == np.float64 else self.ctx.lib.msd_stft_psd_dev
+        check(fn(self.h, x.ptr, dtype_code(dtype), off.ptr, length.ptr, int(nfiles), int(max_frames), out.ptr,
+                 int(ld)))
 
 
 class BlockPlan:

@@ -57,8 +57,11 @@ class BatchPipeline:
         self.block_size = int(fs * block_duration_sec)
         self.block_sec = block_duration_sec
         L = min(self.block_size, nfft)
+        self.band_bins, self.noise_bins = band_bins(nfft, fs, freq_band), band_bins(nfft, fs, noise_band)
         self.blocks = _lib.BlockPlan(self.stage_ctx, self.block_size, nfft, hanning_sym(self.block_size)[:L],
-                                     band_bins(nfft, fs, freq_band), band_bins(nfft, fs, noise_band))
+                                     self.band_bins, self.noise_bins)
+        self.nfft, self.L, self.k_std = nfft, L, float(threshold_std_factor)
+        self.xmax = np.zeros(self.nfiles)  # max |x| per file (near-tie bound, margin.py)
         self.nb = self.n // self.block_size
         self.ld_b = max(1, self.nb)
         bs = block_duration_sec
@@ -76,6 +79,8 @@ class BatchPipeline:
         self.d_nb = ctx.alloc(F * 8)
         self.d_spec = ctx.alloc(F * self.K * self.ld_t * 4) if with_spectrogram else None
         self.d_delta = ctx.alloc(F * self.ld_b * 8)
+        self.d_band = ctx.alloc(F * self.ld_b * 8)   # band / noise dB per block: the near-tie bound
+        self.d_noise = ctx.alloc(F * self.ld_b * 8)
         self.d_thr = ctx.alloc(F * self.ld_b * 8)
         self.d_dets = ctx.alloc(F * self.cap * _lib.DET_DTYPE.itemsize)
         self.d_counts = ctx.alloc(F * 8)
@@ -97,6 +102,7 @@ class BatchPipeline:
         if x.shape != (self.n,):
             raise ValueError(f"file {i}: expected {self.n} samples")
         self.d_x.upload(x, byte_offset=i * self.n_pad * self.dtype.itemsize)
+        self.xmax[i] = float(np.max(np.abs(x.astype(np.float64)))) if x.size else 0.0
 
     def set_start_times(self, file_start_us: np.ndarray, base_us: int):
         self.d_start_us.upload(np.ascontiguousarray(file_start_us, dtype=np.int64))
@@ -117,7 +123,7 @@ class BatchPipeline:
             _lib.check(lib.msd_memset_dev(h, self.d_hist.ptr, 0, self.d_hist.nbytes))
         if self.with_spectrogram:
             self.stft.run_dev(x, self.dtype, self.d_off, self.d_len, self.nfiles, self.T, self.d_spec, self.ld_t)
-        self.blocks.run_dev(x, self.dtype, self.d_off, self.d_len, self.nfiles, self.nb, None, None,
+        self.blocks.run_dev(x, self.dtype, self.d_off, self.d_len, self.nfiles, self.nb, self.d_band, self.d_noise,
                             self.d_delta, self.ld_b)
         _lib.check(lib.msd_detect_dev(h, self.d_delta.ptr, self.d_nb.ptr, self.nfiles, self.ld_b, self.cfg,
                                       self.d_dets.ptr, self.cap, self.d_counts.ptr, self.d_thr.ptr,
@@ -154,7 +160,28 @@ class BatchPipeline:
         self.d_status.download(status)
         margin = np.empty(self.nfiles, np.float64)
         self.d_margin.download(margin)
+        self._near_ties(margin)
         return [dets[i, : min(counts[i], self.cap)] for i in range(self.nfiles)], counts, status, margin
+
+    def _near_ties(self, margin: np.ndarray):
+        """Per file: the decision bound (margin.py) and whether min |delta - thr| is within it
+        (``self.decision_bounds``, ``self.near_tie``); one NearTieWarning names the files."""
+        from . import margin as M
+        band = np.empty((self.nfiles, self.ld_b), np.float64)
+        noise = np.empty((self.nfiles, self.ld_b), np.float64)
+        self.d_band.download(band)
+        self.d_noise.download(noise)
+        win = hanning_sym(self.block_size)[: self.L]
+        self.decision_bounds = np.array([
+            M.decision_bound(M.delta_error_bound(band[i, : self.nb], noise[i, : self.nb], nfft=self.nfft, L=self.L,
+                                                 window=win, xmax=self.xmax[i], band=self.band_bins,
+                                                 noise=self.noise_bins), self.k_std)
+            for i in range(self.nfiles)])
+        self.near_tie = np.isfinite(margin) & (margin <= self.decision_bounds)
+        if self.near_tie.any():
+            idx = np.nonzero(self.near_tie)[0]
+            M.check(float(margin[idx[0]]), float(self.decision_bounds[idx[0]]),
+                    f"{idx.size} file(s) (first: {int(idx[0])}): ")
 
     def hour_counts(self) -> np.ndarray:
         out = np.empty(max(1, self.nbuckets), np.int64)

@@ -10,10 +10,12 @@ work runs on the GPU through libmsdsp (no CPU fallback).  Lower-level pieces:
 * ``write_csv`` / ``write_audacity_labels`` — main.py:640-658 / 630-638
 * ``count_per_hour`` — main.py:687-696 (Counter over utc_start hours)
 
-The per-detection spectrogram + PSD export (``disable_show_and_write=False``,
-main.py:721-806) draws GPU arrays with matplotlib (``figures.py``).  Not implemented:
-the whole-file debug figures (``debug_plot_*``); asking for them raises
-``NotImplementedError`` rather than silently skipping.
+The reference's figures are drawn from GPU arrays with matplotlib / plotly (``figures.py``):
+the per-detection spectrogram + PSD export (``disable_show_and_write=False``,
+main.py:721-806) and the debug figures ``debug_plot_whole`` (main.py:278-306),
+``debug_plot_config`` (:324-350), ``debug_plot_output`` (:531-565, :660-716) and
+``debug_plot_output_interactive`` (:567-624).  They are shown as in the reference; the
+keyword-only ``figure_dir`` also saves them (headless runs).
 """
 from __future__ import annotations
 
@@ -26,6 +28,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib, wav
+from . import margin as margin_mod
 
 
 @dataclass
@@ -50,6 +53,10 @@ class ProcResult:
     block_size: int
     num_blocks: int
     min_margin: float = field(default=float("nan"))
+    # near-tie guard (margin.py): |delta - thr| at or below decision_bound can flip a decision
+    # against the float64 numpy reference; near_tie says whether min_margin is that close
+    decision_bound: float = field(default=float("nan"))
+    near_tie: bool = False
 
 
 _CTX: dict[int, _lib.Context] = {}
@@ -211,7 +218,12 @@ def spectrogram(x, fs=1.0, window="hann", nperseg=None, noverlap=None, nfft=None
                 return_onesided=True, scaling="density", axis=-1, mode="psd", device: int = 0):
     """scipy.signal.spectrogram for the configuration the reference uses (main.py:52-54, :132-133):
     periodic Hann, constant detrend, one-sided density PSD of a real 1-D signal.
-    Returns (f, t, Sxx) with Sxx float32 [nperseg//2+1, T] for u8/i16/f32 input."""
+    As scipy: nperseg defaults to 256 and shrinks (with scipy's warning) to a shorter input;
+    noverlap defaults to nperseg // 8; nfft >= nperseg zero-pads each segment.  nfft must be a
+    power of two in [16, 16384].  Returns (f, t, Sxx) with Sxx [nfft//2+1, T] in scipy's output
+    precision: float32 for u8 / i16 / f32 input, float64 for i32 / i64 / f64 (computed in
+    float64 then)."""
+    import warnings
     x = np.asarray(x)
     if isinstance(window, tuple):
         window = window[0] if len(window) == 1 else window
@@ -219,34 +231,43 @@ def spectrogram(x, fs=1.0, window="hann", nperseg=None, noverlap=None, nfft=None
         raise NotImplementedError("only window='hann' is implemented")
     if x.ndim != 1 or axis not in (-1, 0):
         raise NotImplementedError("only 1-D input is implemented")
-    if nperseg is None:
-        nperseg = 256
-    nperseg = int(nperseg)
-    if noverlap is None:
-        noverlap = nperseg // 8  # scipy.signal.spectrogram default
-    noverlap = int(noverlap)
-    if nfft is not None and int(nfft) != nperseg:
-        raise NotImplementedError("nfft != nperseg (zero-padded frames) is not implemented")
     if detrend != "constant" or not return_onesided or scaling != "density" or mode != "psd":
         raise NotImplementedError("only detrend='constant', one-sided, density, mode='psd' are implemented")
     if np.iscomplexobj(x):
-        raise NotImplementedError("complex (two-sided) input is not implemented yet")
-    if x.shape[0] < nperseg:
-        raise NotImplementedError("input shorter than nperseg (scipy shrinks nperseg) is not implemented")
+        raise NotImplementedError("complex (two-sided) input: use meteorgpu.iq")
+    if x.dtype == np.int64:
+        x = x.astype(np.float64)  # same values up to 2^53; scipy computes these in float64 too
+    n = x.shape[0]
+    nperseg = 256 if nperseg is None else int(nperseg)
+    if nperseg < 1:
+        raise ValueError("nperseg must be a positive integer")
+    if nperseg > n:  # scipy _triage_segments
+        warnings.warn(f"nperseg = {nperseg:d} is greater than input length  = {n:d}, using nperseg = {n:d}",
+                      stacklevel=2)
+        nperseg = n
+    noverlap = nperseg // 8 if noverlap is None else int(noverlap)
     if noverlap >= nperseg:
         raise ValueError("noverlap must be less than nperseg.")
+    nfft = nperseg if nfft is None else int(nfft)
+    if nfft < nperseg:
+        raise ValueError("nfft must be greater than or equal to nperseg.")
+    if nfft < 16 or nfft > 16384 or nfft & (nfft - 1):
+        raise NotImplementedError("nfft must be a power of two in [16, 16384]")
     hop = nperseg - noverlap
+    double = x.dtype in (np.int32, np.float64)  # np.result_type(x, np.complex64) is complex128
     w64 = hann_periodic(nperseg)
-    wc = w64.astype(np.complex64)  # _spectral_helper casts the window to the output dtype
-    scale = 1.0 / (fs * (wc * wc).sum())
-    w32 = wc.real.astype(np.float32)
-    plan = _lib.StftPlan(context(device), nperseg, hop, w32, float(np.real(scale)))
+    wc = w64.astype(np.complex128 if double else np.complex64)  # _spectral_helper casts the window
+    scale = float(np.real(1.0 / (fs * (wc * wc).sum())))
+    if x.dtype not in (np.uint8, np.int16, np.int32, np.float32, np.float64):
+        x = x.astype(np.float64)
+    plan = _lib.StftPlan(context(device), nperseg, hop, wc.real, scale, nfft=nfft,
+                         precision=np.float64 if double else np.float32)
     try:
         sxx = plan.run(np.ascontiguousarray(x))
     finally:
         plan.close()
-    freqs = np.fft.rfftfreq(nperseg, 1 / fs)
-    time = np.arange(nperseg / 2, x.shape[-1] - nperseg / 2 + 1, nperseg - noverlap) / float(fs)
+    freqs = np.fft.rfftfreq(nfft, 1 / fs)
+    time = np.arange(nperseg / 2, n - nperseg / 2 + 1, nperseg - noverlap) / float(fs)
     return freqs, time, sxx
 
 
@@ -276,11 +297,13 @@ def proc_wav_file(file_path,
                   *,
                   required_sample_rate=6000,
                   device=0,
-                  verbose=True):
+                  verbose=True,
+                  figure_dir=None):
     """GPU drop-in for dsp/src/main.py:207-806 (same arguments, asserts and outputs).
 
     ``required_sample_rate`` keeps the reference's ``assert fs == 6000`` (main.py:267);
-    pass ``None`` to accept any rate (e.g. the 48 kHz configurations)."""
+    pass ``None`` to accept any rate (e.g. the 48 kHz configurations).  ``figure_dir``: also
+    save every debug figure there (PNG; plotly figures as HTML instead of fig.show())."""
     say = print if verbose else (lambda *a, **k: None)
     assert os.path.exists(file_path), f"File does not exist: {file_path}"
     if outfile_path is not None:
@@ -295,10 +318,6 @@ def proc_wav_file(file_path,
     if out_csv_file is not None:
         assert os.path.exists(os.path.dirname(out_csv_file)), \
             f"Output directory does not exist: {os.path.dirname(out_csv_file)}"
-    if debug_plot_whole or debug_plot_config or debug_plot_output or debug_plot_output_interactive:
-        raise NotImplementedError("the debug_plot_* figures are not part of the GPU drop-in "
-                                  "(the per-detection export, disable_show_and_write=False, is)")
-
     wav_sample_rate, wav_data = wav.read(file_path)
 
     if wav_start_sec is not None or wav_end_sec is not None:
@@ -318,6 +337,12 @@ def proc_wav_file(file_path,
     assert len(wav_data.shape) == 1, f"Data must be mono or stereo, but got shape {wav_data.shape}"
 
     say("Wav duration [sec]:", len(wav_data) / wav_sample_rate)
+    if debug_plot_whole or debug_plot_config or debug_plot_output or debug_plot_output_interactive:
+        from . import figures
+    if debug_plot_whole:  # main.py:278-306
+        figures.debug_whole(wav_data, wav_sample_rate, freq_band, noise_band, figure_dir, device=device)
+    if debug_plot_config:  # main.py:324-350
+        figures.debug_config(wav_data, wav_sample_rate, freq_band, noise_band, figure_dir, device=device)
     res = process_samples(wav_data, wav_sample_rate, block_duration_sec, freq_band, noise_band, n_fft,
                           threshold_std_factor, wav_start_date_time=wav_start_date_time,
                           flag_adaptive_threshold=flag_adaptive_threshold,
@@ -327,6 +352,13 @@ def proc_wav_file(file_path,
                           threshold_fixed_init_duration_sec=threshold_fixed_init_duration_sec,
                           device=device, verbose=verbose)
 
+    times = np.arange(res.num_blocks) * block_duration_sec  # main.py:529
+    if debug_plot_output:  # main.py:531-565
+        figures.debug_output_delta(times, res.delta_power, res.thresholds, res.detections, flag_adaptive_threshold,
+                                   figure_dir)
+    if debug_plot_output_interactive:  # main.py:567-624
+        figures.debug_output_interactive(times, res.band_power, res.noise_power, res.delta_power, res.thresholds,
+                                         res.detections, freq_band, noise_band, figure_dir)
     for det in res.detections:
         say(f"Detection from {det.t_start:.2f} to {det.t_stop:.2f} seconds, dB: {det.dB:.2f} dB, "
             f"duration: {det.dur_s:.2f} seconds UTC_START: {det.utc_start}, UTC_STOP: {det.utc_stop}")
@@ -337,6 +369,9 @@ def proc_wav_file(file_path,
     if out_csv_file is not None:
         write_csv(res.detections, out_csv_file)
         say("Wrote Items", len(res.detections), "to CSV file:", out_csv_file)
+    if debug_plot_output:  # main.py:660-716: histograms, then the per-hour map
+        figures.debug_output_hists(res.detections, figure_dir)
+        figures.debug_time_map(res.detections, figure_dir)
     if not disable_show_and_write:  # main.py:721-806: per-detection spectrogram + PSD figures
         from .figures import export_detections
         export_detections(res.detections, wav_data, wav_sample_rate, freq_band, outfile_path, device=device)
@@ -367,6 +402,11 @@ def process_samples(wav_data, wav_sample_rate, block_duration_sec, freq_band, no
 
     band, noise, delta, _ = block_powers(wav_data, wav_sample_rate, block_duration_sec, freq_band, noise_band,
                                          n_fft, device=device)
+    L = min(block_size, nfft)
+    xmax = float(np.max(np.abs(np.asarray(wav_data, dtype=np.float64)))) if len(wav_data) else 0.0
+    err = margin_mod.delta_error_bound(band, noise, nfft=nfft, L=L, window=hanning_sym(block_size)[:L], xmax=xmax,
+                                       band=band_bins(nfft, wav_sample_rate, freq_band),
+                                       noise=band_bins(nfft, wav_sample_rate, noise_band))
     assert len(band) == num_blocks and len(noise) == num_blocks
     if not flag_adaptive_threshold:
         dets, thr, margin = get_detections(delta, threshold_std_factor, block_duration_sec, wav_start_date_time,
@@ -377,4 +417,6 @@ def process_samples(wav_data, wav_sample_rate, block_duration_sec, freq_band, no
             delta, threshold_std_factor, block_duration_sec, threshold_estimation_window_sec,
             threshold_freeze_before_detection_sec, threshold_freeze_after_detection_sec,
             threshold_fixed_init_duration_sec, wav_start_date_time, device=device, return_margin=True)
-    return ProcResult(dets, thr, band, noise, delta, block_size, num_blocks, margin)
+    bound = margin_mod.decision_bound(err, threshold_std_factor)
+    near = margin_mod.check(margin, bound)
+    return ProcResult(dets, thr, band, noise, delta, block_size, num_blocks, margin, bound, near)

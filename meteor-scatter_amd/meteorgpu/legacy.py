@@ -3,8 +3,9 @@ meteor_detect_class/prime_detection.py:65-91, on the GPU.
 
 ``specgram`` mirrors ``matplotlib.mlab.specgram`` (what ``plt.specgram`` computes) for a
 real 1-D signal: symmetric Hann (``window_hanning``), no detrend, one-sided PSD with the
-DC / Nyquist rows undoubled, ``/Fs/sum(w**2)`` — on libmsdsp's STFT kernels (float32
-arithmetic; the reference computes in float64, agreement ~1e-6 relative, tested).
+DC / Nyquist rows undoubled, ``/Fs/sum(w**2)``, zero padding to NFFT for a signal shorter than
+NFFT — on libmsdsp's float64 STFT (``stft_any.hip``), the precision mlab computes in
+(mlab.py:299-356); agreement with mlab is at the 1e-12 level (tested).
 ``noise_floor`` adds the band power over the noise band's rows and all frames
 (``np.sum(Pxx[noise_band])``, a device reduction) and the reference's colour floor
 ``vmin = 10*log10(band_power/bandwidth) / (40/23) + C_MS_SPEC_CUT_FACTOR``.
@@ -37,43 +38,45 @@ class SpecgramPlan:
 
     def __init__(self, n: int, NFFT: int = 256, Fs: float = 2, noverlap: int = 128, dtype=np.int16,
                  device: int = 0):
-        if NFFT not in (256, 512, 1024, 2048):
-            raise NotImplementedError("NFFT must be 256, 512, 1024 or 2048 (the STFT kernels' sizes)")
+        NFFT = int(NFFT)
+        if NFFT < 16 or NFFT > 16384 or NFFT & (NFFT - 1):
+            raise NotImplementedError("NFFT must be a power of two in [16, 16384]")
         if not 0 <= noverlap < NFFT:
             raise ValueError("noverlap must be less than NFFT")
-        if n < NFFT:
-            raise NotImplementedError("signals shorter than NFFT (mlab zero-pads them) are not supported")
         self.ctx = context(device)
-        self.n, self.NFFT, self.Fs, self.noverlap = int(n), int(NFFT), float(Fs), int(noverlap)
+        self.n, self.NFFT, self.Fs, self.noverlap = int(n), NFFT, float(Fs), int(noverlap)
         self.dtype = np.dtype(dtype)
+        # mlab._spectral_helper: a signal shorter than NFFT is zero-padded to NFFT (one frame)
+        self.n_dev = max(self.n, NFFT)
         w = hanning_sym(NFFT)                   # window_hanning(np.ones(NFFT)) = np.hanning(NFFT)
         scale = 1.0 / (Fs * (w ** 2).sum())     # result /= Fs; result /= (window**2).sum()
-        self.plan = _lib.StftPlan(self.ctx, NFFT, NFFT - noverlap, w.astype(np.float32), scale)
+        self.plan = _lib.StftPlan(self.ctx, NFFT, NFFT - noverlap, w, scale, nfft=NFFT, precision=np.float64)
         self.plan.set_detrend(False)            # mlab default detrend_none
         self.K = NFFT // 2 + 1
-        self.T = self.plan.frames(self.n)
+        self.T = self.plan.frames(self.n_dev)
         self.ld = max(32, (self.T + 31) // 32 * 32)
-        self.freqs, self.t = _freqs_times(self.n, NFFT, Fs, noverlap)
+        self.freqs, self.t = _freqs_times(self.n_dev, NFFT, Fs, noverlap)
         es = self.dtype.itemsize
-        self.d_x = self.ctx.alloc((self.n + 7) // 8 * 8 * es)
+        self.d_x = self.ctx.alloc((self.n_dev + 7) // 8 * 8 * es)
+        self.d_x.memset(0)
         self.d_off = self.ctx.alloc(8)
         self.d_len = self.ctx.alloc(8)
         self.d_off.upload(np.zeros(1, np.int64))
-        self.d_len.upload(np.array([self.n], np.int64))
-        self.d_spec = self.ctx.alloc(self.K * self.ld * 4)
+        self.d_len.upload(np.array([self.n_dev], np.int64))
+        self.d_spec = self.ctx.alloc(self.K * self.ld * 8)
         self.d_sum = self.ctx.alloc(8)
 
     def run(self, x: np.ndarray):
         x = np.ascontiguousarray(x, dtype=self.dtype)
         if x.shape != (self.n,):
             raise ValueError("signal length differs from the plan's")
-        self.d_x.upload(x)
+        self.d_x.upload(x)  # the zero tail up to NFFT (short signals) was set at construction
         self.plan.run_dev(self.d_x, self.dtype, self.d_off, self.d_len, 1, self.T, self.d_spec, self.ld)
 
     def spectrogram(self) -> np.ndarray:
-        out = np.empty((self.K, self.ld), np.float32)
+        out = np.empty((self.K, self.ld), np.float64)
         self.d_spec.download(out)
-        return out[:, : self.T].astype(np.float64)
+        return out[:, : self.T]
 
     def band_power(self, lo_hz: float, hi_hz: float) -> tuple[float, int]:
         """(np.sum(Pxx[(freqs >= lo) & (freqs <= hi)]), number of bins) on the device."""
@@ -81,8 +84,8 @@ class SpecgramPlan:
         if idx.size == 0:
             return 0.0, 0
         assert idx[-1] - idx[0] + 1 == idx.size
-        _lib.check(self.ctx.lib.msd_spec_band_sum_dev(self.ctx.h, self.d_spec.ptr, 1, self.K, self.T, self.ld,
-                                                      int(idx[0]), int(idx[-1]), self.d_sum.ptr))
+        _lib.check(self.ctx.lib.msd_spec_band_sum_f64_dev(self.ctx.h, self.d_spec.ptr, 1, self.K, self.T, self.ld,
+                                                          int(idx[0]), int(idx[-1]), self.d_sum.ptr))
         s = np.empty(1, np.float64)
         self.d_sum.download(s)
         return float(s[0]), int(idx.size)
@@ -97,7 +100,7 @@ def specgram(x, NFFT=None, Fs=None, noverlap=None, device: int = 0):
     NFFT = 256 if NFFT is None else int(NFFT)
     Fs = 2 if Fs is None else Fs
     noverlap = 128 if noverlap is None else int(noverlap)
-    dt = x.dtype if x.dtype in (np.int16, np.uint8, np.float32) else np.float32
+    dt = x.dtype if x.dtype in (np.int16, np.int32, np.uint8, np.float32, np.float64) else np.float64
     p = SpecgramPlan(len(x), NFFT, Fs, noverlap, dtype=dt, device=device)
     p.run(x.astype(dt, copy=False))
     return p.spectrogram(), p.freqs, p.t
@@ -107,7 +110,7 @@ def noise_floor(x, fs, NFFT=2048, lower_freq=250, upper_freq=800, cut_factor=C_M
     """prime_detection.py:65-91 without the figure: returns (Pxx, freqs, bins, vmin,
     power_density_db_hz) for ``plt.specgram(x, Fs=fs, NFFT=NFFT, noverlap=NFFT // 2)``."""
     x = np.asarray(x)
-    dt = x.dtype if x.dtype in (np.int16, np.uint8, np.float32) else np.float32
+    dt = x.dtype if x.dtype in (np.int16, np.int32, np.uint8, np.float32, np.float64) else np.float64
     p = SpecgramPlan(len(x), NFFT, fs, NFFT // 2, dtype=dt, device=device)
     p.run(x.astype(dt, copy=False))
     band_power, nbins = p.band_power(lower_freq, upper_freq)

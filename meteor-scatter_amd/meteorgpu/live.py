@@ -3,10 +3,12 @@
 
 The per-block Welch PSD band powers (a8, processor.py:206 and :349-369) and the state
 machine (a9, processor.py:391-507) run on the GPU through libmsdsp
-(``msd_welch_bands*``, ``msd_live_detect*``); there is no CPU fallback.  The plots
-(``enable_ui_plots``) and the per-detection spectrogram image export
-(``ConfigSpecExport.output_dir``) are figures, not the data path: asking for them raises
-``NotImplementedError``.
+(``msd_welch_bands*``, ``msd_live_detect*``); there is no CPU fallback.  The per-meteor
+waterfall export (``ConfigSpecExport.output_dir``, processor.py:295-343) draws per-block Welch
+PSD rows computed on the GPU (``msd_welch_psd``: only the rows the image shows, plus the
+full rows of the initialisation blocks that set its colour range).  The live UI animation
+(``enable_ui_plots``, an interactive matplotlib window) is not part of the drop-in: asking for
+it raises ``NotImplementedError``.
 
 Lower-level pieces: ``welch_band_db`` (band dB rows of one signal), ``live_detect`` (the
 state machine over band dB rows), ``LiveBatch`` (many recordings resident in HBM).
@@ -203,9 +205,9 @@ def wav_file_process(wav_file_path: str,
     if config_spec_export.output_dir != "":
         assert os.path.exists(config_spec_export.output_dir), \
             f"Output Directory not found: {config_spec_export.output_dir}"
-    if config_visualization.enable_ui_plots or config_spec_export.output_dir != "":
-        raise NotImplementedError("UI plots and the spectrogram image export are not part of the GPU drop-in; "
-                                  "set enable_ui_plots=False and output_dir=''")
+    if config_visualization.enable_ui_plots:
+        raise NotImplementedError("the live UI animation (enable_ui_plots) is not part of the GPU drop-in; "
+                                  "set enable_ui_plots=False (the spectrogram export, output_dir, is)")
     file_sample_rate, data = wav.read(wav_file_path)
     if required_sample_rate is not None:
         assert file_sample_rate == required_sample_rate, f"Invalid Sample Rate: {file_sample_rate}"
@@ -217,12 +219,138 @@ def wav_file_process(wav_file_path: str,
     if data.ndim > 1:
         print("WARNING: Multichannel file detected. Using first channel only.")
         data = data[:, 0]
+    _print_config(config_detection, config_visualization)
     x, sample_scale = _device_samples(np.ascontiguousarray(data))
+    block_size = int(config_detection.proc_block_sec * file_sample_rate)
+    print()
+    print("###############")
+    print("Prepare Wav")
+    print("###############")
+    print("File Samplerate: ", file_sample_rate)
+    print("File Blockgröße: ", block_size)
+    print("File Dauer: ", len(x) / file_sample_rate)
+    print()
+    print("###############")
+    print("Process Loop")
+    print("###############")
     bdb = welch_band_db(x, file_sample_rate, config_detection, sample_scale, device)
     meteors, _, _ = live_detect(bdb, file_sample_rate, config_detection, device)
     for i, m in enumerate(meteors):
         print("Detected Meteor:", m, "Now Detected Meteors:", i + 1)
+    not_exported = list(meteors)
+    if config_spec_export.output_dir != "":
+        _, not_exported = export_meteor_specs(x, sample_scale, file_sample_rate, bdb.shape[1], meteors,
+                                              config_detection, config_visualization, config_spec_export, device)
+    if len(not_exported) != 0:  # processor.py:539-543
+        print("Detected Meteors not exported: ", len(not_exported))
+        for t in not_exported:
+            print(t)
     return meteors
+
+
+def _print_config(cd: ConfigDetection, cv: ConfigVisualization):
+    """processor.py:25-59: the band edges and window sizes it prints before processing."""
+    (ms0, ms1), (n10, n11), (n20, n21) = band_edges(cd)
+    print()
+    print("###############")
+    print("Init Config")
+    print("###############")
+    print("Freq MS Min: ", ms0)
+    print("Freq MS Max: ", ms1)
+    print("Freq Noise 1 Min: ", n10)
+    print("Freq Noise 1 Max: ", n11)
+    print("Freq Noise 2 Min: ", n20)
+    print("Freq Noise 2 Max: ", n21)
+    print("Waterfall Win Size: ", int(cv.max_range_sec / cd.proc_block_sec))
+    print("Avg Win Size: ", int(cd.avg_win_sec / cd.proc_block_sec))
+
+
+def block_psd_rows(x: np.ndarray, sample_scale: float, fs, cfg: ConfigDetection, b0: int, b1: int, k0: int, k1: int,
+                   device: int = 0) -> np.ndarray:
+    """Welch PSD of blocks [b0, b1), bins [k0, k1], float64 [b1-b0][k1-k0+1]: the rows of
+    processor.py:206's ``welch(block, fs, nfft=n_fft)`` the waterfall image needs (GPU)."""
+    c, win = welch_cfg(fs, cfg, sample_scale)
+    c.nbands = 1
+    c.band_lo[0], c.band_hi[0] = int(k0), int(k1)
+    bs = int(c.block_size)
+    plan = _lib.WelchPlan(context(device), c, win)
+    try:
+        return plan.psd(np.ascontiguousarray(x[b0 * bs: b1 * bs]), k1 - k0 + 1)
+    finally:
+        plan.close()
+
+
+def export_meteor_specs(x: np.ndarray, sample_scale: float, fs, nb: int, meteors, cd: ConfigDetection,
+                        cv: ConfigVisualization, ce: ConfigSpecExport, device: int = 0):
+    """processor.py:295-343: each meteor is exported at the first block after the one that closed
+    it whose waterfall window (the block-end times of the last max_range_sec / proc_block_sec
+    blocks) contains [start - time_before, stop + time_after]; the image is that window's
+    PSD rows in dB (imshow, colour range = the mean PSD dB of the initialisation blocks -
+    wf_offset_vmin .. + wf_offset_vmax), cropped to those times and to signal_freq +-
+    limit_freq_offset_wf2_and_export, saved as output_dir + spec_{start:.2f}_{stop:.2f}.jpg.
+    Only the rows inside the crop (one more on each side) are computed: imshow with the
+    matching sub-extent draws the same picture.  Returns (paths, meteors never exported)."""
+    import matplotlib.pyplot as plt
+    bs = int(cd.proc_block_sec * fs)
+    W = int(cv.max_range_sec / cd.proc_block_sec)  # processor.py:57
+    nfft = int(cd.n_fft)
+    K = nfft // 2 + 1
+    freqs = np.fft.rfftfreq(nfft, 1 / fs)
+    end = lambda b: (b * bs + bs) / fs  # noqa: E731  block_end_elapsed_sec
+    start_of = lambda b: (b * bs) / fs  # noqa: E731
+    # the block that ends the initialisation (processor.py:452-455) and the colour range
+    b_init = next((b for b in range(nb) if start_of(b) >= cd.init_detection_wait_sec), None)
+    mean_init = None
+    if b_init is not None:
+        full = block_psd_rows(x, sample_scale, fs, cd, 0, b_init + 1, 0, K - 1, device)
+        with np.errstate(divide="ignore"):
+            mean_init = np.mean([np.mean(10 * np.log10(r)) for r in full])
+    lo_f = cd.signal_freq - cv.limit_freq_offset_wf2_and_export
+    hi_f = cd.signal_freq + cv.limit_freq_offset_wf2_and_export
+    h = (freqs[-1] - freqs[0]) / K  # imshow row height of the full image
+    k0 = max(0, int(np.floor((lo_f - freqs[0]) / h)) - 1)
+    k1 = min(K - 1, int(np.ceil((hi_f - freqs[0]) / h)) + 1)
+    ms0, ms1 = band_edges(cd)[0]
+    paths, pending = [], []
+    for m in meteors:
+        c = int(round(m.time_stop * fs / bs))  # the block that closed the meteor
+        t_sim0 = m.time_start - ce.time_before_meteor_sec
+        t_sim1 = m.time_stop + ce.time_after_meteor_sec
+        exp_b = None
+        for b in range(c + 1, nb):
+            w0 = end(max(0, b - W + 1))
+            if w0 > t_sim0:
+                break  # the window start only moves later
+            if w0 <= t_sim0 <= end(b) and w0 <= t_sim1 <= end(b):
+                exp_b = b
+                break
+        if exp_b is None:
+            pending.append(m)
+            continue
+        b0 = max(0, exp_b - W + 1)
+        with np.errstate(divide="ignore"):
+            rows = 10 * np.log10(block_psd_rows(x, sample_scale, fs, cd, b0, exp_b + 1, k0, k1, device))
+        vmin = vmax = None
+        if mean_init is not None and b_init is not None and exp_b > b_init:
+            vmin, vmax = mean_init - cv.wf_offset_vmin, mean_init + cv.wf_offset_vmax
+        fig = plt.figure(figsize=(10, 5))
+        plt.imshow(rows.T, aspect="auto", cmap="viridis", origin="lower",
+                   extent=[end(b0), end(exp_b), freqs[0] + k0 * h, freqs[0] + (k1 + 1) * h], vmin=vmin, vmax=vmax)
+        plt.xlim(t_sim0, t_sim1)
+        plt.ylim(lo_f, hi_f)
+        plt.xlabel("Time [s]")
+        plt.ylabel("Frequency [Hz]")
+        plt.title(f"Detection {m.time_start:.2f}-{m.time_stop:.2f}sec (d={m.duration:.2f}sec)\n"
+                  + f"Min={m.db_min:.2f}dB, Max={m.db_max:.2f}dB, Mean={m.db_mean:.2f}dB, Std={m.db_std:.2f}dB")
+        plt.axvline(m.time_start, color="grey", linestyle="--")
+        plt.axvline(m.time_stop, color="grey", linestyle="--")
+        plt.axhline(ms0, color="grey", linestyle="--")
+        plt.axhline(ms1, color="grey", linestyle="--")
+        path = ce.output_dir + f"spec_{m.time_start:.2f}_{m.time_stop:.2f}.jpg"
+        plt.savefig(path, bbox_inches="tight", pad_inches=0)
+        plt.close(fig)
+        paths.append(path)
+    return paths, pending
 
 
 # ------------------------------------------------------------------ batch (device-resident)

@@ -153,6 +153,4 @@ def test_proc_wav_file_asserts_before_gpu(tmp_path):
     with pytest.raises(AssertionError, match="End sample exceeds length of audio data"):
         dsp.proc_wav_file(str(p), 0.2, (993, 1013), (690, 710), 512, 4, wav_end_sec=2.0,
                           disable_show_and_write=True)
-    with pytest.raises(NotImplementedError):
-        dsp.proc_wav_file(str(p), 0.2, (993, 1013), (690, 710), 512, 4, debug_plot_output=True,
-                          disable_show_and_write=True, required_sample_rate=None)
+

@@ -1,0 +1,108 @@
+"""The near-tie guard (meteorgpu/margin.py): a bound on |delta_gpu - delta_numpy| and the flag
+raised when a detector decision (main.py:406, :485 strict '>') lies within it.
+
+CPU: the pocketfft half of the per-bin bound against an exact (long double) DFT on random and
+adversarial blocks; the decision bound's flag on a constructed near-tie delta.
+GPU: the device's delta against numpy's within the per-block bound on random files; the flag
+in ProcResult and BatchPipeline.detections()."""
+import warnings
+
+import numpy as np
+import pytest
+
+from meteorgpu import margin as M
+from oracle import dsp_oracle as O
+
+
+def _exact_bins(xw, nfft, bins):
+    """DFT of the windowed block at the given bins in long double (x86 80-bit)."""
+    n = np.arange(len(xw), dtype=np.longdouble)
+    out = []
+    for k in bins:
+        ang = -2 * np.pi * np.longdouble(k) * n / np.longdouble(nfft)
+        out.append(np.sum(xw.astype(np.longdouble) * (np.cos(ang) + 1j * np.sin(ang))))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("seed,offset,scale", [(0, 0, 1000), (1, 30000, 10), (2, -32768, 1), (3, 0, 32767)])
+def test_pocketfft_within_bin_bound(seed, offset, scale):
+    rng = np.random.default_rng(seed)
+    B, nfft = 1200, 1024
+    x = np.clip(offset + scale * rng.standard_normal(B), -32768, 32767).astype(np.int16)
+    w = np.hanning(B)
+    xw = (x * w)[:nfft]
+    X = np.fft.rfft(x * w, n=nfft)
+    bins = np.array([0, 1, 2, 170, 171, 172, 300, 511, 512])
+    exact = _exact_bins(xw, nfft, bins)
+    S = float(np.abs(x).max()) * float(w[:nfft].sum())
+    bound = M._chain(nfft, nfft, bins) * M.U * S
+    err = np.abs(X[bins].astype(np.clongdouble) - exact).astype(np.float64)
+    assert (err <= bound).all() and err.max() > 0
+
+
+def test_band_db_error_monotone_and_infinite_for_empty_energy():
+    e = np.array([-120.0, 0.0, 60.0, 100.0])
+    b = M.band_db_error(e, 3, 1e-3)
+    assert np.isinf(b[0]) and (np.diff(b[1:]) < 0).all()
+    assert (M.band_db_error(e, 0, 1.0) == 0).all()  # empty band: E = 1e-12 on both sides
+
+
+def test_flag_on_constructed_near_tie():
+    """a block placed one ulp above its adaptive threshold (main.py:474-485) is a near tie for
+    any positive bound; a block 1 dB away is not"""
+    rng = np.random.default_rng(7)
+    d = rng.normal(0, 1, 3000)
+    dets, thr = O.get_detections_adaptive_ref(d, 4.0, 0.2)
+    i = 2000
+    d[i] = np.nextafter(thr[i], np.inf)  # thr[i] only depends on d[i-600:i]
+    dets2, thr2 = O.get_detections_adaptive_ref(d, 4.0, 0.2)
+    assert thr2[i] == thr[i] and any(t0 <= i * 0.2 < t1 for t0, t1, *_ in dets2)
+    margin = abs(d[i] - thr2[i])
+    with pytest.warns(M.NearTieWarning):
+        assert M.check(margin, M.decision_bound(np.full(3000, 1e-12), 4.0))
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert not M.check(1.0, M.decision_bound(np.full(3000, 1e-12), 4.0))
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("fs,bs,n_fft,band,noise", [(6000, 0.2, 512, (993, 1013), (690, 710)),
+                                                    (48000, 0.2, 512, (950, 1050), (2950, 3050)),
+                                                    (6000, 0.1, 256, (980, 1020), (0, 40))])
+def test_device_delta_within_bound(fs, bs, n_fft, band, noise):
+    from meteorgpu import dsp, synth
+    for seed in range(3):
+        x, _ = synth.synth_real(seed=400 + seed, fs=fs, duration_s=60.0, f0=1000.0, rate_per_min=10)
+        x[: fs * 5] = np.clip(x[: fs * 5].astype(np.int32) + 20000, -32768, 32767)  # a DC-offset stretch
+        b, nz, d, B = dsp.block_powers(x, fs, bs, band, noise, n_fft)
+        rb, rn, rd = O.block_powers_ref(x, fs, bs, band, noise, n_fft)
+        nfft = 2 * n_fft
+        L = min(B, nfft)
+        err = M.delta_error_bound(b, nz, nfft=nfft, L=L, window=dsp.hanning_sym(B)[:L],
+                                  xmax=float(np.abs(x.astype(np.float64)).max()),
+                                  band=dsp.band_bins(nfft, fs, band), noise=dsp.band_bins(nfft, fs, noise))
+        assert (np.abs(d - rd) <= err).all()
+        assert err.max() < 1e-6  # the bound is useful: far below any real decision margin
+
+
+@pytest.mark.gpu
+def test_proc_result_and_batch_flags():
+    from meteorgpu import dsp, synth
+    from meteorgpu.batch import BatchPipeline
+    x, _ = synth.synth_real(seed=9, fs=6000, duration_s=120.0, f0=1003.0, band_hz=20.0, rate_per_min=10)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", M.NearTieWarning)
+        res = dsp.process_samples(x, 6000, 0.2, (993, 1013), (690, 710), 512, 4)
+    assert 0 < res.decision_bound < 1e-6 and res.min_margin > res.decision_bound and not res.near_tie
+    bp = BatchPipeline(dsp.context(0), 3, len(x), 6000, freq_band=(993, 1013), noise_band=(690, 710),
+                       with_spectrogram=False)
+    for i in range(3):
+        bp.upload_file(i, x)
+    bp.run()
+    bp.detections()
+    assert not bp.near_tie.any() and np.allclose(bp.decision_bounds, res.decision_bound, rtol=1e-12)
+    bp.xmax[1] = np.inf  # a bound too wide to separate anything: that file is flagged
+    with pytest.warns(M.NearTieWarning, match="1 file"):
+        bp.detections()
+    assert bp.near_tie.tolist() == [False, True, False]
