@@ -29,13 +29,11 @@ namespace {
 
 constexpr int WL_THREADS = 256;
 
-// np.sum over LDS: numpy's exact order up to 128 elements (one pairwise leaf); longer runs
-// (bands wider than 128 bins, nperseg != 256 above 128) use the same 8-accumulator leaf
-// over the whole run — within an ulp or two of numpy's tree, far below the Goertzel vs
-// pocketfft rounding difference of the values summed, and without the recursion's register
-// cost in this kernel
+// np.sum over LDS in numpy's exact order: one pairwise leaf inline up to 128 elements (the
+// default 100 Hz bands: 103 bins at nfft 4096), numpy's full recursion beyond (bands wider
+// than 128 bins, nperseg above 128)
 __device__ __forceinline__ double lds_band_sum(const double *p, int64_t base, int64_t n) {
-    return n <= 128 ? np_sum_small(ArrRef{p}, base, n) : 0.0 + np_pairwise_leaf(ArrRef{p}, base, n);
+    return n <= 128 ? np_sum_small(ArrRef{p}, base, n) : np_sum(ArrRef{p}, base, n);
 }
 
 template <typename T>

@@ -286,6 +286,8 @@ class Context:
         check(self.lib.msd_create(int(device), C.byref(h)))
         self.h = h
         self.device = int(device)
+        self.options: dict[int, int] = {}  # msd_set_option values set on this context
+        self.timing_on = False
 
     def close(self):
         if getattr(self, "h", None):
@@ -311,9 +313,21 @@ class Context:
 
     def set_option(self, option: int, value: int):
         check(self.lib.msd_set_option(self.h, int(option), int(value)))
+        self.options[int(option)] = int(value)
 
     def timing(self, enable: bool = True):
         check(self.lib.msd_timing_enable(self.h, 1 if enable else 0))
+        self.timing_on = bool(enable)
+
+    def sibling(self) -> "Context":
+        """A new context (own HIP stream) on the same device with this one's options and timing
+        switch, e.g. for a stage that runs beside this context's work."""
+        c = Context(self.device)
+        for k, v in self.options.items():
+            c.set_option(k, v)
+        if self.timing_on:
+            c.timing(True)
+        return c
 
     def timing_reset(self):
         check(self.lib.msd_timing_reset(self.h))

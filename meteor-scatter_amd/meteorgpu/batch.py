@@ -36,7 +36,10 @@ class BatchPipeline:
         # (they only share the read-only samples); run() forks from and joins back into ctx.
         # Off by default: on MI355X the step is no faster (7.19-7.21 ms either way)
         # -- the persistent VALU-bound STFT leaves no idle issue slots for them to fill
-        self.side = _lib.Context(ctx.device) if concurrent and with_spectrogram else None
+        # the side context inherits ctx's options (MSD_OPT_*) and timing switch; the options that
+        # matter to block_delta / detect are the timing switch (MSD_OPT_GENERIC_STFT and
+        # MSD_OPT_FRESH_ALL only change the STFT and the stream detector)
+        self.side = ctx.sibling() if concurrent and with_spectrogram else None
         self.stage_ctx = self.side if self.side is not None else ctx
         self.nfiles, self.n, self.fs = int(nfiles), int(n_per_file), float(fs)
         self.dtype = np.dtype(dtype)

@@ -36,21 +36,24 @@ def test_welch_band_db_golden(live, golden_dir):
     np.testing.assert_allclose(got, g["expected"], rtol=0, atol=DB_TOL)
 
 
-@pytest.mark.parametrize("fs,bs,nfft,f0,dtype", [
-    (4000, 0.2, 4096, 1000, np.int16),
-    (4000, 0.5, 4096, 1020, np.int16),
-    (4000, 0.2, 2048, 1025, np.float64),
-    (8000, 0.1, 1024, 1500, np.int16),
-    (4000, 0.05, 512, 1000, np.int16),     # 200-sample blocks: nperseg capped at the block
+@pytest.mark.parametrize("fs,bs,nfft,f0,dtype,width", [
+    (4000, 0.2, 4096, 1000, np.int16, 100),
+    (4000, 0.5, 4096, 1020, np.int16, 100),
+    (4000, 0.2, 2048, 1025, np.float64, 100),
+    (8000, 0.1, 1024, 1500, np.int16, 100),
+    (4000, 0.05, 512, 1000, np.int16, 100),     # 200-sample blocks: nperseg capped at the block
+    (4000, 0.2, 4096, 1000, np.int16, 400),  # 400 Hz channels: 410 bins, numpy's full pairwise tree
+    (8000, 0.2, 4096, 2000, np.int16, 300),  # 154 bins
 ])
-def test_welch_band_db_vs_oracle(live, fs, bs, nfft, f0, dtype):
+def test_welch_band_db_vs_oracle(live, fs, bs, nfft, f0, dtype, width):
     from meteorgpu import synth
     x, _ = synth.synth_real(seed=int(fs * bs) + nfft, fs=fs, duration_s=6.0, f0=f0, sigma=500, rate_per_min=20)
     if dtype == np.float64:
         xin, sc = x.astype(np.float64) / 32768.0, 1.0
     else:
         xin, sc = x, 1 / 32768
-    cfg = live.ConfigDetection(proc_block_sec=bs, n_fft=nfft, signal_freq=f0)
+    cfg = live.ConfigDetection(proc_block_sec=bs, n_fft=nfft, signal_freq=f0, channel_width=width,
+                               noise_channel_offset=max(300, width + 50))
     got = live.welch_band_db(xin, fs, cfg, sample_scale=sc)
     ref = L.welch_band_db_ref(x.astype(np.float64) / 32768.0, fs, _ref_cfg(cfg))
     np.testing.assert_allclose(got, ref, rtol=0, atol=DB_TOL)

@@ -282,33 +282,58 @@ def test_batch_pipeline_matches_single_file_path():
 
 def test_batch_concurrent_stages_identical():
     """BatchPipeline(concurrent=True): block_delta -> detect on a second context's stream beside
-    the STFT (msd_stream_wait fork/join) gives the serial pipeline's outputs bit for bit, over
-    back-to-back steps without host synchronisation (the next step's histogram memset must wait
-    for the previous step's readers)."""
+    the STFT (msd_stream_wait fork/join) against the serial pipeline, bit for bit.  The concurrent
+    pipeline alternates two DIFFERENT input buffers over back-to-back steps with no host
+    synchronisation, so a dropped fork (side stream not waiting for ctx) or join (ctx not
+    waiting for the side stream) leaves outputs of the wrong buffer or a half-written step;
+    a last step runs straight after an upload into the buffer it reads."""
     ctx = dsp.context(0)
     fs, n, F = 48000, 48000 * 60, 8
-    xs = [synth.synth_real(seed=3100 + i, fs=fs, duration_s=60, f0=1000.0, rate_per_min=6)[0] for i in range(F)]
-    out = []
-    for conc in (False, True):
-        bp = BatchPipeline(ctx, F, n, fs, noise_band=(2950.0, 3050.0), concurrent=conc)
-        assert (bp.side is not None) == conc
+    xa = [synth.synth_real(seed=3100 + i, fs=fs, duration_s=60, f0=1000.0, rate_per_min=6)[0] for i in range(F)]
+    xb = [synth.synth_real(seed=3200 + i, fs=fs, duration_s=60, f0=1000.0, rate_per_min=9)[0] for i in range(F)]
+    xc = [synth.synth_real(seed=3300 + i, fs=fs, duration_s=60, f0=1000.0, rate_per_min=12)[0] for i in range(F)]
+
+    def outputs(bp):
+        dets, counts, status, margin = bp.detections()
+        assert (status == 0).all()
+        return (bp.delta(), bp.thresholds(), counts, [d.tobytes() for d in dets], bp.hour_counts(),
+                [bp.spectrogram(i) for i in (0, F - 1)])
+
+    def same(a, b):
+        for u, v in zip(a[:3] + (a[4],), b[:3] + (b[4],)):
+            np.testing.assert_array_equal(u, v)
+        assert a[3] == b[3]
+        for u, v in zip(a[5], b[5]):
+            np.testing.assert_array_equal(u, v)
+        assert a[4].sum() == a[2].sum()
+
+    def serial(xs):
+        bp = BatchPipeline(ctx, F, n, fs, noise_band=(2950.0, 3050.0))
         for i, x in enumerate(xs):
             bp.upload_file(i, x)
         bp.set_start_times(np.arange(F, dtype=np.int64) * 60 * 10 ** 6, 0)
-        for _ in range(3):
-            bp.run()
+        bp.run()
         ctx.synchronize()
-        dets, counts, status, margin = bp.detections()
-        assert (status == 0).all()
-        out.append((bp.delta(), bp.thresholds(), counts, [d.tobytes() for d in dets], bp.hour_counts(),
-                    [bp.spectrogram(i) for i in (0, F - 1)]))
-    a, b = out
-    for u, v in zip(a[:3] + (a[4],), b[:3] + (b[4],)):
-        np.testing.assert_array_equal(u, v)
-    assert a[3] == b[3]
-    for u, v in zip(a[5], b[5]):
-        np.testing.assert_array_equal(u, v)
-    assert a[4].sum() == a[2].sum()
+        return outputs(bp)
+
+    want_b, want_c = serial(xb), serial(xc)
+    assert want_b[2].tolist() != want_c[2].tolist()  # the inputs give different detections
+    bp = BatchPipeline(ctx, F, n, fs, noise_band=(2950.0, 3050.0), concurrent=True)
+    assert bp.side is not None
+    d_b = ctx.alloc(bp.d_x.nbytes)
+    for i in range(F):
+        bp.upload_file(i, xa[i])
+        d_b.upload(np.ascontiguousarray(xb[i], dtype=np.int16), byte_offset=i * bp.n_pad * 2)
+    bp.set_start_times(np.arange(F, dtype=np.int64) * 60 * 10 ** 6, 0)
+    for x in (None, d_b, None, d_b):  # A, B, A, B back to back
+        bp.run(x=x)
+    ctx.synchronize()
+    same(outputs(bp), want_b)
+    for i in range(F):  # upload C into the default buffer and run at once
+        bp.upload_file(i, xc[i])
+    bp.run()
+    ctx.synchronize()
+    same(outputs(bp), want_c)
 
 
 def test_full_day_batch_properties():
