@@ -159,24 +159,63 @@ struct FileCur {
     int64_t base;   // element offset of the file
 };
 
-template <typename T>
+// sample-pair registers per lane for the wave's frame pair (t, t + 1): frame t in raw[0..7], frame
+// t + 1 in raw[RB..RB+7].  SH (hop 512, integer samples): frame t + 1 starts at frame t's
+// sample 512, so its first half IS raw[4..7] (RB = 4, 12 registers, 12 loads instead of 16)
+template <bool SH>
+struct PairRegs {
+    static constexpr int RB = SH ? 4 : 8;
+    static constexpr int N = RB + 8;
+};
+
+// a wave-uniform element offset the compiler can keep in SGPRs (loads then use the scalar base +
+// 32-bit lane offset form instead of per-lane 64-bit address arithmetic)
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <typename T, bool SH>
 __device__ __forceinline__ void load_pair(const T *__restrict__ x, const FileCur &fc, int64_t t, int hop, int l,
-                                          typename PairIO<T>::raw_t (&raw)[2][8]) {
+                                          typename PairIO<T>::raw_t (&raw)[PairRegs<SH>::N]) {
     using IO = PairIO<T>;
+    constexpr int RB = PairRegs<SH>::RB;
+    if (t < fc.nfr) {  // wave-uniform
+        const T *p = x + uniform_i64(fc.base + t * (int64_t)hop) + 2 * l;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        if (t + q < fc.nfr) {  // wave-uniform
-            const T *p = x + fc.base + (t + q) * (int64_t)hop + 2 * l;
+        for (int r = 0; r < 8; ++r) raw[r] = IO::load(p + 128 * r);
+    } else {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) raw[q][r] = IO::load(p + 128 * r);
-        } else {
+        for (int r = 0; r < 8; ++r) raw[r] = IO::zero();
+    }
+    constexpr int r0 = SH ? 4 : 0;  // SH: the second frame's first half is already in raw[4..7]
+    if (t + 1 < fc.nfr) {
+        const T *p = x + uniform_i64(fc.base + (t + 1) * (int64_t)hop) + 2 * l;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) raw[q][r] = IO::zero();
-        }
+        for (int r = r0; r < 8; ++r) raw[RB + r] = IO::load(p + 128 * r);
+    } else {
+#pragma unroll
+        for (int r = r0; r < 8; ++r) raw[RB + r] = IO::zero();
     }
 }
 
-template <typename T, int WIDE>  // WIDE: 64-bit output offsets (files of 2^21 frames and more)
+// lanes 0 and 1 take their post-pass partner value from their own registers (a0 / a1 for lane 0,
+// b0 / b1 for lane 1) instead of the DPP one: two exec-masked moves (full-rate v_mov_b32) instead
+// of two v_cndmask_b32 selects (quarter-rate) per value.  The wave is fully active here.
+__device__ __forceinline__ void lane01_fix(float &m0, float &m1, float &m2, float &m3, float a0, float a1, float a2,
+                                           float a3, float b0, float b1, float b2, float b3) {
+    asm volatile(
+        "s_mov_b64 exec, 1\n\t"
+        "v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7\n\t"
+        "s_mov_b64 exec, 2\n\t"
+        "v_mov_b32 %0, %8\n\tv_mov_b32 %1, %9\n\tv_mov_b32 %2, %10\n\tv_mov_b32 %3, %11\n\t"
+        "s_mov_b64 exec, -1"
+        : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3)
+        : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
+}
+
+// WIDE: 64-bit output offsets (files of 2^20 frames and more); SH: hop 512 with integer samples
+template <typename T, int WIDE, bool SH>
 __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len,
     int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float wscale, int detrend,
@@ -188,7 +227,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     float *tile = reinterpret_cast<float *>(smem);
     const int tid = threadIdx.x;
     const int l = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar frame addresses
     float2 *scr = reinterpret_cast<float2 *>(smem + F_SCR_OFF) + wave * F_SCRF;
     float2 *t_win = reinterpret_cast<float2 *>(smem + F_TAB_OFF);
     float2 *t_tw2 = t_win + 8 * 64 - 64;  // rows r = 1..7
@@ -226,33 +265,41 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     FileCur cur = file_at(tb / tiles_per_file, tb % tiles_per_file);
     const int wcol = wave * 2;  // the two tile columns (frames) of this wave
 
-    raw_t raw[2][8];
-    load_pair<T>(x, cur, cur.ti * F_TT + wcol, hop, l, raw);
+    constexpr int RB = PairRegs<SH>::RB, NR = PairRegs<SH>::N;
+    raw_t raw[NR];
+    load_pair<T, SH>(x, cur, cur.ti * F_TT + wcol, hop, l, raw);
+    bool b_ok = cur.ti * F_TT + wcol + 1 < cur.nfr;  // the pair's second frame exists (wave-uniform)
+    // 32-bit byte offsets of this thread's write-out rows k = 128 j + tid / 8 from the tile's base
+    uint32_t wo_off[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        wo_off[j] = (uint32_t)(128 * j + (tid >> 3)) * ((uint32_t)ld * 4u) + 16u * (uint32_t)(tid & 7);
     // ---- tile → HBM: 513 rows x 32 floats (128 B), 8 lanes x 16 B per row.  Issued one
     // iteration late (in the middle of the next tile's transform), so the stores drain while
     // that tile computes; the next prefetch is issued before them, so the wait for it at the top
     // of the loop never waits for a tile's stores.
     auto write_out = [&](const FileCur &wc) {
         // scalar base + lane offsets, 8 lanes x 16 B per row: two 8-B LDS reads → one 16-B
-        // store.  WIDE = 0: 32-bit offsets (K*ld*4 < 2^32, i.e. ld < 2^21 frames); WIDE = 1:
+        // store.  WIDE = 0: 32-bit offsets (K*ld*4 < 2^31, i.e. ld < 2^20 frames); WIDE = 1:
         // 64-bit (longer files)
         char *of = reinterpret_cast<char *>(out + wc.f * (int64_t)F_K * ld + wc.ti * F_TT);
         const int qq = tid & 7;
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        // WIDE = 0: a buffer resource on the tile's base and the precomputed 32-bit row offsets (no
+        // per-store 64-bit address arithmetic)
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(of, 0, (int)((uint32_t)F_K * (uint32_t)ld * 4u), 0x00020000);
 #pragma unroll
-        for (int k0 = 0; k0 < F_K; k0 += F_NW * 64 / 8) {
-            const int k = k0 + (tid >> 3);
+        for (int j = 0; j < 5; ++j) {
+            const int k = 128 * j + (tid >> 3);
             if (k < F_K) {
                 const float2 a = *reinterpret_cast<const float2 *>(&tile[tile_at(k, 4 * qq)]);
                 const float2 b = *reinterpret_cast<const float2 *>(&tile[tile_at(k, 4 * qq + 2)]);
-                const float4 v = make_float4(a.x, a.y, b.x, b.y);
-                float4 *dst;
-                if constexpr (WIDE)
-                    dst = reinterpret_cast<float4 *>(of + ((int64_t)k * ld * 4 + 16 * qq));
-                else
-                    dst = reinterpret_cast<float4 *>(of + ((uint32_t)k * ((uint32_t)ld * 4u) + 16u * (uint32_t)qq));
+                const f4v v = f4v{a.x, a.y, b.x, b.y};
                 // streaming (non-temporal) stores: written once, never re-read here (A/B: -1 to -2 %)
-                typedef float f4v __attribute__((ext_vector_type(4)));
-                __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v *>(dst));
+                if constexpr (WIDE)
+                    __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(of + ((int64_t)k * ld * 4 + 16 * qq)));
+                else
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, wo_off[j], 0, 2 /* nt */);
             }
         }
     };
@@ -262,6 +309,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     for (int64_t tl = tb; tl < te; ++tl) {
         const bool has_next = tl + 1 < te;
         const FileCur nxt = has_next ? advance(cur) : cur;
+        const bool b_cur = b_ok;
         float2 v[2][8], wv[8];
         // ---- detrend (consumes raw); the window is applied inside pass 1
         {
@@ -270,8 +318,15 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             for (int q = 0; q < 2; ++q) {
                 if constexpr (IO::kInt) {
                     int s = 0;
+                    if constexpr (SH) {  // frame sums from the three half sums (h1 shared)
+                        int h[3] = {0, 0, 0};
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) s = IO::sum2(raw[q][r], s);
+                        for (int r = 0; r < 12; ++r) h[r >> 2] = IO::sum2(raw[r], h[r >> 2]);
+                        s = h[q] + h[q + 1];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) s = IO::sum2(raw[RB * q + r], s);
+                    }
                     s = row_sum_i(s);
                     const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
                                     __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
@@ -281,7 +336,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 } else {
                     float s = 0.f;
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) s += IO::lo(raw[q][r]) + IO::hi(raw[q][r]);
+                    for (int r = 0; r < 8; ++r) s += IO::lo(raw[RB * q + r]) + IO::hi(raw[RB * q + r]);
                     s = row_sum_f(s);
                     auto rl = [](float a, int lane) {
                         return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), lane));
@@ -290,16 +345,27 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                     mean[q] = detrend ? tot * (1.0f / 1024.0f) : 0.f;
                 }
             }
+            // each sample register converted once (SH: the shared half serves both frames)
+            float2 fr[NR];
+#pragma unroll
+            for (int i = 0; i < NR; ++i) fr[i] = make_float2(IO::lo(raw[i]), IO::hi(raw[i]));
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 wv[r] = t_win[r * 64 + l];
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
-                    v[q][r] = make_float2(IO::lo(raw[q][r]) - mean[q], IO::hi(raw[q][r]) - mean[q]);
+                    v[q][r] = make_float2(fr[RB * q + r].x - mean[q], fr[RB * q + r].y - mean[q]);
+            }
+            if (SH && !b_cur) {  // no second frame: its tile column must be zero (the loads were not)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[1][r] = make_float2(0.f, 0.f);
             }
         }
         // ---- prefetch the next tile's frame pair into the (now free) sample registers
-        if (has_next) load_pair<T>(x, nxt, nxt.ti * F_TT + wcol, hop, l, raw);
+        if (has_next) {
+            load_pair<T, SH>(x, nxt, nxt.ti * F_TT + wcol, hop, l, raw);
+            b_ok = nxt.ti * F_TT + wcol + 1 < nxt.nfr;
+        }
 
         // ---- pass 1 (Ns = 1): out[8 l + r].  One scratch per wave: frame A's transpose is
         // read back before frame B's is written (LDS executes a wave's accesses in order)
@@ -362,11 +428,15 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float2 wk = t_post[r * 64 + l];
+            float2 mm[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) mm[q] = make_float2(dpp_f<0xB1>(v[q][7 - r].x), dpp_f<0xB1>(v[q][7 - r].y));
+            lane01_fix(mm[0].x, mm[0].y, mm[1].x, mm[1].y, v[0][(8 - r) & 7].x, v[0][(8 - r) & 7].y,
+                       v[1][(8 - r) & 7].x, v[1][(8 - r) & 7].y, v[0][7 - r].x, v[0][7 - r].y, v[1][7 - r].x,
+                       v[1][7 - r].y);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const float2 sv = v[q][7 - r];
-                float2 m = make_float2(dpp_f<0xB1>(sv.x), dpp_f<0xB1>(sv.y));
-                if (l < 2) m = (l == 0) ? v[q][(8 - r) & 7] : sv;
+                const float2 m = mm[q];
                 const float2 z = v[q][r];
                 const float2 e = make_float2(z.x + m.x, z.y - m.y);
                 const float2 o = make_float2(z.y + m.y, m.x - z.x);  // -i (z - conj m)
@@ -403,8 +473,10 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 template <typename T>
 int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int64_t *len, int64_t nfiles, float *out,
                   int64_t ld) {
-    const bool wide = (uint64_t)F_K * (uint64_t)ld * 4u >= (1ull << 32);
-    auto kern = wide ? stft1024_kernel<T, 1> : stft1024_kernel<T, 0>;
+    const bool wide = (uint64_t)F_K * (uint64_t)ld * 4u >= (1ull << 31);
+    const bool sh = PairIO<T>::kInt && p->hop == 512;
+    auto kern = wide ? (sh ? stft1024_kernel<T, 1, PairIO<T>::kInt> : stft1024_kernel<T, 1, false>)
+                     : (sh ? stft1024_kernel<T, 0, PairIO<T>::kInt> : stft1024_kernel<T, 0, false>);
     if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(kern), F_LDS)) return rc;
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->ctx->device);

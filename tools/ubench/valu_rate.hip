@@ -112,6 +112,13 @@ int main() {
         run2<2, 1>(c[0], c[1], out, cyc, cus);
         run2<1, 1>(c[0], c[1], out, cyc, cus);
     }
+    // waves per SIMD: fma / add / pk_add at 1, 2, 4, 8
+    const int cfg2[][2] = {{1, 4}, {1, 8}, {1, 16}, {2, 16}};
+    for (auto &c : cfg2) {
+        run2<8, 0>(c[0], c[1], out, cyc, cus);
+        run2<8, 1>(c[0], c[1], out, cyc, cus);
+        run2<8, 6>(c[0], c[1], out, cyc, cus);
+    }
     hipFree(out);
     hipFree(cyc);
     return 0;
