@@ -87,8 +87,23 @@ struct IQ<int16_t> {  // interleaved int16 I, Q
     __device__ static float2 f(raw_t r) { return make_float2(cvt_i16_lo(r), cvt_i16_hi(r)); }
     using acc_t = int;
     __device__ static int wave_sum(int v) { return wave_sum_i(v); }
-    __device__ static int add_re(raw_t r, int acc) { return dot2_i16<1, 0>(r, acc); }
-    __device__ static int add_im(raw_t r, int acc) { return dot2_i16<0, 1>(r, acc); }
+    // the thread's I and Q sums from the converted samples: float adds of integers stay exact
+    // (|sum| <= 16 * 2^15 = 2^19), so full-rate v_add_f32 replace the quarter-rate v_dot2c
+    __device__ static void thread_sums(const float2 *v, int &sr, int &si) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a += v[r].x;
+            b += v[r].y;
+        }
+        sr = (int)a;
+        si = (int)b;
+    }
+    // the frame mean from the four waves' exact sums (|total| <= 2^27): float(total) / 4096 is
+    // float((double)total / 4096), the power-of-two scale commuting with the rounding
+    __device__ static float mean(const int *red) {
+        return (float)(red[0] + red[1] + red[2] + red[3]) * (1.0f / CS_N);
+    }
 };
 template <>
 struct IQ<float> {  // interleaved float32 I, Q (complex64)
@@ -97,8 +112,18 @@ struct IQ<float> {  // interleaved float32 I, Q (complex64)
     __device__ static float2 f(raw_t r) { return r; }
     using acc_t = float;
     __device__ static float wave_sum(float v) { return wave_sum_f(v); }
-    __device__ static float add_re(raw_t r, float acc) { return acc + r.x; }
-    __device__ static float add_im(raw_t r, float acc) { return acc + r.y; }
+    __device__ static void thread_sums(const float2 *v, float &sr, float &si) {
+        sr = 0.f;
+        si = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            sr += v[r].x;
+            si += v[r].y;
+        }
+    }
+    __device__ static float mean(const float *red) {
+        return (float)(((double)red[0] + (double)red[1] + (double)red[2] + (double)red[3]) * (1.0 / CS_N));
+    }
 };
 
 // SH = hop / 256 when the hop is a multiple of 256 below N (C5: hop 1024 → 4), else 0.
@@ -114,7 +139,7 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
     using io = IQ<T>;
     __shared__ float2 buf[CS_LDS_F2];
     __shared__ float2 tw256[256];
-    __shared__ double red[2][CS_T / 64];
+    __shared__ typename io::acc_t red[2][CS_T / 64];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     for (int i = tid; i < 256; i += CS_T) tw256[i] = g_tw[16 * i];  // W256^i = W4096^(16 i)
@@ -136,7 +161,7 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
     // load rows [R0, 16) of frame t of the stream at element offset `base`
     auto load_rows = [&](int64_t base, int64_t t, auto r0c) {
         constexpr int R0 = decltype(r0c)::value;
-        const T *p = x + 2 * (base + t * (int64_t)hop);
+        const T *p = x + 2 * uniform_i64(base + t * (int64_t)hop);
 #pragma unroll
         for (int r = R0; r < 16; ++r) raw[r] = io::load(p + 2 * (tid + 256 * r));
     };
@@ -159,18 +184,15 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
             // ---- detrend: the frame's complex mean (scipy 'constant'): exact integer sums for
             // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; per wave, then one LDS slot
             // per wave
-            typename io::acc_t sr = 0, si = 0;
+            typename io::acc_t sr, si;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                v[r] = io::f(raw[r]);
-                sr = io::add_re(raw[r], sr);
-                si = io::add_im(raw[r], si);
-            }
+            for (int r = 0; r < 16; ++r) v[r] = io::f(raw[r]);
+            io::thread_sums(v, sr, si);
             sr = io::wave_sum(sr);  // DPP row sums + readlane: no LDS round trips
             si = io::wave_sum(si);
             if (lane == 0) {
-                red[0][wave] = (double)sr;
-                red[1][wave] = (double)si;
+                red[0][wave] = sr;
+                red[1][wave] = si;
             }
             {  // prefetch frame t + 1 (raw is consumed); the segment's last frame reloads itself
                 const int64_t tn = (g + 1 < gv ? g + 1 : g) - s * max_frames;
@@ -185,8 +207,8 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
             lds_barrier();
             float mr = 0.f, mi = 0.f;
             if (detrend) {
-                mr = (float)((red[0][0] + red[0][1] + red[0][2] + red[0][3]) * (1.0 / CS_N));
-                mi = (float)((red[1][0] + red[1][1] + red[1][2] + red[1][3]) * (1.0 / CS_N));
+                mr = io::mean(red[0]);
+                mi = io::mean(red[1]);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = make_float2((v[r].x - mr) * wr[r], (v[r].y - mi) * wr[r]);
@@ -211,11 +233,15 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
 #pragma unroll
             for (int j = 0; j < 16; ++j) v[j] = buf[(16 * k2a + j) * 17 + q3];
             dft16(v);
+            // the frame's 16 KB through a buffer resource on its (wave-uniform) base: the thread's
+            // byte offset in a VGPR, the row offset 1 KB * k2b as the scalar offset, no per-lane
+            // 64-bit address arithmetic; streaming (non-temporal) stores, written once (A/B: -1 to -2 %)
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<float *>(uniform_i64(reinterpret_cast<int64_t>(of))), 0, CS_N * 4, 0x00020000);
 #pragma unroll
             for (int k2b = 0; k2b < 16; ++k2b) {
                 const float pw = v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y;
-                // streaming (non-temporal) stores: written once, never re-read here (A/B: -1 to -2 %)
-                __builtin_nontemporal_store(pw, of + tid + 256 * k2b);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pw), rsrc, 4 * tid, 1024 * k2b, 2 /* nt */);
             }
             // no barrier at the end: the next frame writes buf / red only after its first
             // barrier, which every wave reaches after its pass-3 reads of this frame

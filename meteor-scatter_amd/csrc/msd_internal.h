@@ -98,6 +98,14 @@ namespace msd {
 // vmcnt(0), which drains every outstanding prefetch and store at each barrier.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// a wave-uniform 64-bit value the compiler can keep in SGPRs (a load through x + uniform_i64(off) +
+// lane offset then uses the scalar-base + 32-bit lane offset form, no per-lane 64-bit arithmetic)
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // DPP: v + v[lane ^ 1], v[lane ^ 2], mirrored half rows, mirrored rows → each lane
 // holds the sum of its row of 16
 __device__ __forceinline__ int row_sum_i(int v) {

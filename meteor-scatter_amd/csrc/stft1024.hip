@@ -168,12 +168,6 @@ struct PairRegs {
     static constexpr int N = RB + 8;
 };
 
-// a wave-uniform element offset the compiler can keep in SGPRs (loads then use the scalar base +
-// 32-bit lane offset form instead of per-lane 64-bit address arithmetic)
-__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 template <typename T, bool SH>
 __device__ __forceinline__ void load_pair(const T *__restrict__ x, const FileCur &fc, int64_t t, int hop, int l,
