@@ -126,18 +126,20 @@ def cpu_model() -> str:
 
 
 def load_pmc_traffic(name, **match):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
-    profiles/<name>_pmc.json, if it was collected for this workload (the `match` keys agree);
-    FETCH_SIZE doubled per the gfx950 rule."""
+    """HBM bytes per launch of the roofline kernel and where they come from: the committed
+    rocprofv3 PMC summary profiles/<name>_pmc.json (FETCH_SIZE doubled per the gfx950 rule),
+    if it was collected for this workload (the `match` keys agree).  The counters are NOT
+    sampled in the run being reported (PMC passes cannot share a run with the timing): the
+    figure is profile-derived, and "traffic_source" in the bench line names the profile round."""
     p = os.path.join(ROOT, "profiles", f"{name}_pmc.json")
     try:
         with open(p) as fh:
             d = json.load(fh)
         if all(d.get(k) == v for k, v in match.items()):
-            return float(d["hbm_bytes_per_launch"])
+            return float(d["hbm_bytes_per_launch"]), f"profiles/{name}_pmc.json ({d.get('source', '?')})"
     except (OSError, ValueError, KeyError):
         pass
-    return None
+    return None, None
 
 
 LIVE_FS, LIVE_FILE_S, LIVE_FILES = 4000, 3600, 24
@@ -296,6 +298,7 @@ def main_c5(a, world, rank, local, job_of):
     samples = shard  # per rank: its 3 h (the 3072-sample frame tail is read, not counted)
     hrs = f"{a.c5_seconds / 3600:g} h"
     alg_bytes = (det.s1 - det.s0) * 4 + T * C5_N * 4
+    c5_traffic = load_pmc_traffic("cstft", frames=T, nperseg=C5_N)
     out = {
         "metric": "Msamples/s processed (192 kHz I/Q: 4096-pt two-sided spectrogram, 75% overlap, band delta, "
                   "adaptive detector)",
@@ -315,7 +318,7 @@ def main_c5(a, world, rank, local, job_of):
         "exact_threshold_frames": int(res.refined),
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": load_pmc_traffic("cstft", frames=T, nperseg=C5_N),
+                     "traffic": c5_traffic[0], "traffic_source": c5_traffic[1],
                      "kernel": "cstft4096_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
         "kernel_ms_per_step": kms,
@@ -534,6 +537,7 @@ def main():
     if not a.no_spectrogram and stft_launches:
         avg_s = stft_ms / stft_launches / 1e3
         alg_bytes = F * (n * 2 + bp.K * bp.T * 4)  # samples read once + spectrogram written once
+        traffic, traffic_src = load_pmc_traffic("stft", files=F, nperseg=NPERSEG)
         achieved = alg_bytes / avg_s / 1e9
         out["roofline"] = {
             "bound": "hbm",
@@ -541,7 +545,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_pmc_traffic("stft", files=F, nperseg=NPERSEG),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "stft1024_kernel<int16>",
             "kernel_ms": round(avg_s * 1e3, 4),
             "algorithmic_bytes_per_launch": alg_bytes,
