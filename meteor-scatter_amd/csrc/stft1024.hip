@@ -37,10 +37,14 @@ constexpr int F_SCRF = 576;               // float2 per frame scratch (phys(511)
 constexpr int F_TILE_BYTES = ((F_K * F_PITCH * 4 + 15) / 16) * 16;
 constexpr int F_SCR_OFF = F_TILE_BYTES;
 constexpr int F_TAB_OFF = F_SCR_OFF + F_NW * F_SCRF * 8;
-// tables laid out [r][lane] (lane-contiguous reads): window pairs (8 rows),
-// pass-2 twiddles W64^{(l&7) r} and pass-3 twiddles W512^{pi(l) r} (rows r = 1..7),
-// post twiddles W1024^{pi(l) + 64 r} (8 rows)
-constexpr int F_LDS = F_TAB_OFF + (8 + 7 + 7 + 8) * 64 * 8;
+// per-lane constants, one 208-B row per lane [lane][26 float2]: window pairs w[2(l + 64 r)..] (r = 0..7,
+// at 0), post twiddles W1024^{pi(l) + 64 r} (r = 0..3, at 8), pass-2 twiddles W64^{(l&7) r} (r = 1..7,
+// at 12) and pass-3 twiddles W512^{pi(l) r} (r = 1..7, at 19).  Read as ds_read_b128 (4 LDS cycles
+// per KB, the ds_read_b64 rate; the [r][lane] layout's reads were paired into ds_read2st64_b64 at
+// 8 cycles per KB); the 52-dword row stride is 4 x odd, so a b128 lane group hits 16 disjoint
+// 4-bank ranges (conflict-free)
+constexpr int F_TABW = 26;
+constexpr int F_LDS = F_TAB_OFF + F_TABW * 64 * 8;
 static_assert(F_LDS <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -223,21 +227,26 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const int l = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar frame addresses
     float2 *scr = reinterpret_cast<float2 *>(smem + F_SCR_OFF) + wave * F_SCRF;
-    float2 *t_win = reinterpret_cast<float2 *>(smem + F_TAB_OFF);
-    float2 *t_tw2 = t_win + 8 * 64 - 64;  // rows r = 1..7
-    float2 *t_tw3 = t_tw2 + 7 * 64;
-    float2 *t_post = t_tw3 + 8 * 64;  // rows r = 0..7 (t_tw3 rows end at 7 * 64 + 64)
+    float2 *t_all = reinterpret_cast<float2 *>(smem + F_TAB_OFF);
+    const float2 *tab = t_all + l * F_TABW;  // this lane's constants
     auto pi_of = [](int i) { return (int)k_pass3_lane[i]; };
-    for (int i = tid; i < 8 * 64; i += F_NW * 64) {
-        const int r = i >> 6, li = i & 63;
-        const float2 gw = *reinterpret_cast<const float2 *>(g_win + 2 * (li + 64 * r));
-        t_win[i] = make_float2(gw.x * wscale, gw.y * wscale);  // window * sqrt(scale / 2)
-        if (r > 0) {
-            t_tw2[i] = g_tw[8 * (li & 7) * r];
-            t_tw3[i] = g_tw[pi_of(li) * r];
+    for (int i = tid; i < 64 * F_TABW; i += F_NW * 64) {
+        const int li = i / F_TABW, c = i % F_TABW;
+        float2 e;
+        if (c < 8) {
+            const float2 gw = *reinterpret_cast<const float2 *>(g_win + 2 * (li + 64 * c));
+            e = make_float2(gw.x * wscale, gw.y * wscale);  // window * sqrt(scale / 2)
+        } else if (c < 12) {
+            e = g_post[pi_of(li) + 64 * (c - 8)];
+        } else if (c < 19) {
+            e = g_tw[8 * (li & 7) * (c - 11)];
+        } else {
+            e = g_tw[pi_of(li) * (c - 18)];
         }
-        t_post[i] = g_post[pi_of(li) + 64 * r];
+        t_all[i] = e;
     }
+    // the table entries as ds_read_b128 (two float2 each) / ds_read_b64
+    auto tab4 = [&](int c) { return *reinterpret_cast<const float4 *>(tab + c); };
     const int pi = pi_of(l);
     __syncthreads();
 
@@ -344,8 +353,13 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 #pragma unroll
             for (int i = 0; i < NR; ++i) fr[i] = make_float2(IO::lo(raw[i]), IO::hi(raw[i]));
 #pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+                const float4 w4 = tab4(r);
+                wv[r] = make_float2(w4.x, w4.y);
+                wv[r + 1] = make_float2(w4.z, w4.w);
+            }
+#pragma unroll
             for (int r = 0; r < 8; ++r) {
-                wv[r] = t_win[r * 64 + l];
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
                     v[q][r] = make_float2(fr[RB * q + r].x - mean[q], fr[RB * q + r].y - mean[q]);
@@ -381,11 +395,21 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         if (have_prev) write_out(prev);
         // ---- pass 2 (Ns = 8): out[64 (l>>3) + (l&7) + 8 r]
         const int o2 = 64 * (l >> 3) + (l & 7);
+        float2 tw3_1;  // the first pass-3 twiddle shares the pass-2 table's last ds_read_b128
+        {
+            float2 w[8];  // pass-2 twiddles r = 1..7 at 12..18
 #pragma unroll
-        for (int r = 1; r < 8; ++r) {
-            const float2 w = t_tw2[r * 64 + l];
-            v[0][r] = cmul(v[0][r], w);
-            v[1][r] = cmul(v[1][r], w);
+            for (int r = 1; r < 8; r += 2) {
+                const float4 w4 = tab4(11 + r);
+                w[r] = make_float2(w4.x, w4.y);
+                if (r < 7) w[r + 1] = make_float2(w4.z, w4.w);
+                else tw3_1 = make_float2(w4.z, w4.w);
+            }
+#pragma unroll
+            for (int r = 1; r < 8; ++r) {
+                v[0][r] = cmul(v[0][r], w[r]);
+                v[1][r] = cmul(v[1][r], w[r]);
+            }
         }
         dft8(v[0]);
         dft8(v[1]);
@@ -399,11 +423,20 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             wave_sync();
         }
         // ---- pass 3 (Ns = 64): butterfly pi(l) → lane holds Z[pi(l) + 64 r]
+        {
+            float2 w[8];  // pass-3 twiddles r = 1..7 at 19..25
+            w[1] = tw3_1;
 #pragma unroll
-        for (int r = 1; r < 8; ++r) {
-            const float2 w = t_tw3[r * 64 + l];
-            v[0][r] = cmul(v[0][r], w);
-            v[1][r] = cmul(v[1][r], w);
+            for (int r = 2; r < 8; r += 2) {
+                const float4 w4 = tab4(18 + r);
+                w[r] = make_float2(w4.x, w4.y);
+                w[r + 1] = make_float2(w4.z, w4.w);
+            }
+#pragma unroll
+            for (int r = 1; r < 8; ++r) {
+                v[0][r] = cmul(v[0][r], w[r]);
+                v[1][r] = cmul(v[1][r], w[r]);
+            }
         }
         dft8(v[0]);
         dft8(v[1]);
@@ -419,9 +452,16 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         // the window carries sqrt(scale / 2): |X'|^2 is the doubled one-sided density; lane 0's
         // r = 0 pair (DC, Nyquist) is not doubled
         const float sc0 = l == 0 ? 0.5f : 1.0f;
+        float2 wpost[4];  // post twiddles at 8..11: two ds_read_b128
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+            const float4 w4 = tab4(8 + r);
+            wpost[r] = make_float2(w4.x, w4.y);
+            wpost[r + 1] = make_float2(w4.z, w4.w);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float2 wk = t_post[r * 64 + l];
+            const float2 wk = wpost[r];
             float2 mm[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) mm[q] = make_float2(dpp_f<0xB1>(v[q][7 - r].x), dpp_f<0xB1>(v[q][7 - r].y));
