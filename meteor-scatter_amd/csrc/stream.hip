@@ -599,8 +599,12 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
                                                   double *__restrict__ seg_margin, double *__restrict__ thr_used,
                                                   int32_t *__restrict__ overflow, int32_t *__restrict__ need,
                                                   const double *__restrict__ eps, uint8_t *__restrict__ exact,
-                                                  int32_t *__restrict__ list, int32_t *__restrict__ list_count) {
+                                                  int32_t *__restrict__ list, int32_t *__restrict__ list_count,
+                                                  int32_t *__restrict__ changed) {
     const int64_t s = blockIdx.x;
+    // the round's change counter, which the propagate kernel after this one increments (zeroed
+    // here instead of by a separate memset launch per round)
+    if (changed && s == 0 && threadIdx.x == 0) *changed = 0;
     if (!active[s]) return;
     const int lane = threadIdx.x;
     const int64_t a = s * P.seg_len;
@@ -626,7 +630,8 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
             ex = exact[j];
         }
     };
-    // two steps in flight: the loads of step k + 128 are issued while step k is walked
+    // two steps in flight: the loads of step k + 128 are issued while step k is walked (deeper
+    // rings, 8 steps unrolled, measured slower: the walk is bound by its own instruction latency)
     double dv_n, fr_n, ep_n = 0.0, dv_m, fr_m, ep_m = 0.0;
     uint8_t ex_n = 1, ex_m = 1;
     ld(a, dv_n, fr_n, ep_n, ex_n);
@@ -1183,11 +1188,10 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
                 hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
                                    p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
                                    p->d_margin, p->d_thr, overflow, nullptr, p->d_eps, p->d_exact,
-                                   p->decide ? p->d_list : nullptr, p->d_done + p->ntiles);
+                                   p->decide ? p->d_list : nullptr, p->d_done + p->ntiles, changed);
             }
             MSD_HIP(hipGetLastError());
             ++nround;
-            MSD_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), st));
             hipLaunchKernelGGL(propagate_kernel, dim3((unsigned)((p->nseg + 255) / 256)), dim3(256), 0, st, st_in(p),
                                st_out(p), p->d_active, p->nseg, p->seg_len, p->frame0, P.F0, changed);
             MSD_HIP(hipGetLastError());
@@ -1214,7 +1218,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
             KernelTimer timer(p->ctx, K_SSCAN);
             hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail, p->d_fresh, P,
                                st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns, p->d_margin, p->d_thr,
-                               overflow, p->d_need, nullptr, nullptr, nullptr, nullptr);
+                               overflow, p->d_need, nullptr, nullptr, nullptr, nullptr, nullptr);
         }
         MSD_HIP(hipGetLastError());
         MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));
