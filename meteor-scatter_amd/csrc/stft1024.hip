@@ -108,9 +108,17 @@ __constant__ int8_t k_pass3_lane[64] = {0,  32, 1,  63, 3,  61, 5,  59, 6,  58, 
                                         2,  62, 4,  60, 8,  56, 9,  55, 10, 54, 11, 53, 17, 47, 19, 45,
                                         20, 44, 21, 43, 22, 42, 23, 41, 24, 40, 29, 35, 30, 34, 31, 33};
 
-// Output tile: bin k, frame column c at k * 34 + c (pitch 34 keeps rows 8-B aligned; an
-// XOR-swizzled pitch-32 tile read by conflict-free ds_read_b128 measured 1.5 % slower)
-__device__ __forceinline__ int tile_at(int k, int c) { return k * F_PITCH + c; }
+// Output tile: bin k, frame column c at k * 34 + ((c + rot(k)) & 31) (pitch 34 keeps rows 8-B
+// aligned; an XOR-swizzled pitch-32 tile read by conflict-free ds_read_b128 measured 1.5 % slower).
+// The half-row rotation of rows k = 32, 40, 48, 56 (mod 64) makes the post pass's tile writes
+// conflict-free: a 16-lane ds_write_b64 group holds 8 conjugate pairs (j, 64 - j) of butterflies,
+// whose rows 2k mod 32 banks cover 15 residues k mod 16 with one doubled (0 or 8, the pair
+// j = 0 / 32, 16 / 48, 8 / 56 or 24 / 40), a 2-way conflict in every group (SQ_LDS_BANK_CONFLICT
+// 1.30e8 = 32 cycles per wave-iteration, all of the kernel's); moving one row of each such pair
+// by 16 banks fills the missing residue.  The write-out's rows 2m, 2m + 1 keep complementary
+// banks (tools/lds_bank_model.py checks every access pattern of the kernel).
+__device__ __forceinline__ int tile_rot(int k) { return (k & 39) == 32 ? 16 : 0; }
+__device__ __forceinline__ int tile_at(int k, int c) { return k * F_PITCH + ((c + tile_rot(k)) & 31); }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -287,6 +295,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         // 64-bit (longer files)
         char *of = reinterpret_cast<char *>(out + wc.f * (int64_t)F_K * ld + wc.ti * F_TT);
         const int qq = tid & 7;
+        const int rw = tile_rot(tid >> 3);  // = tile_rot(k) for every j (k = 128 j + tid / 8)
         typedef float f4v __attribute__((ext_vector_type(4)));
         // WIDE = 0: a buffer resource on the tile's base and the precomputed 32-bit row offsets (no
         // per-store 64-bit address arithmetic)
@@ -295,8 +304,9 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         for (int j = 0; j < 5; ++j) {
             const int k = 128 * j + (tid >> 3);
             if (k < F_K) {
-                const float2 a = *reinterpret_cast<const float2 *>(&tile[tile_at(k, 4 * qq)]);
-                const float2 b = *reinterpret_cast<const float2 *>(&tile[tile_at(k, 4 * qq + 2)]);
+                const int c0 = k * F_PITCH + ((4 * qq + rw) & 31);  // tile_at(k, 4 qq); + 2: tile_at(k, 4 qq + 2)
+                const float2 a = *reinterpret_cast<const float2 *>(&tile[c0]);
+                const float2 b = *reinterpret_cast<const float2 *>(&tile[c0 + 2]);
                 const f4v v = f4v{a.x, a.y, b.x, b.y};
                 // streaming (non-temporal) stores: written once, never re-read here (A/B: -1 to -2 %)
                 if constexpr (WIDE)
@@ -490,10 +500,14 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             p256[q] = (z.x * z.x + z.y * z.y) * 4.0f;
         }
         lds_barrier();  // the previous tile's write-out has finished reading the tile
+        // tile_at(pi + 64 r, wcol) and tile_at(512 - pi - 64 r, wcol): the rotations depend on the
+        // row mod 64 only, i.e. on pi
+        const int mb = (512 - pi) & 63;
+        const int ta = tile_at(pi, wcol), tb = tile_at(mb, wcol) + (512 - pi - mb) * F_PITCH;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            *reinterpret_cast<float2 *>(&tile[tile_at(pi + 64 * r, wcol)]) = make_float2(pa[0][r], pa[1][r]);
-            *reinterpret_cast<float2 *>(&tile[tile_at(512 - pi - 64 * r, wcol)]) = make_float2(pb[0][r], pb[1][r]);
+            *reinterpret_cast<float2 *>(&tile[ta + 64 * r * F_PITCH]) = make_float2(pa[0][r], pa[1][r]);
+            *reinterpret_cast<float2 *>(&tile[tb - 64 * r * F_PITCH]) = make_float2(pb[0][r], pb[1][r]);
         }
         if (l == 0) *reinterpret_cast<float2 *>(&tile[tile_at(256, wcol)]) = make_float2(p256[0], p256[1]);
         lds_barrier();  // tile complete
