@@ -151,8 +151,9 @@ int msd_create(int device, msd_ctx **out) {
     MSD_HIP(hipSetDevice(device));
     auto *c = new msd_ctx();
     c->device = device;
-    hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device);
-    if (c->num_cu <= 0) c->num_cu = 256;
+    if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        c->num_cu <= 0)
+        c->num_cu = 256;  // grid sizing only: a wrong count costs balance, not correctness
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;

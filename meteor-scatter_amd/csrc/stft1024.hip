@@ -526,8 +526,7 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
     auto kern = wide ? (sh ? stft1024_kernel<T, 1, PairIO<T>::kInt> : stft1024_kernel<T, 1, false>)
                      : (sh ? stft1024_kernel<T, 0, PairIO<T>::kInt> : stft1024_kernel<T, 0, false>);
     if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(kern), F_LDS)) return rc;
-    int cus = 256;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->ctx->device);
+    const int cus = p->ctx->num_cu;  // queried once in msd_create
     const int64_t tiles_per_file = ld / F_TT;
     const int64_t ntiles = tiles_per_file * nfiles;
     int64_t wgs = cus;  // one 16-wave workgroup per CU (LDS-bound residency)
