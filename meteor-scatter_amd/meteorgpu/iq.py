@@ -170,17 +170,23 @@ class IQShardDetector:
         """interleaved I/Q of the shard's samples [s0, s1) on the host → the shard's delta in the
         stream plan, `chunk_frames` frames at a time (or all at once without chunking)"""
         iq_shard = np.ascontiguousarray(iq_shard)
+        self.process_source(lambda a, b: iq_shard[2 * a: 2 * b])
+
+    def process_source(self, read):
+        """as process_host, with the samples pulled chunk by chunk: read(a, b) returns the
+        interleaved I/Q of shard samples [a, b) (relative to s0), so a recording longer than host
+        memory streams from its source (a file, an SDR ring) through HBM"""
         nloc = self.f1 - self.f0
         if not self.chunk:
             if nloc > 0:
-                self.upload(iq_shard)
+                self.upload(np.ascontiguousarray(read(0, self.s1 - self.s0)))
             self.spectrogram_and_delta()
             return
         for c0 in range(0, nloc, self.chunk):
             nf = min(self.chunk, nloc - c0)
             a = c0 * self.hop
             b = a + (nf - 1) * self.hop + self.N
-            self.batch.upload(0, iq_shard[2 * a: 2 * b])
+            self.batch.upload(0, np.ascontiguousarray(read(a, b)))
             self.d_frames.upload(np.array([nf], np.int64))
             self.batch.run()  # frames past nf read stale samples; their powers are not used
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,

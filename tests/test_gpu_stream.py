@@ -204,6 +204,102 @@ def test_iq_sharded_threads():
         assert np.array_equal(r.detections["db"], np.array([d.dB for d in one]))
 
 
+def test_iq_half_hour_sharded_matches_whole():
+    """C5 at scale with the reference's defaults (window 120 s = 22 500 frames, freeze 20 s, fixed
+    init 10 s): a 30-minute 192 kHz stream (337 k frames, tiled from seeded 1-minute chunks as the
+    bench does) time-sharded over 4 rank-threads, each with its own context and spectrogram of its
+    samples, gives the detections, dB values and thresholds of one process holding the whole
+    stream, bit for bit (the oracle comparison lives at sizes the CPU finishes in seconds)"""
+    from meteorgpu import _lib, iq, synth
+    fs, minutes = 192000, 30
+    chunk = fs * 60
+    pool = []
+    for j in range(4):
+        i_, q_, _ = synth.synth_iq(700 + j, fs, 60.0, 1000.0, sigma=1000.0, rate_per_min=6, snr_db=(10.0, 30.0))
+        z = np.empty(2 * chunk, np.int16)
+        z[0::2], z[1::2] = i_, q_
+        pool.append(z)
+    n = chunk * minutes + 3072
+    buf = np.empty(2 * n, np.int16)
+    for k in range(minutes + 1):
+        a, b = k * chunk, min((k + 1) * chunk, n)
+        if a < b:
+            buf[2 * a: 2 * b] = pool[k % 4][: 2 * (b - a)]
+
+    def run(world, thresholds):
+        def body(r, comm):
+            ctx = _lib.Context(0)
+            try:
+                det = iq.IQShardDetector(ctx, n, fs, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
+                                         rank=r, world=world)
+                det.upload(buf[2 * det.s0: 2 * det.s1])
+                det.spectrogram_and_delta()
+                res = det.detect(comm, thresholds=thresholds)
+                det.close()
+                return res
+            finally:
+                ctx.close()
+        return run_threads(world, body)
+
+    for thresholds in (False, True):
+        one = run(1, thresholds)[0]
+        assert len(one.detections) > 100
+        four = run(4, thresholds)
+        for r in four:
+            assert np.array_equal(r.detections, one.detections)
+            assert r.thr0 == one.thr0
+        if thresholds:  # each rank holds the thresholds of its own frames
+            got = np.concatenate([np.asarray(r.thresholds) for r in four])
+            assert np.array_equal(got, np.asarray(one.thresholds), equal_nan=True)
+
+
+def test_iq_day_eight_shards_chunked_matches_whole():
+    """C5 as BASELINE configures it: 24 h of 192 kHz I/Q (16.2 M frames, 66 GB of int16 in, 265 GB
+    of spectrogram), time-sharded over 8 rank-threads (the 8-GPU layout on one device, each with its
+    own context), each streaming its 3 h through HBM in 2^19-frame chunks
+    (IQShardDetector.process_source), the reference's default detector settings, decisions only
+    (the bench's mode): the same detections, dB values and whole-stream threshold as one process
+    streaming the whole day.  The stream is tiled from seeded 1-minute chunks, as in the bench."""
+    from meteorgpu import _lib, iq, synth
+    fs, chunk, period = 192000, 192000 * 60, 4
+    pool = np.empty(2 * chunk * period, np.int16)  # 4 minutes, repeated
+    for j in range(period):
+        i_, q_, _ = synth.synth_iq(900 + j, fs, 60.0, 1000.0, sigma=1000.0, rate_per_min=6, snr_db=(10.0, 30.0))
+        pool[2 * j * chunk: 2 * (j + 1) * chunk: 2], pool[2 * j * chunk + 1: 2 * (j + 1) * chunk: 2] = i_, q_
+    P = chunk * period
+    n = fs * 24 * 3600 + 3072
+
+    def stream(a, b):  # interleaved samples [a, b) of the day
+        parts = []
+        while a < b:
+            o = a % P
+            m = min(b - a, P - o)
+            parts.append(pool[2 * o: 2 * (o + m)])
+            a += m
+        return np.concatenate(parts) if len(parts) > 1 else parts[0]
+
+    def run(world):
+        def body(r, comm):
+            ctx = _lib.Context(0)
+            try:
+                det = iq.IQShardDetector(ctx, n, fs, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
+                                         rank=r, world=world, chunk_frames=1 << 19)
+                assert det.W == 22500
+                det.process_source(lambda a, b: stream(det.s0 + a, det.s0 + b))
+                res = det.detect(comm, thresholds=False)
+                det.close()
+                return res
+            finally:
+                ctx.close()
+        return run_threads(world, body)
+
+    one = run(1)[0]
+    assert len(one.detections) > 5000
+    for r in run(8):
+        assert np.array_equal(r.detections, one.detections)
+        assert r.thr0 == one.thr0
+
+
 def test_stream_detector_over_rccl_single_rank():
     """The C5 exchange path through RCCL (msd_comm_allgather behind stream.RcclComm) at world
     size 1 on the one-GPU box: variable-length allgathers round-trip, and the detector run
