@@ -371,6 +371,66 @@ def test_full_day_batch_properties():
     np.testing.assert_array_equal(deltas[1437], d0)
 
 
+@pytest.mark.gpu
+def test_c4_day_sharded_over_eight_ranks():
+    """C4 at full size: the 1440-file day cut into 8 contiguous file ranges (meteorgpu.shard.shard_range,
+    as bench.py --shard-day), one BatchPipeline per rank-thread with its own context.  The hour
+    histograms summed (the RCCL all-reduce's job) equal one pipeline over the whole day; every
+    file's detections, counts and delta, and the spectrograms of each range's first and last file,
+    equal the whole-day pipeline's bit for bit."""
+    import threading
+    from meteorgpu.shard import shard_range
+    fs, n, F, W = 48000, 48000 * 60, 1440, 8
+    pool = [synth.synth_real(seed=4100 + j, fs=fs, duration_s=60, f0=1000.0, rate_per_min=6)[0] for j in range(4)]
+    epoch, day0 = datetime.datetime(1970, 1, 1), datetime.datetime(2025, 6, 1)
+    us = lambda t: (t - epoch) // datetime.timedelta(microseconds=1)  # noqa: E731
+
+    def make(ctx, lo, hi, spec_files):
+        bp = BatchPipeline(ctx, hi - lo, n, fs, noise_band=(2950.0, 3050.0))  # the bench's bands
+        for i in range(hi - lo):
+            bp.upload_file(i, pool[(lo + i) % 4])
+        bp.set_start_times(np.array([us(day0 + datetime.timedelta(minutes=lo + i)) for i in range(hi - lo)],
+                                    np.int64), us(day0))
+        bp.run()
+        ctx.synchronize()
+        dets, counts, status, _ = bp.detections()
+        return dict(dets=dets, counts=counts, status=status, hist=bp.hour_counts(), delta=bp.delta(),
+                    spec={lo + i: bp.spectrogram(i) for i in spec_files})
+
+    whole = make(dsp.context(0), 0, F, range(4))  # files 0-3 = the 4 pool inputs
+    assert (whole["status"] == 0).all() and whole["counts"].sum() > 1000 and whole["hist"].sum() == whole["counts"].sum()
+    results, errs = [None] * W, []
+
+    def body(r):
+        try:
+            ctx = _lib.Context(0)
+            try:
+                lo, hi = shard_range(F, r, W)
+                results[r] = (lo, hi, make(ctx, lo, hi, (0, hi - lo - 1)))
+            finally:
+                ctx.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(W)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+    assert np.array_equal(sum(res["hist"] for _, _, res in results), whole["hist"])
+    assert [lo for lo, _, _ in results] == sorted(lo for lo, _, _ in results) and results[-1][1] == F
+    for lo, hi, res in results:
+        assert (res["status"] == 0).all()
+        assert np.array_equal(res["counts"], whole["counts"][lo:hi])
+        assert np.array_equal(res["delta"], whole["delta"][lo:hi])
+        for i in range(hi - lo):
+            assert np.array_equal(res["dets"][i], whole["dets"][lo + i])
+        for f, sp in res["spec"].items():  # file f has pool input f % 4, as whole-day file f % 4
+            assert np.array_equal(sp, whole["spec"][f % 4])
+
+
 @pytest.mark.parametrize("dt", [np.int16, np.float32, np.uint8])
 def test_stft_fast_path_matches_generic_kernel(dt):
     """The specialised N=1024 kernel and the generic Stockham kernel agree (A/B switch)."""
