@@ -126,23 +126,38 @@ struct IQ<float> {  // interleaved float32 I, Q (complex64)
     }
 };
 
+// int16 I/Q at 75 % overlap (C5) runs 4 waves per SIMD: 128 VGPRs with the [k][j1] pass-2 twiddle
+// table (its reads need no per-k index registers; 16 B of spills, outside the frame loop) — A/B
+// 12.27 → 11.79 ms.  The other variants keep 3 waves and the W256^m table (float32 I/Q at 4 waves
+// spills inside the loop, 12.33 → 14.55 ms; the [k][j1] table alone at 3 waves is 2 % slower)
+template <typename T, int SH>
+struct CsTune {
+    static constexpr bool kW4 = std::is_same<T, int16_t>::value && SH == 4;
+    static constexpr int kWavesPerSimd = kW4 ? 4 : 1;  // launch-bounds minimum (1: no constraint)
+};
+
 // SH = hop / 256 when the hop is a multiple of 256 below N (C5: hop 1024 → 4), else 0.
 // Thread j holds z[j + 256 r]; the next frame of the same stream needs z[j + 256 (r + SH)],
 // so with SH > 0 it keeps raw[SH..15] (shifted down) and loads only raw[16-SH..15]: each
 // sample is loaded once per workgroup instead of N / hop times.
 template <typename T, int SH>
-__global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x, const int64_t *__restrict__ off,
-                                                         const int64_t *__restrict__ len, int64_t nstreams,
-                                                         int64_t max_frames, int64_t total, int64_t per, int hop,
-                                                         int detrend, const float *__restrict__ g_win,
-                                                         const float2 *__restrict__ g_tw, float *__restrict__ out) {
+__global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft4096_kernel(
+    const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len, int64_t nstreams,
+    int64_t max_frames, int64_t total, int64_t per, int hop, int detrend, const float *__restrict__ g_win,
+    const float2 *__restrict__ g_tw, float *__restrict__ out) {
     using io = IQ<T>;
     __shared__ float2 buf[CS_LDS_F2];
-    __shared__ float2 tw256[256];
+    // pass-2 twiddles W256^(j1 k).  kW4: at k * 16 + j1 — a half-wave reads 16 consecutive entries
+    // (its two q values share them), conflict-free, the row an immediate offset, no index
+    // registers; else W256^m at m = (j1 k) & 255 (2- to 8-way conflicts for even k: 10 extra LDS
+    // cycles per wave and frame)
+    constexpr bool W4 = CsTune<T, SH>::kW4;
+    __shared__ float2 tw2[256];
     __shared__ typename io::acc_t red[2][CS_T / 64];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < 256; i += CS_T) tw256[i] = g_tw[16 * i];  // W256^i = W4096^(16 i)
+    for (int i = tid; i < 256; i += CS_T)  // W256^x = W4096^(16 x)
+        tw2[i] = g_tw[16 * (W4 ? ((i & 15) * (i >> 4)) & 255 : i)];
     // per-thread constants: window (x sqrt(scale)) and the pass-1 twiddles W4096^(j q)
     float wr[16];
     float2 tw1[16];
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(CS_T) void cstft4096_kernel(const T *__restrict__ x
             for (int j2 = 0; j2 < 16; ++j2) v[j2] = buf[q2 * CS_P + j1 + 16 * j2];
             dft16(v);
 #pragma unroll
-            for (int k = 1; k < 16; ++k) v[k] = c_mul(v[k], tw256[(j1 * k) & 255]);
+            for (int k = 1; k < 16; ++k) v[k] = c_mul(v[k], tw2[W4 ? 16 * k + j1 : (j1 * k) & 255]);
             lds_barrier();  // everyone has read pass 1's layout
 #pragma unroll
             for (int k = 0; k < 16; ++k) buf[(16 * k + j1) * 17 + q2] = v[k];  // u[q][k2a][j1], column-major
@@ -336,12 +351,17 @@ int msd_cstft_psd_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
     DeviceGuard g(p->ctx->device);
     const int64_t total = nstreams * max_frames;
-    int64_t wgs = (int64_t)p->ctx->num_cu * 3;  // persistent: LDS (37 KB) allows 4 per CU
-    if (wgs > total) wgs = total;
-    const int64_t per = (total + wgs - 1) / wgs;
-    wgs = (total + per - 1) / per;
     KernelTimer timer(p->ctx, K_CSTFT);
     auto launch = [&](auto kern, const auto *xp) {
+        // persistent: as many workgroups as stay resident (registers and the 37 KB of LDS decide;
+        // the compiler's register count sets 3 or 4 per CU)
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, CS_T, 0) != hipSuccess || per_cu < 1)
+            per_cu = 3;
+        int64_t wgs = (int64_t)p->ctx->num_cu * per_cu;
+        if (wgs > total) wgs = total;
+        const int64_t per = (total + wgs - 1) / wgs;
+        wgs = (total + per - 1) / per;
         hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
                            max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out);
     };

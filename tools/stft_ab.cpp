@@ -5,6 +5,7 @@
 //   STFT_AB_MODE=c3 (default): msd_stft_psd_dev, 1440 x 60 s 48 kHz int16, 1024 / 512
 //                              (STFT_AB_FILES overrides the file count)
 //   STFT_AB_MODE=c5:           msd_cstft_psd_dev, one 3 h 192 kHz int16 I/Q stream, 4096 / 1024
+//                              (STFT_AB_F32=1: the same samples as float32 I/Q)
 //   STFT_AB_CLK=1: a variant built with -DXP_CLK leaves block 0's shader-cycle and 100 MHz
 //                  realtime counts in the first 16 output bytes; printed per round.
 // Build: g++ -O2 -std=c++17 tools/stft_ab.cpp -I include -I /opt/rocm/include -D__HIP_PLATFORM_AMD__
@@ -76,7 +77,9 @@ int main(int argc, char **argv) {
     const int64_t N = c5 ? 4096 : 1024, hop = c5 ? 1024 : 512, K = c5 ? 4096 : 513;
     const double fs = c5 ? 192000.0 : 48000.0;
     const int64_t T = (n - N) / hop + 1, ld = c5 ? T : (T + 31) / 32 * 32;
-    const int64_t esz = c5 ? 4 : 2;  // bytes per sample (int16, or int16 I + Q)
+    // STFT_AB_F32=1 (c5): float32 I/Q (the int16 samples / 32768) instead of int16
+    const bool f32 = c5 && getenv("STFT_AB_F32");
+    const int64_t esz = c5 ? (f32 ? 8 : 4) : 2;  // bytes per sample (int16, or I + Q)
     const int kid = c5 ? 6 : 0;      // msd_timing kernel id
     std::vector<Lib> libs;
     for (int i = 2; i < argc; ++i) {
@@ -141,9 +144,15 @@ int main(int argc, char **argv) {
     int64_t *doff, *dlen;
     CK(hipMalloc(&dx, (size_t)esz * npad * nfiles));
     CK(hipMalloc(&dout, sizeof(float) * K * ld * nfiles));
+    std::vector<float> hostf;
+    if (f32) {
+        hostf.resize(host.size());
+        for (size_t i = 0; i < host.size(); ++i) hostf[i] = host[i] / 32768.f;
+    }
+    const void *src = f32 ? static_cast<const void *>(hostf.data()) : static_cast<const void *>(host.data());
     if (c5) {
         for (int64_t i = 0; i < n; i += blk)
-            CK(hipMemcpy(dx + esz * i, host.data(), (size_t)esz * std::min(blk, n - i), hipMemcpyHostToDevice));
+            CK(hipMemcpy(dx + esz * i, src, (size_t)esz * std::min(blk, n - i), hipMemcpyHostToDevice));
     } else {
         for (int64_t f = 0; f < nfiles; ++f)
             CK(hipMemcpy(dx + esz * f * npad, host.data() + (f % 16) * npad, (size_t)esz * npad,
@@ -168,7 +177,7 @@ int main(int argc, char **argv) {
             }
     }
     auto launch = [&](Lib &l) {
-        return c5 ? l.cpsd_dev(l.cplan, dx, MSD_CI16, doff, dlen, nfiles, T, dout)
+        return c5 ? l.cpsd_dev(l.cplan, dx, f32 ? MSD_CF32 : MSD_CI16, doff, dlen, nfiles, T, dout)
                   : l.psd_dev(l.plan, dx, MSD_I16, doff, dlen, nfiles, T, dout, ld);
     };
 
