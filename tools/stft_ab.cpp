@@ -48,7 +48,6 @@ struct Lib {
     int (*t_reset)(msd_ctx *);
     int (*t_get)(msd_ctx *, int, double *, int64_t *);
     const char *(*last_error)(void);
-    int (*set_bands)(msd_cstft_plan *, int32_t, int32_t, int32_t, int32_t, double *) = nullptr;  // optional
     msd_ctx *ctx = nullptr;
     msd_stft_plan *plan = nullptr;
     msd_cstft_plan *cplan = nullptr;
@@ -100,7 +99,6 @@ int main(int argc, char **argv) {
         sym(l, l.t_reset, "msd_timing_reset");
         sym(l, l.t_get, "msd_timing_get");
         sym(l, l.last_error, "msd_last_error");
-        l.set_bands = reinterpret_cast<decltype(l.set_bands)>(dlsym(l.h, "msd_cstft_set_band_energies"));
         libs.push_back(l);
     }
     // periodic Hann (float32) and scipy's density scale 1 / (fs * sum w^2)
@@ -165,17 +163,6 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(doff, off.data(), sizeof(int64_t) * nfiles, hipMemcpyHostToDevice));
     CK(hipMemcpy(dlen, len.data(), sizeof(int64_t) * nfiles, hipMemcpyHostToDevice));
     const double gbytes = (double)nfiles * ((double)esz * n + 4.0 * K * T) * 1e-9;
-    // STFT_AB_BANDS=1 (c5): the fused band energies of the C5 bench bands (950..1050 Hz, bins 21..22;
-    // -3050..-2950 Hz, bins -65..-63) in every library that has msd_cstft_set_band_energies
-    if (c5 && getenv("STFT_AB_BANDS")) {
-        double *de;
-        CK(hipMalloc(&de, sizeof(double) * 2 * T));
-        for (auto &l : libs)
-            if (l.set_bands && l.set_bands(l.cplan, 21, 22, -65, -63, de)) {
-                fprintf(stderr, "%s: %s\n", l.path.c_str(), l.last_error());
-                return 3;
-            }
-    }
     auto launch = [&](Lib &l) {
         return c5 ? l.cpsd_dev(l.cplan, dx, f32 ? MSD_CF32 : MSD_CI16, doff, dlen, nfiles, T, dout)
                   : l.psd_dev(l.plan, dx, MSD_I16, doff, dlen, nfiles, T, dout, ld);
