@@ -126,13 +126,14 @@ struct IQ<float> {  // interleaved float32 I, Q (complex64)
     }
 };
 
-// int16 I/Q at 75 % overlap (C5) runs 4 waves per SIMD: 128 VGPRs with the [k][j1] pass-2 twiddle
-// table (its reads need no per-k index registers; 16 B of spills, outside the frame loop) — A/B
-// 12.27 → 11.79 ms.  The other variants keep 3 waves and the W256^m table (float32 I/Q at 4 waves
-// spills inside the loop, 12.33 → 14.55 ms; the [k][j1] table alone at 3 waves is 2 % slower)
+// int16 I/Q runs 4 waves per SIMD: 128 VGPRs with the [k][j1] pass-2 twiddle table (its reads need
+// no per-k index registers; 8-68 B of spills, outside the frame loop) — A/B at hop 1024 (C5)
+// 12.27 → 11.79 ms, hop 2048 6.38 → 6.19, hop 1000 13.05 → 12.53.  float32 I/Q keeps 3 waves and the
+// W256^m table (at 4 waves it spills inside the loop, 12.33 → 14.55 ms; the [k][j1] table alone at 3
+// waves is 2 % slower)
 template <typename T, int SH>
 struct CsTune {
-    static constexpr bool kW4 = std::is_same<T, int16_t>::value && SH == 4;
+    static constexpr bool kW4 = std::is_same<T, int16_t>::value;
     static constexpr int kWavesPerSimd = kW4 ? 4 : 1;  // launch-bounds minimum (1: no constraint)
 };
 

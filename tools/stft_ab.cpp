@@ -73,7 +73,9 @@ int main(int argc, char **argv) {
     // geometry: nfiles streams of n samples (complex samples for c5), N-point frames at hop
     const int64_t nfiles = c5 ? 1 : (getenv("STFT_AB_FILES") ? atoll(getenv("STFT_AB_FILES")) : 1440);
     const int64_t n = c5 ? 192000LL * 3600 * 3 + 3072 : 2880000;
-    const int64_t N = c5 ? 4096 : 1024, hop = c5 ? 1024 : 512, K = c5 ? 4096 : 513;
+    // STFT_AB_HOP (c5): another hop (C5: 1024, 75 % overlap)
+    const int64_t N = c5 ? 4096 : 1024, K = c5 ? 4096 : 513;
+    const int64_t hop = c5 ? (getenv("STFT_AB_HOP") ? atoll(getenv("STFT_AB_HOP")) : 1024) : 512;
     const double fs = c5 ? 192000.0 : 48000.0;
     const int64_t T = (n - N) / hop + 1, ld = c5 ? T : (T + 31) / 32 * 32;
     // STFT_AB_F32=1 (c5): float32 I/Q (the int16 samples / 32768) instead of int16
