@@ -73,6 +73,11 @@ struct msd_stream_plan {
     bool scanned = false;
     bool want_exact = true;  // msd_stream_set_exact_thresholds
     int32_t listed = -1;     // decisions only: frames listed by the last msd_stream_scan (host copy)
+    // pinned host block for the small per-step readbacks (counters, exit state, margins, chunk
+    // sums): the copies are asynchronous DMA and a decision point costs one stream sync, where a
+    // pageable destination costs a staged, host-synchronous copy each (≈ 18 µs per copy in the C5
+    // step's timeline)
+    void *h_pin = nullptr;
 };
 
 namespace msd {
@@ -84,6 +89,13 @@ struct SState {  // msd_stream_state
     int64_t fz, last_stop;
     double thr;
     int64_t reserved;
+};
+
+struct PinHdr {  // head of msd_stream_plan::h_pin, then margins [nseg], then chunk sums
+    int32_t changed, overflow;  // copied from d_active[nseg .. nseg + 1]
+    int32_t listed, computed;
+    int64_t count;
+    SState ex;
 };
 
 
@@ -910,6 +922,9 @@ void build_program(int64_t n, std::vector<int4> &rec) {
 
 using namespace msd;
 
+static PinHdr *pin_hdr(msd_stream_plan *p) { return static_cast<PinHdr *>(p->h_pin); }
+static double *pin_margin(msd_stream_plan *p) { return reinterpret_cast<double *>(pin_hdr(p) + 1); }
+static double *pin_chunks(msd_stream_plan *p) { return pin_margin(p) + (p->nseg > 0 ? p->nseg : 1); }
 static SState *st_in(msd_stream_plan *p) { return reinterpret_cast<SState *>(p->d_state); }
 static SState *st_out(msd_stream_plan *p) { return reinterpret_cast<SState *>(p->d_state) + p->nseg; }
 
@@ -982,6 +997,9 @@ int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total
     if ((e = hipMalloc(&p->d_count, sizeof(int64_t))) != hipSuccess) return cleanup(e, "hipMalloc count");
     if ((e = hipMalloc(&p->d_pos, sizeof(int64_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc pos");
     if ((e = hipMalloc(&p->d_chunks, sizeof(double) * nchunk)) != hipSuccess) return cleanup(e, "hipMalloc chunks");
+    if ((e = hipHostMalloc(&p->h_pin, sizeof(PinHdr) + sizeof(double) * (nseg1 + nchunk), hipHostMallocDefault)) !=
+        hipSuccess)
+        return cleanup(e, "hipHostMalloc stream readbacks");
     p->ntiles = (nl1 + FR_FRAMES - 1) / FR_FRAMES;
     p->nblk = (p->n_tail + nl1 + p->head_cap) / PB + 1;
     if ((e = hipMalloc(&p->d_need, sizeof(int32_t) * p->ntiles)) != hipSuccess) return cleanup(e, "hipMalloc need");
@@ -1012,6 +1030,7 @@ void msd_stream_plan_destroy(msd_stream_plan *p) {
                     p->d_eps, p->d_exact, p->d_list};
     for (void *b : bufs)
         if (b) hipFree(b);
+    if (p->h_pin) hipHostFree(p->h_pin);
     delete p;
 }
 
@@ -1051,8 +1070,9 @@ int msd_stream_chunk_sums(msd_stream_plan *p, int32_t use_mean, double mean, dou
         hipLaunchKernelGGL(chunk_sums_kernel<false>, dim3(blocks), dim3(256), 0, p->ctx->stream, p->d_x, x0, c0, nc,
                            p->n_total, 0.0, p->d_chunks);
     MSD_HIP(hipGetLastError());
-    MSD_HIP(hipMemcpyAsync(sums, p->d_chunks, sizeof(double) * nc, hipMemcpyDeviceToHost, p->ctx->stream));
+    MSD_HIP(hipMemcpyAsync(pin_chunks(p), p->d_chunks, sizeof(double) * nc, hipMemcpyDeviceToHost, p->ctx->stream));
     MSD_HIP(hipStreamSynchronize(p->ctx->stream));
+    std::memcpy(sums, pin_chunks(p), sizeof(double) * nc);
     return MSD_OK;
 }
 
@@ -1145,9 +1165,10 @@ int msd_stream_refine(msd_stream_plan *p, int32_t *computed) {
                                p->d_fresh, p->d_exact);
         }
         MSD_HIP(hipGetLastError());
-        MSD_HIP(hipMemcpyAsync(computed, count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        MSD_HIP(hipMemcpyAsync(&pin_hdr(p)->computed, count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         MSD_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), st));
         MSD_HIP(hipStreamSynchronize(st));
+        *computed = pin_hdr(p)->computed;
         return MSD_OK;
     }
     MSD_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), st));
@@ -1157,8 +1178,9 @@ int msd_stream_refine(msd_stream_plan *p, int32_t *computed) {
                            p->d_fresh, p->d_need, p->d_done, count);
     }
     MSD_HIP(hipGetLastError());
-    MSD_HIP(hipMemcpyAsync(computed, count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(&pin_hdr(p)->computed, count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     MSD_HIP(hipStreamSynchronize(st));
+    *computed = pin_hdr(p)->computed;
     return MSD_OK;
 }
 
@@ -1214,14 +1236,16 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
                                st_out(p), p->d_active, p->nseg, p->seg_len, p->frame0, P.F0, changed);
             MSD_HIP(hipGetLastError());
         }
-        int32_t hc[2];
-        MSD_HIP(hipMemcpyAsync(hc, changed, sizeof(hc), hipMemcpyDeviceToHost, st));
-        MSD_HIP(hipMemcpyAsync(&ex, st_out(p) + (p->nseg - 1), sizeof(SState), hipMemcpyDeviceToHost, st));
+        PinHdr *h = pin_hdr(p);
+        MSD_HIP(hipMemcpyAsync(&h->changed, changed, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        MSD_HIP(hipMemcpyAsync(&h->ex, st_out(p) + (p->nseg - 1), sizeof(SState), hipMemcpyDeviceToHost, st));
         if (p->decide)  // frames listed so far: a refine with none to compute needs no GPU round trip
-            MSD_HIP(hipMemcpyAsync(&p->listed, p->d_done + p->ntiles, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            MSD_HIP(hipMemcpyAsync(&h->listed, p->d_done + p->ntiles, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         MSD_HIP(hipStreamSynchronize(st));
-        if (hc[1]) return fail(MSD_ERR_CAPACITY, "msd_stream_scan: more runs in a segment than cap_per_seg");
-        if (hc[0] == 0) break;
+        ex = h->ex;
+        if (p->decide) p->listed = h->listed;
+        if (h->overflow) return fail(MSD_ERR_CAPACITY, "msd_stream_scan: more runs in a segment than cap_per_seg");
+        if (h->changed == 0) break;
         if (nround > p->nseg + 2 + R) return fail(MSD_ERR_INVALID, "msd_stream_scan: no fixed point");
     }
     if (p->cfg.adaptive && !p->decide) {
@@ -1258,14 +1282,13 @@ int msd_stream_runs(msd_stream_plan *p, msd_det *runs, int64_t cap, int64_t *cou
     hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(1024), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
                        p->d_count, p->d_pos);
     MSD_HIP(hipGetLastError());
-    int64_t n = 0;
-    MSD_HIP(hipMemcpyAsync(&n, p->d_count, sizeof(n), hipMemcpyDeviceToHost, st));
-    std::vector<double> mg(p->nseg);
-    MSD_HIP(hipMemcpyAsync(mg.data(), p->d_margin, sizeof(double) * p->nseg, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(&pin_hdr(p)->count, p->d_count, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(pin_margin(p), p->d_margin, sizeof(double) * p->nseg, hipMemcpyDeviceToHost, st));
     MSD_HIP(hipStreamSynchronize(st));
+    const int64_t n = pin_hdr(p)->count;
     *count = n;
     if (margin)
-        for (double v : mg) *margin = v < *margin ? v : *margin;
+        for (int64_t i = 0; i < p->nseg; ++i) *margin = pin_margin(p)[i] < *margin ? pin_margin(p)[i] : *margin;
     if (n > cap) return fail(MSD_ERR_CAPACITY, "msd_stream_runs: more runs than capacity");
     if (n > 0) {
         if (!runs) return fail(MSD_ERR_INVALID, "msd_stream_runs: null runs");
@@ -1353,17 +1376,16 @@ int msd_stream_detect_local(msd_stream_plan *p, int32_t exact_thresholds, msd_de
     hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(1024), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
                        p->d_count, p->d_pos);
     MSD_HIP(hipGetLastError());
-    int64_t nr = 0;
-    std::vector<double> mg((size_t)p->nseg);
-    MSD_HIP(hipMemcpyAsync(&nr, p->d_count, sizeof(nr), hipMemcpyDeviceToHost, st));
-    MSD_HIP(hipMemcpyAsync(mg.data(), p->d_margin, sizeof(double) * p->nseg, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(&pin_hdr(p)->count, p->d_count, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(pin_margin(p), p->d_margin, sizeof(double) * p->nseg, hipMemcpyDeviceToHost, st));
     MSD_HIP(hipStreamSynchronize(st));
-    for (double v : mg) *margin = v < *margin ? v : *margin;
+    const int64_t nr = pin_hdr(p)->count;
+    for (int64_t i = 0; i < p->nseg; ++i) *margin = pin_margin(p)[i] < *margin ? pin_margin(p)[i] : *margin;
     *count = nr;
     if (nr > cap) return fail(MSD_ERR_CAPACITY, "msd_stream_detect_local: more runs than capacity");
     if (nr == 0) return MSD_OK;
     if (!out) return fail(MSD_ERR_INVALID, "msd_stream_detect_local: null out");
-    MSD_HIP(hipMemcpy(out, p->d_out, sizeof(msd_det) * nr, hipMemcpyDeviceToHost));
+    if (!adaptive) MSD_HIP(hipMemcpy(out + (nr - 1), p->d_out + (nr - 1), sizeof(msd_det), hipMemcpyDeviceToHost));
     if (!adaptive && out[nr - 1].stop == n) {  // burst_stops gets len-1 (main.py:414-415)
         out[nr - 1].stop = n - 1;
         if (out[nr - 1].stop - out[nr - 1].start <= 0)
