@@ -56,7 +56,7 @@ struct msd_stream_plan {
     msd_det *d_out = nullptr;   // compacted runs [nseg*cap]
     int64_t *d_count = nullptr;
     int64_t *d_pos = nullptr;   // [nseg] runs emitted before each segment
-    double *d_chunks = nullptr; // chunk sums
+    double *d_chunks = nullptr; // chunk sums [nchunk] + the local path's mean, thr0
     int4 *d_prog = nullptr;     // fresh-threshold leaf records for windows of exactly W frames
     int32_t *d_need = nullptr;  // [ntiles] a scan used fresh thresholds in the tile
     int32_t *d_done = nullptr;  // [ntiles] the tile's exact thresholds are computed (+1: counter)
@@ -194,15 +194,30 @@ __device__ double wave_np_sum(const A &a, int64_t base, int64_t n) {
 template <bool SQ>
 __global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restrict__ x, int64_t x0,
                                                          int64_t first_chunk, int64_t nchunks, int64_t n_total,
-                                                         double mean, double *__restrict__ out) {
+                                                         double mean_v, const double *__restrict__ mean_ptr,
+                                                         double *__restrict__ out) {
     const int lane = threadIdx.x & 63;
     const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= nchunks) return;
+    const double mean = mean_ptr ? *mean_ptr : mean_v;  // the local path keeps the mean on the device
     const int64_t g = (first_chunk + c) * CHUNK;
     const int64_t m = n_total - g < CHUNK ? n_total - g : CHUNK;
     const double *p = x + (g - x0);
     const double r = SQ ? wave_chunk_sum(SqDevRef{p, mean}, 0, m) : wave_chunk_sum(ArrRef{p}, 0, m);
     if (lane == 0) out[c] = r;
+}
+
+// the whole stream's np.mean / thr0 from its chunk sums, as the host forms them (s = 0.0; s += chunk
+// sum, in order; mean = s / n; thr0 = mean + k * sqrt(s2 / n)), for the one-process path: no host
+// round trip between the two passes.  stats[0] = mean (STAGE 0), stats[1] = thr0 (STAGE 1).
+template <int STAGE>
+__global__ void stream_stats_kernel(const double *__restrict__ sums, int64_t nc, int64_t n, double k,
+                                    double *__restrict__ stats) {
+    if (threadIdx.x != 0) return;
+    double s = 0.0;
+    for (int64_t i = 0; i < nc; ++i) s += sums[i];
+    if (STAGE == 0) stats[0] = s / (double)n;
+    else stats[1] = stats[0] + k * sqrt(s / (double)n);
 }
 
 // ------------------------------------------------------------------ fresh thresholds
@@ -996,7 +1011,8 @@ int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total
     if ((e = hipMalloc(&p->d_margin, sizeof(double) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc margin");
     if ((e = hipMalloc(&p->d_count, sizeof(int64_t))) != hipSuccess) return cleanup(e, "hipMalloc count");
     if ((e = hipMalloc(&p->d_pos, sizeof(int64_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc pos");
-    if ((e = hipMalloc(&p->d_chunks, sizeof(double) * nchunk)) != hipSuccess) return cleanup(e, "hipMalloc chunks");
+    if ((e = hipMalloc(&p->d_chunks, sizeof(double) * (nchunk + 2))) != hipSuccess)
+        return cleanup(e, "hipMalloc chunks");
     if ((e = hipHostMalloc(&p->h_pin, sizeof(PinHdr) + sizeof(double) * (nseg1 + nchunk), hipHostMallocDefault)) !=
         hipSuccess)
         return cleanup(e, "hipHostMalloc stream readbacks");
@@ -1065,10 +1081,10 @@ int msd_stream_chunk_sums(msd_stream_plan *p, int32_t use_mean, double mean, dou
     const unsigned blocks = (unsigned)((nc + 3) / 4);
     if (use_mean)
         hipLaunchKernelGGL(chunk_sums_kernel<true>, dim3(blocks), dim3(256), 0, p->ctx->stream, p->d_x, x0, c0, nc,
-                           p->n_total, mean, p->d_chunks);
+                           p->n_total, mean, nullptr, p->d_chunks);
     else
         hipLaunchKernelGGL(chunk_sums_kernel<false>, dim3(blocks), dim3(256), 0, p->ctx->stream, p->d_x, x0, c0, nc,
-                           p->n_total, 0.0, p->d_chunks);
+                           p->n_total, 0.0, nullptr, p->d_chunks);
     MSD_HIP(hipGetLastError());
     MSD_HIP(hipMemcpyAsync(pin_chunks(p), p->d_chunks, sizeof(double) * nc, hipMemcpyDeviceToHost, p->ctx->stream));
     MSD_HIP(hipStreamSynchronize(p->ctx->stream));
@@ -1344,17 +1360,27 @@ int msd_stream_detect_local(msd_stream_plan *p, int32_t exact_thresholds, msd_de
         if ((rc = msd_stream_set_exact_thresholds(p, exact_thresholds))) return rc;
         if ((rc = msd_stream_fresh(p))) return rc;
     }
-    // np.mean / np.std of the whole stream (main.py:464-466, :399-400): s = 0.0; s += chunk sums
-    std::vector<double> sums((size_t)(n / CHUNK + 2));
-    int64_t nc = 0, c0 = 0;
-    if ((rc = msd_stream_chunk_sums(p, 0, 0.0, sums.data(), (int64_t)sums.size(), &nc, &c0))) return rc;
-    double s = 0.0;
-    for (int64_t i = 0; i < nc; ++i) s += sums[(size_t)i];
-    const double mean = s / (double)n;
-    if ((rc = msd_stream_chunk_sums(p, 1, mean, sums.data(), (int64_t)sums.size(), &nc, &c0))) return rc;
-    double s2 = 0.0;
-    for (int64_t i = 0; i < nc; ++i) s2 += sums[(size_t)i];
-    const double thr0 = mean + p->cfg.k_std * std::sqrt(s2 / (double)n);
+    // np.mean / np.std of the whole stream (main.py:464-466, :399-400): s = 0.0; s += chunk sums,
+    // both passes and the sums on the device (the protocol's msd_stream_chunk_sums does the same
+    // through the host for N ranks), one readback of thr0
+    double thr0;
+    {
+        DeviceGuard g(p->ctx->device);
+        hipStream_t st = p->ctx->stream;
+        const int64_t nc = (n + CHUNK - 1) / CHUNK;
+        const unsigned blocks = (unsigned)((nc + 3) / 4);
+        double *stats = p->d_chunks + (n / CHUNK + 2);
+        hipLaunchKernelGGL(chunk_sums_kernel<false>, dim3(blocks), dim3(256), 0, st, p->d_x, (int64_t)0, (int64_t)0, nc,
+                           n, 0.0, nullptr, p->d_chunks);
+        hipLaunchKernelGGL(stream_stats_kernel<0>, dim3(1), dim3(64), 0, st, p->d_chunks, nc, n, p->cfg.k_std, stats);
+        hipLaunchKernelGGL(chunk_sums_kernel<true>, dim3(blocks), dim3(256), 0, st, p->d_x, (int64_t)0, (int64_t)0, nc,
+                           n, 0.0, stats, p->d_chunks);
+        hipLaunchKernelGGL(stream_stats_kernel<1>, dim3(1), dim3(64), 0, st, p->d_chunks, nc, n, p->cfg.k_std, stats);
+        MSD_HIP(hipGetLastError());
+        MSD_HIP(hipMemcpyAsync(pin_chunks(p), stats + 1, sizeof(double), hipMemcpyDeviceToHost, st));
+        MSD_HIP(hipStreamSynchronize(st));
+        thr0 = pin_chunks(p)[0];
+    }
     *thr0_out = thr0;
     // the freeze / run scan to its fixed point, refined until it reads exact thresholds only
     const msd_stream_state clean{-1, -2, thr0, 0};
