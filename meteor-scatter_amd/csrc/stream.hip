@@ -210,12 +210,34 @@ __global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restric
 // the whole stream's np.mean / thr0 from its chunk sums, as the host forms them (s = 0.0; s += chunk
 // sum, in order; mean = s / n; thr0 = mean + k * sqrt(s2 / n)), for the one-process path: no host
 // round trip between the two passes.  stats[0] = mean (STAGE 0), stats[1] = thr0 (STAGE 1).
+__global__ __launch_bounds__(256) void fresh_clear_kernel(int32_t *__restrict__ need, int64_t n_need, int32_t need_v,
+                                                          int32_t *__restrict__ done, int64_t n_done,
+                                                          uint8_t *__restrict__ exact, int64_t n_exact) {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = i0; i < n_need; i += step) need[i] = need_v;
+    for (int64_t i = i0; i < n_done; i += step) done[i] = 0;
+    if (exact) {
+        uint32_t *e4 = reinterpret_cast<uint32_t *>(exact);  // hipMalloc'd: 4-B aligned
+        for (int64_t i = i0; i < n_exact / 4; i += step) e4[i] = 0u;
+        for (int64_t i = (n_exact / 4) * 4 + i0; i < n_exact; i += step) exact[i] = 0;
+    }
+}
+
+// The 256 threads stage the sums in LDS (independent loads), thread 0 adds them in order.
 template <int STAGE>
-__global__ void stream_stats_kernel(const double *__restrict__ sums, int64_t nc, int64_t n, double k,
-                                    double *__restrict__ stats) {
-    if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void stream_stats_kernel(const double *__restrict__ sums, int64_t nc, int64_t n,
+                                                           double k, double *__restrict__ stats) {
+    __shared__ double sh[2048];
     double s = 0.0;
-    for (int64_t i = 0; i < nc; ++i) s += sums[i];
+    for (int64_t b = 0; b < nc; b += 2048) {
+        const int64_t m = nc - b < 2048 ? nc - b : 2048;
+        for (int64_t i = threadIdx.x; i < m; i += 256) sh[i] = sums[b + i];
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int64_t i = 0; i < m; ++i) s += sh[i];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
     if (STAGE == 0) stats[0] = s / (double)n;
     else stats[1] = stats[0] + k * sqrt(s / (double)n);
 }
@@ -1137,12 +1159,12 @@ int msd_stream_fresh(msd_stream_plan *p) {
         const char *e = getenv("MSD_FRESH_ALL");
         return e && e[0] == '1';
     }();
-    MSD_HIP(hipMemsetAsync(p->d_need, 0, sizeof(int32_t) * p->ntiles, st));
-    if (all || p->ctx->fresh_all) MSD_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_need), 1, p->ntiles, st));
-    MSD_HIP(hipMemsetAsync(p->d_done, 0, sizeof(int32_t) * (p->ntiles + 1), st));
     // decisions-only: every frame predicted (with its error bound), exact ones listed by the scan
     p->decide = !p->want_exact && P.W > 0 && !(all || p->ctx->fresh_all);
-    if (p->decide) MSD_HIP(hipMemsetAsync(p->d_exact, 0, p->n_local, st));
+    // need = 0 (1 with MSD_FRESH_ALL), done = 0, exact = 0 (decisions only): one launch
+    hipLaunchKernelGGL(fresh_clear_kernel, dim3(512), dim3(256), 0, st, p->d_need, p->ntiles,
+                       (all || p->ctx->fresh_all) ? 1 : 0, p->d_done, p->ntiles + 1, p->decide ? p->d_exact : nullptr,
+                       p->n_local);
     // frames [0, jshort) have windows shorter than W: exact right away
     int64_t jshort = P.W - p->frame0;
     jshort = jshort < 0 ? 0 : (jshort > p->n_local ? p->n_local : jshort);
@@ -1372,10 +1394,10 @@ int msd_stream_detect_local(msd_stream_plan *p, int32_t exact_thresholds, msd_de
         double *stats = p->d_chunks + (n / CHUNK + 2);
         hipLaunchKernelGGL(chunk_sums_kernel<false>, dim3(blocks), dim3(256), 0, st, p->d_x, (int64_t)0, (int64_t)0, nc,
                            n, 0.0, nullptr, p->d_chunks);
-        hipLaunchKernelGGL(stream_stats_kernel<0>, dim3(1), dim3(64), 0, st, p->d_chunks, nc, n, p->cfg.k_std, stats);
+        hipLaunchKernelGGL(stream_stats_kernel<0>, dim3(1), dim3(256), 0, st, p->d_chunks, nc, n, p->cfg.k_std, stats);
         hipLaunchKernelGGL(chunk_sums_kernel<true>, dim3(blocks), dim3(256), 0, st, p->d_x, (int64_t)0, (int64_t)0, nc,
                            n, 0.0, stats, p->d_chunks);
-        hipLaunchKernelGGL(stream_stats_kernel<1>, dim3(1), dim3(64), 0, st, p->d_chunks, nc, n, p->cfg.k_std, stats);
+        hipLaunchKernelGGL(stream_stats_kernel<1>, dim3(1), dim3(256), 0, st, p->d_chunks, nc, n, p->cfg.k_std, stats);
         MSD_HIP(hipGetLastError());
         MSD_HIP(hipMemcpyAsync(pin_chunks(p), stats + 1, sizeof(double), hipMemcpyDeviceToHost, st));
         MSD_HIP(hipStreamSynchronize(st));
