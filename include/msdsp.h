@@ -82,6 +82,9 @@ int msd_set_option(msd_ctx *ctx, int option, int value);
  * 4 = Welch band powers, 5 = live detector, 6 = complex (I/Q) STFT, 7 = I/Q band delta,
  * 8 = stream fresh thresholds, 9 = stream scan. */
 int msd_timing_enable(msd_ctx *ctx, int enable);
+/* which kernels get events while timing is on: bit k = kernel id k (default all); a timed
+ * region that times only its roofline kernel carries no events around the others */
+int msd_timing_select(msd_ctx *ctx, uint32_t kernel_mask);
 int msd_timing_reset(msd_ctx *ctx);
 int msd_timing_get(msd_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
 

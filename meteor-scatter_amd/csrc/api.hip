@@ -38,7 +38,7 @@ int ensure_dyn_lds(const void *kernel, int bytes) {
 }
 
 KernelTimer::KernelTimer(msd_ctx *c, int k) : ctx(c), kernel(k) {
-    if (!ctx->timing) return;
+    if (!ctx->timing || !((ctx->timing_mask >> k) & 1u)) return;
     auto take = [&]() {
         hipEvent_t e = nullptr;
         if (!ctx->pool.empty()) {
@@ -246,6 +246,12 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
 int msd_timing_enable(msd_ctx *ctx, int enable) {
     if (!ctx) return fail(MSD_ERR_INVALID, "null ctx");
     ctx->timing = enable != 0;
+    return MSD_OK;
+}
+
+int msd_timing_select(msd_ctx *ctx, uint32_t kernel_mask) {
+    if (!ctx) return fail(MSD_ERR_INVALID, "null ctx");
+    ctx->timing_mask = kernel_mask;
     return MSD_OK;
 }
 

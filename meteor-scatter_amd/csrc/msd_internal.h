@@ -42,6 +42,7 @@ struct msd_ctx {
     hipEvent_t fence_ev = nullptr;      // cross-stream ordering (msd_fence)
     hipEvent_t join_ev = nullptr;       // cross-context ordering (msd_stream_wait), this ctx signalling
     bool timing = false;
+    uint32_t timing_mask = 0xffffffffu;  // msd_timing_select: kernel ids timed while timing is on
     bool force_generic = false;  // MSD_OPT_GENERIC_STFT
     bool fresh_all = false;      // MSD_OPT_FRESH_ALL
     std::vector<msd::EventPair> pending;  // recorded, not yet folded into totals

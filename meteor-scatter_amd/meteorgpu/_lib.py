@@ -151,6 +151,7 @@ _SIGS = [
     ("msd_memset_dev", C.c_int, [_P, _P, C.c_int, C.c_size_t]),
     ("msd_set_option", C.c_int, [_P, C.c_int, C.c_int]),
     ("msd_timing_enable", C.c_int, [_P, C.c_int]),
+    ("msd_timing_select", C.c_int, [_P, C.c_uint32]),
     ("msd_timing_reset", C.c_int, [_P]),
     ("msd_timing_get", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     ("msd_stft_plan_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_double, C.POINTER(_P)]),
@@ -318,6 +319,11 @@ class Context:
     def timing(self, enable: bool = True):
         check(self.lib.msd_timing_enable(self.h, 1 if enable else 0))
         self.timing_on = bool(enable)
+
+    def timing_select(self, kernels=None):
+        """time only these kernel ids (K_*) while timing is on; None: all"""
+        mask = 0xFFFFFFFF if kernels is None else sum(1 << int(k) for k in kernels)
+        check(self.lib.msd_timing_select(self.h, mask))
 
     def sibling(self) -> "Context":
         """A new context (own HIP stream) on the same device with this one's options and timing
