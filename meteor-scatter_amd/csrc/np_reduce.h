@@ -45,61 +45,27 @@ __device__ __forceinline__ double np_pairwise_leaf(const A &a, int64_t base, int
     return res;
 }
 
-// Iterative post-order walk of numpy's recursion tree over [base, base+n), n <= 8192
-// (one ufunc buffer chunk).  leaf(b, m) returns the sum of a leaf (m <= 128); the walk
-// combines the leaves exactly as numpy's recursion does.  The explicit stack lives in
-// scratch (a cold, single-thread path: detect.hip's leaf-table builder).
-constexpr int NP_TREE_DEPTH = 48;
+// Walk of numpy's recursion tree over [base, base+n), n <= 8192 (one ufunc buffer chunk), in
+// numpy's order (left subtree first).  leaf(b, m) returns the sum of a leaf (m <= 128); the walk
+// combines the leaves exactly as numpy's recursion does.  Compile-time recursion over the depth
+// (7 splits cover 8192): no stack array, so nothing lives in scratch (the iterative walk's
+// stack did: detect.hip's leaf-table builder, 1.2 KB of scratch per lane)
+template <int D, typename LeafFn>
+__device__ __forceinline__ double np_tree_rec(int64_t base, int64_t n, const LeafFn &leaf) {
+#pragma clang fp contract(off)
+    if constexpr (D == 0) {
+        return leaf(base, n);
+    } else {
+        if (n <= 128) return leaf(base, n);
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        const double l = np_tree_rec<D - 1>(base, n2, leaf);
+        return l + np_tree_rec<D - 1>(base + n2, n - n2, leaf);
+    }
+}
 template <typename LeafFn>
 __device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
-#pragma clang fp contract(off)
-    if (n <= 128) return leaf(base, n);
-    int64_t st_base[NP_TREE_DEPTH];
-    int st_n[NP_TREE_DEPTH];
-    double st_left[NP_TREE_DEPTH];
-    int st_state[NP_TREE_DEPTH];
-    int sp = 0;
-    st_base[0] = base;
-    st_n[0] = (int)n;
-    st_state[0] = 0;
-    double ret = 0.0;
-    while (sp >= 0) {
-        const int64_t b = st_base[sp];
-        const int m = st_n[sp];
-        if (m <= 128) {
-            ret = leaf(b, m);
-            --sp;
-            // deliver ret to the parent
-            while (sp >= 0) {
-                if (st_state[sp] == 1) {  // left finished: start the right half
-                    st_left[sp] = ret;
-                    st_state[sp] = 2;
-                    int n2 = st_n[sp] / 2;
-                    n2 -= n2 % 8;
-                    const int np1 = sp + 1;
-                    st_base[np1] = st_base[sp] + n2;
-                    st_n[np1] = st_n[sp] - n2;
-                    st_state[np1] = 0;
-                    sp = np1;
-                    break;
-                } else {  // state 2: both halves done
-                    ret = st_left[sp] + ret;
-                    --sp;
-                }
-            }
-            continue;
-        }
-        // internal node, first visit: descend left
-        st_state[sp] = 1;
-        int n2 = m / 2;
-        n2 -= n2 % 8;
-        const int np1 = sp + 1;
-        st_base[np1] = b;
-        st_n[np1] = n2;
-        st_state[np1] = 0;
-        sp = np1;
-    }
-    return ret;
+    return np_tree_rec<7>(base, n, leaf);
 }
 
 // numpy's recursion written as compile-time recursion over the depth (n <= 8192 needs at
