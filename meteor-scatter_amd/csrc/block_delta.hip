@@ -257,11 +257,18 @@ __global__ __launch_bounds__(256) void block_delta2_kernel(
             default: break;
         }
         __builtin_amdgcn_wave_barrier();
+        // band dB on the group's lane 0, noise dB on lane 1 (one float64 log10 issued per wave
+        // instead of two in a row); lane 0 takes lane 1's value by a shuffle of the whole wave
+        double e_db = 0.0;
+        if (sub < 2 && valid) {
+            const double e = (sub == 0 ? np_sum_small(ArrRef{pb}, 0, nband) : np_sum_small(ArrRef{pb}, nband, nnoise)) +
+                             1e-12;
+            e_db = 10.0 * log10(e);
+        }
+        const double nd_next = __shfl_down(e_db, 1, 64);
         if (sub == 0 && valid) {
-            const double be = np_sum_small(ArrRef{pb}, 0, nband) + 1e-12;
-            const double ne = np_sum_small(ArrRef{pb}, nband, nnoise) + 1e-12;
-            const double bd = 10.0 * log10(be);
-            const double nd = 10.0 * log10(ne);
+            const double bd = e_db;
+            const double nd = nd_next;
             const int64_t o = f * ld + b;
             if (band_db) band_db[o] = bd;
             if (noise_db) noise_db[o] = nd;
