@@ -120,23 +120,25 @@ __global__ __launch_bounds__(DT_THREADS, 4) void detect_kernel(const double *__r
     const double *d = delta + f * P.ld;
     const msd_det_cfg &cfg = P.cfg;
 
+    // a file that fits one LDS chunk (a 60 s file: 300 blocks) is staged once: the global sums,
+    // the fresh windows and the scan read it from LDS
+    const bool whole = nb <= chunk;
+    if (whole) {
+        for (int64_t i = tid; i < nb; i += DT_THREADS) c_delta[i] = d[i];
+        __syncthreads();
+    }
+    const double *src = whole ? c_delta : d;
+
     // ---- 1. global threshold (main.py:399-400, :464-466) ----
-    const double s1 = wg_np_sum(ArrRef{d}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
+    const double s1 = wg_np_sum(ArrRef{src}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
     const double gmean = s1 / (double)nb;
-    const double s2 = wg_np_sum(SqDevRef{d, gmean}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
+    const double s2 = wg_np_sum(SqDevRef{src, gmean}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
     const double gstd = sqrt(s2 / (double)nb);
     const double thr0 = gmean + cfg.k_std * gstd;
 
-    // ---- 2. fresh adaptive thresholds (main.py:475-480), all blocks in parallel; a file that
-    // fits one LDS chunk (a 60 s file: 300 blocks) has its windows read from LDS ----
+    // ---- 2. fresh adaptive thresholds (main.py:475-480), all blocks in parallel ----
     double *tf = thr + f * P.ld;
-    const bool whole = nb <= chunk;
     if (cfg.adaptive) {
-        if (whole) {
-            for (int64_t i = tid; i < nb; i += DT_THREADS) c_delta[i] = d[i];
-            __syncthreads();
-        }
-        const double *src = whole ? c_delta : d;
         const int64_t W = cfg.window_blocks;
         for (int64_t i = tid; i < nb; i += DT_THREADS) {
             if (i < cfg.fixed_init_blocks) {
