@@ -628,24 +628,57 @@ __global__ __launch_bounds__(256) void fresh_short_kernel(const double *__restri
     }
 }
 
-// decisions-only mode: the frames the marking pass listed, numpy-exact, one wave per frame
+// decisions-only mode: the frames the marking pass listed, numpy-exact, one 4-wave workgroup per
+// frame: wave w sums the window's 8192-element chunks w, w + 4, ... (numpy's pairwise tree per
+// chunk), and the chunk sums are added in order from 0.0 (s += chunk), as np.sum does; a window of
+// more than FL_MAXCH chunks is summed by wave 0 alone (wave_np_sum, the same association)
+constexpr int FL_MAXCH = 64;
 __global__ __launch_bounds__(256) void fresh_list_kernel(const double *__restrict__ x, FreshParams P,
                                                          const int32_t *__restrict__ list,
                                                          const int32_t *__restrict__ count, double *__restrict__ fresh,
                                                          uint8_t *__restrict__ exact) {
+#pragma clang fp contract(off)
+    __shared__ double csum[2][FL_MAXCH];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t n = *count;
-    for (int64_t q = (int64_t)blockIdx.x * 4 + w; q < n; q += (int64_t)gridDim.x * 4) {
+    for (int64_t q = blockIdx.x; q < n; q += gridDim.x) {
         const int64_t j = list[q];
         const int64_t i = P.frame0 + j;
         const int64_t len = i < P.W ? i : P.W;
         const int64_t base = P.n_tail + j - len;
-        const double m = wave_np_sum(ArrRef{x}, base, len) / (double)len;
-        const double v = wave_np_sum(SqDevRef{x, m}, base, len);
-        if (lane == 0) {
+        const int64_t nch = (len + NP_BUFSIZE - 1) / NP_BUFSIZE;
+        if (nch > FL_MAXCH) {
+            if (w == 0) {
+                const double m = wave_np_sum(ArrRef{x}, base, len) / (double)len;
+                const double v = wave_np_sum(SqDevRef{x, m}, base, len);
+                if (lane == 0) {
+                    fresh[j] = m + P.k * sqrt(v / (double)len);
+                    exact[j] = 1;
+                }
+            }
+            continue;
+        }
+        auto chunk_len = [&](int64_t c) { return len - c * NP_BUFSIZE < NP_BUFSIZE ? len - c * NP_BUFSIZE : NP_BUFSIZE; };
+        for (int64_t c = w; c < nch; c += 4) {
+            const double r = wave_chunk_sum(ArrRef{x}, base + c * NP_BUFSIZE, chunk_len(c));
+            if (lane == 0) csum[0][c] = r;
+        }
+        __syncthreads();
+        double s = 0.0;
+        for (int64_t c = 0; c < nch; ++c) s += csum[0][c];
+        const double m = s / (double)len;
+        for (int64_t c = w; c < nch; c += 4) {
+            const double r = wave_chunk_sum(SqDevRef{x, m}, base + c * NP_BUFSIZE, chunk_len(c));
+            if (lane == 0) csum[1][c] = r;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double v = 0.0;
+            for (int64_t c = 0; c < nch; ++c) v += csum[1][c];
             fresh[j] = m + P.k * sqrt(v / (double)len);
             exact[j] = 1;
         }
+        __syncthreads();  // csum is rewritten by the next frame
     }
 }
 
