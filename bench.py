@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=16, help="processes of the multi-core CPU baseline "
                     "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
+    ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 run appended to the line (key \"c5\")")
     ap.add_argument("--shard-day", action="store_true",
                     help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
                          "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "
@@ -240,14 +241,25 @@ C5_BAND, C5_NOISE = (950.0, 1050.0), (-3050.0, -2950.0)  # Hz from the SDR centr
 
 
 def main_c5(a, world, rank, local, job_of):
+    """--workload c5: the C5 line alone."""
+    from meteorgpu import _lib
+    ctx = _lib.Context(local)
+    job = job_of(ctx)
+    out = run_c5(a, ctx, job, rank, world)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if job is not None:
+        job.close()
+
+
+def run_c5(a, ctx, job, rank, world):
     """BASELINE config C5: a 24 h 192 kHz I/Q stream time-sharded over the GPUs (3 h of it per
     GPU; weak scaling: the stream is 3 h x N long).  A step = the whole path on every rank:
     two-sided 4096-point power spectrogram at 75 % overlap (frame-major float32, kept in HBM),
     the per-frame band / noise dB delta, and the reference's adaptive detector over the WHOLE
-    stream (meteorgpu.stream: halo, chunk-sum and shard-edge state exchanges over RCCL)."""
+    stream (meteorgpu.stream: halo, chunk-sum and shard-edge state exchanges over RCCL).
+    Returns the bench line (identical on every rank but cpu_baseline, rank 0 only)."""
     from meteorgpu import _lib, iq, stream, synth
-    ctx = _lib.Context(local)
-    job = job_of(ctx)
     shard = int(C5_FS * a.c5_seconds)
     n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
@@ -349,10 +361,7 @@ def main_c5(a, world, rank, local, job_of):
                                          f"(oracle/iq_oracle.py), 1 thread"}
     out["ranks_seen"] = job.ranks_seen() if job is not None else 1
     det.close()
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if job is not None:
-        job.close()
+    return out
 
 
 def main_files(a, world, rank, local, job_of):
@@ -408,7 +417,7 @@ def main_files(a, world, rank, local, job_of):
             job.close()
 
 
-def dry_run(rank, world):
+def dry_run(rank, world, files):
     """Launcher self-test without a GPU: the ranks share a random 128-byte id through the
     rendezvous file, each publishes the digest it saw, and rank 0 checks they all agree."""
     import hashlib
@@ -422,7 +431,13 @@ def dry_run(rank, world):
         launch.release(0, tag=f"seen{r}")
     launch.release(0)
     ok = all(d == hashlib.sha1(uid).digest() for d in seen)
-    print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": len(seen), "id_agreed": ok}), flush=True)
+    from meteorgpu.shard import shard_range
+    # the C4 strong-scaling pass the real run appends (key "strong_scaling"): one day of --files
+    # files over the ranks, contiguous slices
+    strong = {"files_total": files, "files_per_rank": [int(np.subtract(*shard_range(files, r, world)[::-1]))
+                                                       for r in range(world)], "scaling": "strong"}
+    print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": len(seen), "id_agreed": ok,
+                      "strong_scaling": strong}), flush=True)
     if not ok:
         sys.exit(1)
 
@@ -437,7 +452,7 @@ def main():
     if world != a.gpus:
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)")
     if a.dry_run:
-        return dry_run(rank, world)
+        return dry_run(rank, world, a.files)
     from meteorgpu import _lib
     ndev = _lib.device_count()
     if local >= ndev:
@@ -449,8 +464,6 @@ def main():
         return
 
     from meteorgpu import synth
-    from meteorgpu.batch import BatchPipeline
-
     pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
     mp_base = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
@@ -461,24 +474,112 @@ def main():
                    "sample": f"{mp_files} of the 60 s 48 kHz files on {a.cpu_procs} processes ({dt:.1f} s), "
                              f"same path as cpu_baseline; CPU: {cpu_model()}"}
     ctx = _lib.Context(local)
+    job = job_of(ctx)
+    from meteorgpu.shard import shard_range
     n = FS * SECONDS
-    if a.shard_day:  # C4 strong scaling: files [lo, hi) of one day
-        from meteorgpu.shard import shard_range
+    if a.shard_day:  # C4 strong scaling as the headline: files [lo, hi) of one day
         lo, hi = shard_range(a.files, rank, world)
     else:  # rank r holds day r (weak scaling)
         lo, hi = 0, a.files
+    r = run_c3(a, ctx, job, rank, world, pool, lo, hi, a.shard_day, detail=True)
+    F = hi - lo
+    samples = (a.files if a.shard_day else world * F) * n
+    out = {
+        "metric": "Msamples/s processed (48 kHz SDR stream) + % HBM roofline, 1/2/4/8 MI355X",
+        "value": round(samples * a.steps / r["elapsed"] / 1e6, 1),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(r["elapsed"] / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if a.shard_day else "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: {POOL} seeded 60 s 48 kHz int16 noise+ping recordings replicated over {F} files/GPU",
+        "config": {
+            "workload": "C3 day batch: 1440 x 60 s 48 kHz mono int16 per GPU; STFT 1024/512 density PSD "
+                        "(float32 [513][T]) + block band dB (0.2 s, n_fft 512 -> 1024-pt rFFT crop, bands 950-1050/2950-3050 Hz) + "
+                        "adaptive detector + per-hour counts (RCCL all-reduce)" if not a.no_spectrogram else
+                        "C3 day batch, detect-only",
+            "files_per_gpu": F,
+            "samples_per_file": n,
+            "frames_per_file": r["T"],
+            "bins": r["K"],
+            "parallelism": (f"one day of {a.files} files sharded over {world} GPU(s) (C4, strong scaling)"
+                            if a.shard_day else f"a day of files per GPU over {world} GPU(s) (weak scaling)")
+                           + ", 1 process per GPU",
+        },
+        "detections_per_step": r["detections"],
+    }
+    if "roofline" in r:
+        out["roofline"] = r["roofline"]
+    out["kernel_ms_per_step"] = r["kernel_ms"]
+    if not a.shard_day:
+        # BASELINE configs[3] (C4): the SAME 1440-file day sharded over the N ranks (strong scaling),
+        # measured after the weak-scaling line so that the driver's 1/2/4/8 runs carry both curves
+        if world > 1 or job is not None:
+            slo, shi = shard_range(a.files, rank, world)
+            rs = run_c3(a, ctx, job, rank, world, pool, slo, shi, True, detail=False)
+            strong = {"value": round(a.files * n * a.steps / rs["elapsed"] / 1e6, 1),
+                      "ms_per_step": round(rs["elapsed"] / a.steps * 1e3, 4), "files_total": a.files,
+                      "files_per_gpu_max": -(-a.files // world), "detections_per_step": rs["detections"],
+                      "hour_total": rs["hour_total"], "scaling": "strong", "steps": a.steps}
+            if "roofline" in rs:
+                strong["stft_kernel_ms"] = rs["roofline"]["kernel_ms"]
+        else:  # one rank: the strong-scaling configuration is the run above
+            strong = {"value": out["value"], "ms_per_step": out["ms_per_step"], "files_total": a.files,
+                      "files_per_gpu_max": a.files, "detections_per_step": r["detections"],
+                      "hour_total": r["hour_total"], "scaling": "strong", "steps": a.steps,
+                      "note": "N = 1: the same run as the headline line"}
+        strong["ranks_seen"] = job.ranks_seen() if job is not None else 1
+        out["strong_scaling"] = strong
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
+        v, dt = cpu_baseline(pool, a.cpu_files)
+        out["cpu_baseline"] = {
+            "value": round(v, 2),
+            "unit": "Msamples/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": f"{a.cpu_files} of the 60 s 48 kHz files ({dt:.1f} s): scipy.signal.spectrogram "
+                      f"1024/512 + main.py block loop + adaptive detector (oracle/), 1 thread",
+        }
+    if mp_base is not None:
+        out["cpu_baseline_multicore"] = mp_base
+    if not a.no_c5 and not a.shard_day:
+        # BASELINE configs[4] (C5) in the same run, after the C3 timed region: the driver's record
+        # then carries a C5 number of its own (the full line under "c5")
+        c5 = run_c5(a, ctx, job, rank, world)
+        out["c5"] = {k: c5[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "scaling",
+                                        "dtype", "roofline", "kernel_ms_per_step", "detections_per_step",
+                                        "state_rounds", "exact_threshold_frames", "config", "cpu_baseline",
+                                        "certification") if k in c5}
+    out["ranks_seen"] = job.ranks_seen() if job is not None else 1
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if job is not None:
+        job.close()
+
+
+def run_c3(a, ctx, job, rank, world, pool, lo, hi, one_day, detail):
+    """C3 / C4: files [lo, hi) of a day on this rank (one_day: of ONE day sharded over the ranks,
+    else day `rank`); warm-up, then a.steps timed steps.  Returns the max-over-ranks time, the
+    detections, the all-reduced hour total and (detail) the roofline and kernel breakdown.  The
+    pipeline is freed before returning."""
+    from meteorgpu import _lib
+    from meteorgpu.batch import BatchPipeline
+    n = FS * SECONDS
     F = hi - lo
     bp = BatchPipeline(ctx, F, n, FS, nperseg=NPERSEG, noverlap=NOVERLAP, freq_band=BAND, noise_band=NOISE,
                        with_spectrogram=not a.no_spectrogram, concurrent=a.concurrent_stages)
     for i in range(F):
-        bp.upload_file(i, pool[(lo + i + (0 if a.shard_day else rank)) % POOL])
-    # file i starts at minute i of the day: 2025-06-01 (one day sharded) or 2025-06-(1+r) (a day per rank)
+        bp.upload_file(i, pool[(lo + i + (0 if one_day else rank)) % POOL])
+    # file i starts at minute lo + i of the day: 2025-06-01 (one day sharded) or 2025-06-(1+r) (a day per rank)
     epoch = datetime.datetime(1970, 1, 1)
-    day0 = datetime.datetime(2025, 6, 1) + datetime.timedelta(days=0 if a.shard_day else rank)
+    day0 = datetime.datetime(2025, 6, 1) + datetime.timedelta(days=0 if one_day else rank)
     us = lambda t: (t - epoch) // datetime.timedelta(microseconds=1)  # noqa: E731
     bp.set_start_times(np.array([us(day0 + datetime.timedelta(minutes=lo + i)) for i in range(F)], np.int64),
                        us(day0))
-    job = job_of(ctx)
 
     def step():
         bp.run()
@@ -517,50 +618,13 @@ def main():
     hist = bp.hour_counts()
     assert int(hist.sum()) == total_dets, "hour histogram != detections"
     stft_ms, stft_launches = ctx.timing_get(_lib.K_STFT)
-    for c in bp.contexts:
-        c.timing_select(None)
-        c.timing_reset()
-    step()
-    sync_all()
-    blk_ms, blk_launches = bp.stage_ctx.timing_get(_lib.K_BLOCK)
-    det_ms, det_launches = bp.stage_ctx.timing_get(_lib.K_DSCAN)
-
-    samples = (a.files if a.shard_day else world * F) * n
-    value = samples * a.steps / elapsed / 1e6
-    out = {
-        "metric": "Msamples/s processed (48 kHz SDR stream) + % HBM roofline, 1/2/4/8 MI355X",
-        "value": round(value, 1),
-        "unit": "Msamples/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "strong" if a.shard_day else "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": f"synthetic: {POOL} seeded 60 s 48 kHz int16 noise+ping recordings replicated over {F} files/GPU",
-        "config": {
-            "workload": "C3 day batch: 1440 x 60 s 48 kHz mono int16 per GPU; STFT 1024/512 density PSD "
-                        "(float32 [513][T]) + block band dB (0.2 s, n_fft 512 -> 1024-pt rFFT crop, bands 950-1050/2950-3050 Hz) + "
-                        "adaptive detector + per-hour counts (RCCL all-reduce)" if not a.no_spectrogram else
-                        "C3 day batch, detect-only",
-            "files_per_gpu": F,
-            "samples_per_file": n,
-            "frames_per_file": bp.T,
-            "bins": bp.K,
-            "parallelism": (f"one day of {a.files} files sharded over {world} GPU(s) (C4, strong scaling)"
-                            if a.shard_day else f"a day of files per GPU over {world} GPU(s) (weak scaling)")
-                           + ", 1 process per GPU",
-        },
-        "detections_per_step": total_dets,
-    }
+    res = {"elapsed": elapsed, "detections": total_dets, "hour_total": int(hist.sum()), "T": bp.T, "K": bp.K}
     if not a.no_spectrogram and stft_launches:
         avg_s = stft_ms / stft_launches / 1e3
         alg_bytes = F * (n * 2 + bp.K * bp.T * 4)  # samples read once + spectrogram written once
         traffic, traffic_src = load_pmc_traffic("stft", files=F, nperseg=NPERSEG)
         achieved = alg_bytes / avg_s / 1e9
-        out["roofline"] = {
+        res["roofline"] = {
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -572,28 +636,23 @@ def main():
             "kernel_ms": round(avg_s * 1e3, 4),
             "algorithmic_bytes_per_launch": alg_bytes,
         }
-    out["kernel_ms_per_step"] = {
-        "stft": round(stft_ms / max(stft_launches, 1), 4),
-        "block_delta": round(blk_ms / max(blk_launches, 1), 4),
-        "detect": round(det_ms / max(det_launches, 1), 4),
-    }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
-        v, dt = cpu_baseline(pool, a.cpu_files)
-        out["cpu_baseline"] = {
-            "value": round(v, 2),
-            "unit": "Msamples/s",
-            "cores": 1,
-            "kind": "port",
-            "sample": f"{a.cpu_files} of the 60 s 48 kHz files ({dt:.1f} s): scipy.signal.spectrogram "
-                      f"1024/512 + main.py block loop + adaptive detector (oracle/), 1 thread",
+    for c in bp.contexts:
+        c.timing_select(None)
+        c.timing_reset()
+    if detail:
+        step()
+        sync_all()
+        blk_ms, blk_launches = bp.stage_ctx.timing_get(_lib.K_BLOCK)
+        det_ms, det_launches = bp.stage_ctx.timing_get(_lib.K_DSCAN)
+        res["kernel_ms"] = {
+            "stft": round(stft_ms / max(stft_launches, 1), 4),
+            "block_delta": round(blk_ms / max(blk_launches, 1), 4),
+            "detect": round(det_ms / max(det_launches, 1), 4),
         }
-    if mp_base is not None:
-        out["cpu_baseline_multicore"] = mp_base
-    out["ranks_seen"] = job.ranks_seen() if job is not None else 1
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if job is not None:
-        job.close()
+    for c in bp.contexts:
+        c.timing(False)
+    bp.close()
+    return res
 
 
 if __name__ == "__main__":

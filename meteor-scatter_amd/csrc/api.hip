@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <map>
 #include <set>
 #include <tuple>
 
@@ -26,14 +27,17 @@ int hip_fail(hipError_t e, const char *what) {
 }
 
 int ensure_dyn_lds(const void *kernel, int bytes) {
+    // the attribute is a per-kernel maximum: only ever raised, so a smaller request after a larger
+    // one (plans of different sizes sharing one instantiation) never lowers it under a later launch
     static std::mutex mu;
-    static std::set<std::tuple<const void *, int, int>> done;  // (kernel, device, bytes)
+    static std::map<std::pair<const void *, int>, int> set_to;  // (kernel, device) -> bytes set
     int dev = 0;
     MSD_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(mu);
-    if (done.count({kernel, dev, bytes})) return MSD_OK;
+    int &cur = set_to[{kernel, dev}];
+    if (bytes <= cur) return MSD_OK;
     MSD_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-    done.insert({kernel, dev, bytes});
+    cur = bytes;
     return MSD_OK;
 }
 

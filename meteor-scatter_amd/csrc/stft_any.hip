@@ -103,7 +103,52 @@ __device__ __forceinline__ void stockham(const C *__restrict__ src, C *__restric
     }
 }
 
-template <typename T, typename R>
+// the same pass in place on one buffer (float64 at nfft 16384: two M-point buffers would need 256 KB
+// of LDS, the workgroup has 160 KB): every thread first reads all its butterflies' inputs into
+// registers (M <= 8192: at most 32 complex values), the workgroup synchronises, then writes
+template <int R, typename C>
+__device__ __forceinline__ void stockham_inplace(C *__restrict__ buf, const C *__restrict__ tw, int M, int Ns) {
+    constexpr int NB = 32 / R;  // butterflies per thread at M = 8192
+    const int nbf = M / R;
+    C v[NB][R];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = threadIdx.x + b * SA_THREADS;
+        if (j < nbf)
+#pragma unroll
+            for (int q = 0; q < R; ++q) v[b][q] = buf[j + q * nbf];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = threadIdx.x + b * SA_THREADS;
+        if (j >= nbf) continue;
+        const int k = j & (Ns - 1);
+        if (Ns > 1) {
+            const int step = M / (Ns * R);
+#pragma unroll
+            for (int q = 1; q < R; ++q) v[b][q] = cmul(v[b][q], tw[k * q * step]);
+        }
+        if constexpr (R == 4) {
+            const C t0 = cadd(v[b][0], v[b][2]), t1 = csub(v[b][0], v[b][2]), t2 = cadd(v[b][1], v[b][3]),
+                    t3 = mul_mi(csub(v[b][1], v[b][3]));
+            v[b][0] = cadd(t0, t2);
+            v[b][1] = cadd(t1, t3);
+            v[b][2] = csub(t0, t2);
+            v[b][3] = csub(t1, t3);
+        } else {
+            const C a = v[b][0];
+            v[b][0] = cadd(a, v[b][1]);
+            v[b][1] = csub(a, v[b][1]);
+        }
+        const int o = (j - k) * R + k;
+#pragma unroll
+        for (int q = 0; q < R; ++q) buf[o + q * Ns] = v[b][q];
+    }
+}
+
+// INPLACE: one M-point LDS buffer (stockham_inplace) instead of two
+template <typename T, typename R, bool INPLACE>
 __global__ __launch_bounds__(SA_THREADS) void stft_any_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len, int nperseg, int hop,
     int M, int logM, R scale, int detrend, const R *__restrict__ win, const typename Cx<R>::t *__restrict__ tw,
@@ -111,7 +156,7 @@ __global__ __launch_bounds__(SA_THREADS) void stft_any_kernel(
     using C = typename Cx<R>::t;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     C *A = reinterpret_cast<C *>(smem);
-    C *B = A + M;
+    C *B = INPLACE ? A : A + M;
     __shared__ double red[SA_THREADS / 64];
 
     const int64_t f = blockIdx.y;
@@ -151,6 +196,18 @@ __global__ __launch_bounds__(SA_THREADS) void stft_any_kernel(
     // ---- radix-4 passes (one radix-2 first when log2 M is odd), ping-pong A <-> B
     C *src = A, *dst = B;
     int Ns = 1;
+    if constexpr (INPLACE) {
+        if (logM & 1) {
+            stockham_inplace<2>(A, tw, M, Ns);
+            Ns *= 2;
+            __syncthreads();
+        }
+        for (int p = 0; p < logM / 2; ++p) {
+            stockham_inplace<4>(A, tw, M, Ns);
+            Ns *= 4;
+            __syncthreads();
+        }
+    } else {
     if (logM & 1) {
         stockham<2>(src, dst, tw, M, Ns);
         Ns *= 2;
@@ -166,6 +223,7 @@ __global__ __launch_bounds__(SA_THREADS) void stft_any_kernel(
         C *tmp = src;
         src = dst;
         dst = tmp;
+    }
     }
     // ---- real split: X[k] = (Z[k] + conj Z[M-k]) / 2 + W_{2M}^k (Z[k] - conj Z[M-k]) / (2i)
     for (int k = threadIdx.x; k < K; k += SA_THREADS) {
@@ -185,8 +243,14 @@ int launch_any_t(msd_stft_plan *p, const void *x, const int64_t *off, const int6
                  int64_t ld) {
     using C = typename Cx<R>::t;
     const int M = p->M;
-    const int lds = 2 * M * (int)sizeof(C);
-    auto kern = stft_any_kernel<T, R>;
+    // two ping-pong buffers where they fit beside the static LDS, else one (in-place passes);
+    // M <= 8192 (nfft <= 16384), so one buffer always fits (float64: 128 KB)
+    constexpr int kLdsMax = 160 * 1024 - 1024;
+    const bool inplace = 2 * M * (int)sizeof(C) > kLdsMax;
+    if (M * (int)sizeof(C) > kLdsMax || M > 8192)
+        return fail(MSD_ERR_UNSUPPORTED, "stft: nfft too large for one workgroup's LDS");
+    const int lds = (inplace ? 1 : 2) * M * (int)sizeof(C);
+    auto kern = inplace ? stft_any_kernel<T, R, true> : stft_any_kernel<T, R, false>;
     if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(kern), lds)) return rc;
     if (ld > 0x7fffffffLL || nfiles > 65535) return fail(MSD_ERR_UNSUPPORTED, "stft: grid too large for this shape");
     int logM = 0;

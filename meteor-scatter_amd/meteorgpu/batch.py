@@ -191,6 +191,16 @@ class BatchPipeline:
         self.d_hist.download(out)
         return out[: self.nbuckets]
 
+    def close(self):
+        """Frees the plans and the device buffers (after the context's stream has drained)."""
+        self.ctx.synchronize()
+        for pl in (self.stft, self.blocks):
+            pl.close()
+        for b in (self.d_x, self.d_off, self.d_len, self.d_nb, self.d_spec, self.d_delta, self.d_band, self.d_noise,
+                  self.d_thr, self.d_dets, self.d_counts, self.d_margin, self.d_status, self.d_start_us, self.d_hist):
+            if b is not None:
+                b.free()
+
 
 class Communicator:
     """RCCL communicator over the ranks of one job (one process per GPU).  The

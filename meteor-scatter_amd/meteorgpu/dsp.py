@@ -221,8 +221,8 @@ def spectrogram(x, fs=1.0, window="hann", nperseg=None, noverlap=None, nfft=None
     As scipy: nperseg defaults to 256 and shrinks (with scipy's warning) to a shorter input;
     noverlap defaults to nperseg // 8; nfft >= nperseg zero-pads each segment.  nfft must be a
     power of two in [16, 16384].  Returns (f, t, Sxx) with Sxx [nfft//2+1, T] in scipy's output
-    precision: float32 for u8 / i16 / f32 input, float64 for i32 / i64 / f64 (computed in
-    float64 then)."""
+    precision, np.result_type(x, np.complex64): float32 for u8 / i16 / u16 / f32 input, float64 for
+    i32 / u32 / i64 / f64 (computed in float64 then)."""
     import warnings
     x = np.asarray(x)
     if isinstance(window, tuple):
@@ -235,6 +235,9 @@ def spectrogram(x, fs=1.0, window="hann", nperseg=None, noverlap=None, nfft=None
         raise NotImplementedError("only detrend='constant', one-sided, density, mode='psd' are implemented")
     if np.iscomplexobj(x):
         raise NotImplementedError("complex (two-sided) input: use meteorgpu.iq")
+    # scipy's output precision: np.result_type(x, np.complex64) (complex128 for i32 / u32 / i64 / u64 /
+    # f64 input), decided on the caller's dtype before any conversion for the kernel
+    double = np.result_type(x.dtype, np.complex64) == np.complex128
     if x.dtype == np.int64:
         x = x.astype(np.float64)  # same values up to 2^53; scipy computes these in float64 too
     n = x.shape[0]
@@ -254,7 +257,6 @@ def spectrogram(x, fs=1.0, window="hann", nperseg=None, noverlap=None, nfft=None
     if nfft < 16 or nfft > 16384 or nfft & (nfft - 1):
         raise NotImplementedError("nfft must be a power of two in [16, 16384]")
     hop = nperseg - noverlap
-    double = x.dtype in (np.int32, np.float64)  # np.result_type(x, np.complex64) is complex128
     w64 = hann_periodic(nperseg)
     wc = w64.astype(np.complex128 if double else np.complex64)  # _spectral_helper casts the window
     scale = float(np.real(1.0 / (fs * (wc * wc).sum())))

@@ -13,8 +13,9 @@ Two ways in:
     key, waits for all of them, and returns the first failing exit code (the others are then
     terminated).  ``bench.py --gpus N`` uses it when WORLD_SIZE is unset.
   * an external launcher (``python -m torch.distributed.run ... bench.py``) sets the same
-    variables; the rendezvous key is then derived from its run id, the shared parent PID and
-    MASTER_PORT, which every worker of one launch has in common.
+    variables; the rendezvous key is then derived from its run id and restart count, the shared
+    parent PID and MASTER_PORT, which every worker of one launch attempt has in common.  Jobs
+    must be single-node (LOCAL_WORLD_SIZE == WORLD_SIZE, checked).
 """
 from __future__ import annotations
 
@@ -55,9 +56,22 @@ def rdzv_key() -> str:
     k = os.environ.get("MSD_RDZV_KEY")
     if k:
         return k
-    raw = "|".join((os.environ.get("TORCHELASTIC_RUN_ID", ""), str(os.getppid()),
-                    os.environ.get("MASTER_ADDR", ""), os.environ.get("MASTER_PORT", "")))
+    check_single_node()
+    # the restart count separates the attempts of an elastic job: a failed attempt may leave its
+    # file behind (no release()), and the next attempt's ranks must not read the old RCCL id
+    raw = "|".join((os.environ.get("TORCHELASTIC_RUN_ID", ""), os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"),
+                    str(os.getppid()), os.environ.get("MASTER_ADDR", ""), os.environ.get("MASTER_PORT", "")))
     return hashlib.sha1(raw.encode()).hexdigest()[:16]
+
+
+def check_single_node() -> None:
+    """The file rendezvous needs every rank on one node (one shared directory, one parent PID):
+    refuse a launch whose LOCAL_WORLD_SIZE differs from WORLD_SIZE."""
+    world = os.environ.get("WORLD_SIZE")
+    local = os.environ.get("LOCAL_WORLD_SIZE")
+    if world is not None and local is not None and int(local) != int(world):
+        raise RuntimeError(f"meteorgpu.launch: single-node jobs only (LOCAL_WORLD_SIZE={local}, "
+                           f"WORLD_SIZE={world}); the RCCL id rendezvous goes through a node-local file")
 
 
 def rdzv_path(tag: str = "rccl") -> str:

@@ -31,8 +31,14 @@ def _bench(*args, timeout=240):
 
 
 def test_spawn_c3():
-    d = _bench("--files", "16")
+    """the default line: C3 (weak), the C4 strong-scaling pass over the same ranks, and C5 appended"""
+    d = _bench("--files", "16", "--c5-seconds", "60")
     assert d["scaling"] == "weak" and d["config"]["files_per_gpu"] == 16 and d["roofline"]["frac"] > 0
+    s = d["strong_scaling"]
+    assert s["scaling"] == "strong" and s["files_total"] == 16 and s["ranks_seen"] == 1 and s["value"] > 0
+    assert s["hour_total"] == s["detections_per_step"] == d["detections_per_step"]  # same day at N = 1
+    c5 = d["c5"]
+    assert c5["value"] > 0 and c5["roofline"]["frac"] > 0 and c5["detections_per_step"] > 0
 
 
 def test_spawn_c4_shard_day():

@@ -39,6 +39,10 @@ def _signal(fs, n, dtype, seed):
         return x / 32768.0
     if np.dtype(dtype) == np.int32:
         return x.astype(np.int32) * 65536
+    if np.dtype(dtype) == np.uint32:
+        return (x.astype(np.int64) + 32768).astype(np.uint32) * 65536
+    if np.dtype(dtype) == np.uint16:
+        return (x.astype(np.int32) + 32768).astype(np.uint16)
     return x
 
 
@@ -65,6 +69,10 @@ CASES = [
     (48000, 1024, 512, 1024, np.int32, 48000 * 3),     # float64 path (scipy: complex128)
     (48000, 4096, 1024, 4096, np.float64, 48000 * 3),
     (48000, 2048, 0, 2048, np.uint8, 48000 * 2),
+    (48000, 16384, 8192, 16384, np.float64, 48000 * 4),  # float64 nfft 16384: one in-place LDS buffer
+    (48000, 8192, 2048, 16384, np.int32, 48000 * 2),     # float64, zero padding to 16384
+    (48000, 1024, 512, 1024, np.uint32, 48000 * 2),      # scipy: complex128 (np.result_type), float64 out
+    (48000, 1024, 512, 1024, np.uint16, 48000 * 2),      # scipy: complex64, float32 out
 ]
 
 
@@ -96,6 +104,17 @@ def test_short_input_shrinks_nperseg(n):
     assert S.shape == Sr.shape == (513, 1)
     np.testing.assert_array_equal(t, tr)
     assert _frame_err(S, Sr) <= SPEC_TOL
+
+
+def test_dyn_lds_attribute_only_grows():
+    """one stft_any instantiation serves plans of different nfft: a large plan, a small one, then
+    the large one again must launch (the LDS attribute is never lowered under a later launch)"""
+    x = _signal(6000, 6000 * 8, np.int16, seed=5)
+    for nfft in (8192, 1024, 8192):
+        fr, tr, Sr = sp_spec(x, fs=6000, window="hann", nperseg=1000, noverlap=500, nfft=nfft, scaling="density",
+                             mode="psd")
+        f, t, S = dsp.spectrogram(x, fs=6000, window="hann", nperseg=1000, noverlap=500, nfft=nfft)
+        assert S.shape == Sr.shape and _frame_err(S, Sr) <= SPEC_TOL
 
 
 def test_shape_errors_match_scipy():

@@ -28,7 +28,11 @@ def test_bench_spawns_n_ranks(n, tmp_path):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # only rank 0 prints
     d = json.loads(lines[0])
+    strong = d.pop("strong_scaling")
     assert d == {"dry_run": True, "n_gpus": n, "ranks_seen": n, "id_agreed": True}
+    # the C4 (strong scaling) pass the real N-rank line carries: one 1440-file day over the n ranks
+    assert strong["scaling"] == "strong" and strong["files_total"] == 1440
+    assert sum(strong["files_per_rank"]) == 1440 and max(strong["files_per_rank"]) == -(-1440 // n)
     assert not list(tmp_path.iterdir())  # rendezvous files cleaned up
 
 
@@ -85,3 +89,20 @@ def test_env_and_keys(monkeypatch, tmp_path):
     assert launch.share_bytes(1, lambda: b"", tag="x") == b"abc"
     launch.release(0, tag="x")
     assert not list(tmp_path.iterdir())
+
+
+def test_rdzv_key_restart_and_single_node(monkeypatch):
+    """an elastic restart gets a new key (a failed attempt's file is never read), and a multi-node
+    launch is refused (the rendezvous file is node-local)"""
+    from meteorgpu import launch
+    monkeypatch.delenv("MSD_RDZV_KEY", raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    monkeypatch.setenv("MASTER_PORT", "1234")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    k0 = launch.rdzv_key()
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    assert launch.rdzv_key() != k0
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    with pytest.raises(RuntimeError, match="single-node"):
+        launch.rdzv_key()

@@ -47,6 +47,7 @@ def test_noise_floor_golden(golden_dir):
 @pytest.mark.parametrize("NFFT,fs,dtype,seconds", [
     (2048, 5000, np.int16, 8.0), (1024, 5000, np.int16, 8.0), (256, 6000, np.int16, 8.0),
     (512, 5000, np.float32, 8.0), (4096, 5000, np.int16, 8.0), (8192, 5000, np.float64, 8.0),
+    (16384, 5000, np.int16, 12.0),  # float64 at nfft 16384: the in-place LDS passes (2 buffers = 256 KB)
     (2048, 5000, np.int16, 0.3)])  # the last: shorter than NFFT, zero-padded to one frame
 def test_specgram_vs_mlab(NFFT, fs, dtype, seconds):
     from meteorgpu import legacy, synth
