@@ -341,6 +341,13 @@ def run_c5(a, ctx, job, rank, world):
         "detections_per_step": int(len(res.detections)),
         "state_rounds": int(res.rounds),
         "exact_threshold_frames": int(res.refined),
+        # every step certifies each decision against the float64 reference and recomputes in float64
+        # the delta the uncertain ones depend on (meteorgpu.iq.IQShardDetector.detect)
+        "certification": {"certified": bool(res.certified), "near_tie": bool(res.near_tie),
+                          "uncertain_before_refinement": int(res.uncertain_initial),
+                          "refined_delta_frames": int(res.refined_delta_frames),
+                          "detector_passes": int(res.detector_passes),
+                          "decision_bound_db": float(res.decision_bound), "min_slack_db": float(res.min_slack)},
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": c5_traffic[0], "traffic_source": c5_traffic[1],

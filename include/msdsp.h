@@ -210,6 +210,11 @@ int msd_cstft_set_detrend(msd_cstft_plan *plan, int detrend);
 int64_t msd_cstft_frames(const msd_cstft_plan *plan, int64_t n);
 int msd_cstft_psd_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                       int64_t nstreams, int64_t max_frames, float *out);
+/* the same, plus (etot != NULL) each frame's total power sum_k out[k] as 16 float32 partial sums,
+ * etot[(s*max_frames + t)*16 + i] (device): Parseval's input norm for the fp32 FFT's per-bin error
+ * bound (msd_iq_band_delta_bound_dev) */
+int msd_cstft_psd_energy_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                             int64_t nstreams, int64_t max_frames, float *out, float *etot);
 /* one stream, host buffers: n complex samples in, out float32 [T][N] */
 int msd_cstft_psd(msd_cstft_plan *plan, const void *x, int dtype, int64_t n, float *out, int64_t *frames);
 
@@ -225,6 +230,14 @@ int msd_cstft_psd(msd_cstft_plan *plan, const void *x, int dtype, int64_t n, flo
 int msd_iq_band_delta_dev(msd_ctx *ctx, const float *spec, int64_t nstreams, int64_t max_frames,
                           const int64_t *frames, int32_t nperseg, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
                           int32_t noise_hi, double *band_db, double *noise_db, double *delta, int64_t ld);
+/* the same plus ed[s*ld + t] (device float64): a bound on |delta - delta_ref| against the float64
+ * reference (scipy's spectrogram of complex128 input, its band sums and dB), from the standard
+ * rounding-error model of the fp32 FFT and the frame energies etot of msd_cstft_psd_energy_dev
+ * (stream.hip IQ_CHAIN); +inf where a band touches bins -1..1 (the detrend's DC term). */
+int msd_iq_band_delta_bound_dev(msd_ctx *ctx, const float *spec, const float *etot, int64_t nstreams,
+                                int64_t max_frames, const int64_t *frames, int32_t nperseg, int32_t band_lo,
+                                int32_t band_hi, int32_t noise_lo, int32_t noise_hi, double *band_db, double *noise_db,
+                                double *delta, double *ed, int64_t ld);
 
 /* -------------------------- C5: the detector over one long stream, time-sharded over ranks
  * get_detections_adaptive() (dsp/src/main.py:450-522) and get_detections() (:396-448) over
@@ -256,7 +269,8 @@ typedef struct {
     int64_t freeze_until; /* freeze_until_idx (main.py:455), -1 initially             */
     int64_t last_stop;    /* last frame of the last run, -2 if there is none           */
     double thr;           /* the `threshold` variable after the previous frame         */
-    int64_t reserved;
+    int64_t src;          /* the frame whose fresh threshold thr is; -1: thr0          */
+    double thr_err;       /* certification: thr's error bound against the reference  */
 } msd_stream_state;
 int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total, int64_t frame0, int64_t n_local,
                            int64_t seg_len, int64_t cap_per_seg, int64_t head_frames, msd_stream_plan **out);
@@ -301,6 +315,36 @@ int msd_stream_db(msd_stream_plan *plan, msd_det *dets, int64_t n);
  * reference: MSD_ERR_INDEX (empty global input), MSD_ERR_ASSERT (zero-duration last run). */
 int msd_stream_detect_local(msd_stream_plan *plan, int32_t exact_thresholds, msd_det *out, int64_t cap,
                             int64_t *count, double *thr0_out, double *margin, int32_t *rounds, int32_t *refined);
+
+/* Certification against the float64 reference (C5: delta from the fp32 spectrogram).  With
+ * msd_stream_set_certify(plan, 1) every scan also checks each decision delta > thr of the final
+ * trajectory against error bounds: ed per frame (|delta - delta_ref|, written by
+ * msd_iq_band_delta_bound_dev into msd_stream_error_buffers' local part; halos exchanged like
+ * delta's; 0 = exact), the fresh thresholds' bound mean(ed) + |k| rms(ed) over their window
+ * (computed by msd_stream_fresh), and thr0's over the whole stream (msd_stream_set_terr0 from the
+ * ranks' msd_stream_ed_sums; msd_stream_detect_local computes it itself).  A decision with
+ * |delta - thr| <= ed + threshold bound (+ the predictor's bound, decisions only) is uncertain;
+ * msd_stream_certificate returns their count, the smallest slack, the largest error zone (ed +
+ * threshold bound) of any decision and up to cap of them as
+ * (global frame, frame whose window gave the threshold, -1 = thr0).  Zero uncertain decisions:
+ * the detections are the reference's. */
+int msd_stream_set_certify(msd_stream_plan *plan, int32_t on);
+int msd_stream_error_buffers(msd_stream_plan *plan, double **ed, double **tail, double **head);
+int msd_stream_ed_sums(msd_stream_plan *plan, double *sum_ed, double *sum_ed2);
+int msd_stream_set_terr0(msd_stream_plan *plan, double sum_ed, double sum_ed2);
+int msd_stream_certificate(msd_stream_plan *plan, int64_t *uncertain, double *min_slack, double *max_zone,
+                           int64_t *frames, int64_t *srcs, int64_t cap, int64_t *listed);
+/* The refinement of uncertain decisions: delta of the frames in `ranges` ([nranges][2] host
+ * int64, [first, end) frame indices, sorted and disjoint; frame t starts at complex sample t*hop
+ * of x) recomputed in float64 from the samples -- the reference's quantity (scipy spectrogram of
+ * complex128 input, periodic Hann, constant detrend, density; band sums in np.sum order;
+ * 10*log10(E + 1e-12)) by a direct DFT of the band bins (blocks of gcd(nperseg, hop) samples, the
+ * Hann window as three bin taps) -- into delta[t] and its error bound against the reference into
+ * ed[t] (device float64).  x: device interleaved I/Q (MSD_CI16 or MSD_CF32), n_samples complex
+ * samples.  Synchronous. */
+int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg, int64_t hop,
+                       double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo, int32_t noise_hi,
+                       const int64_t *ranges, int64_t nranges, double *delta, double *ed);
 
 /* ------------------------------------------- a10: legacy spectrogram noise floor
  * prime_detection.py:65-91: band_power = np.sum(Pxx[noise_band]) sums the spectrogram over

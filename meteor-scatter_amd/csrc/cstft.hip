@@ -141,11 +141,15 @@ struct CsTune {
 // Thread j holds z[j + 256 r]; the next frame of the same stream needs z[j + 256 (r + SH)],
 // so with SH > 0 it keeps raw[SH..15] (shifted down) and loads only raw[16-SH..15]: each
 // sample is loaded once per workgroup instead of N / hop times.
-template <typename T, int SH>
+// EN: also the frame's total power in 16 partial sums, etot[g][16] (wave w, row r of 16 lanes at
+// 4 w + r): by Parseval the input norm behind the fp32 FFT's per-bin error bound (the C5 detector's
+// delta error bound, msd_iq_band_delta_bound_dev) -- 15 adds per thread, one row DPP reduction and
+// one 4-lane store per wave and frame
+template <typename T, int SH, bool EN>
 __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft4096_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len, int64_t nstreams,
     int64_t max_frames, int64_t total, int64_t per, int hop, int detrend, const float *__restrict__ g_win,
-    const float2 *__restrict__ g_tw, float *__restrict__ out) {
+    const float2 *__restrict__ g_tw, float *__restrict__ out, float *__restrict__ etot) {
     using io = IQ<T>;
     __shared__ float2 buf[CS_LDS_F2];
     // pass-2 twiddles W256^(j1 k).  kW4: at k * 16 + j1 — a half-wave reads 16 consecutive entries
@@ -254,10 +258,16 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
             // 64-bit address arithmetic; streaming (non-temporal) stores, written once (A/B: -1 to -2 %)
             const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
                 reinterpret_cast<float *>(uniform_i64(reinterpret_cast<int64_t>(of))), 0, CS_N * 4, 0x00020000);
+            float esum = 0.f;
 #pragma unroll
             for (int k2b = 0; k2b < 16; ++k2b) {
                 const float pw = v[k2b].x * v[k2b].x + v[k2b].y * v[k2b].y;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pw), rsrc, 4 * tid, 1024 * k2b, 2 /* nt */);
+                if constexpr (EN) esum += pw;
+            }
+            if constexpr (EN) {
+                esum = row_sum_f(esum);
+                if ((lane & 15) == 0) etot[g * 16 + wave * 4 + (lane >> 4)] = esum;
             }
             // no barrier at the end: the next frame writes buf / red only after its first
             // barrier, which every wave reaches after its pass-3 reads of this frame
@@ -347,6 +357,11 @@ int64_t msd_cstft_frames(const msd_cstft_plan *p, int64_t n) {
 
 int msd_cstft_psd_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len,
                       int64_t nstreams, int64_t max_frames, float *out) {
+    return msd_cstft_psd_energy_dev(p, x, dtype, off, len, nstreams, max_frames, out, nullptr);
+}
+
+int msd_cstft_psd_energy_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                             int64_t nstreams, int64_t max_frames, float *out, float *etot) {
     if (!p || (nstreams > 0 && (!x || !off || !len || !out))) return fail(MSD_ERR_INVALID, "msd_cstft_psd_dev: null");
     if (dtype != MSD_CI16 && dtype != MSD_CF32) return fail(MSD_ERR_UNSUPPORTED, "cstft: dtype must be CI16 or CF32");
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
@@ -364,20 +379,22 @@ int msd_cstft_psd_dev(msd_cstft_plan *p, const void *x, int dtype, const int64_t
         const int64_t per = (total + wgs - 1) / wgs;
         wgs = (total + per - 1) / per;
         hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
-                           max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out);
+                           max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out, etot);
     };
     const int sh = p->hop % 256 == 0 ? p->hop / 256 : 0;
-    if (dtype == MSD_CI16) {
-        const auto *xp = static_cast<const int16_t *>(x);
-        if (sh == 4) launch(cstft4096_kernel<int16_t, 4>, xp);       // 75 % overlap (C5)
-        else if (sh == 8) launch(cstft4096_kernel<int16_t, 8>, xp);  // 50 %
-        else launch(cstft4096_kernel<int16_t, 0>, xp);
-    } else {
-        const auto *xp = static_cast<const float *>(x);
-        if (sh == 4) launch(cstft4096_kernel<float, 4>, xp);
-        else if (sh == 8) launch(cstft4096_kernel<float, 8>, xp);
-        else launch(cstft4096_kernel<float, 0>, xp);
-    }
+    auto by_shift = [&](auto en, const auto *xp) {
+        constexpr bool EN = decltype(en)::value;
+        using T = std::remove_cv_t<std::remove_pointer_t<decltype(xp)>>;
+        if (sh == 4) launch(cstft4096_kernel<T, 4, EN>, xp);       // 75 % overlap (C5)
+        else if (sh == 8) launch(cstft4096_kernel<T, 8, EN>, xp);  // 50 %
+        else launch(cstft4096_kernel<T, 0, EN>, xp);
+    };
+    auto by_energy = [&](const auto *xp) {
+        if (etot) by_shift(std::integral_constant<bool, true>{}, xp);
+        else by_shift(std::integral_constant<bool, false>{}, xp);
+    };
+    if (dtype == MSD_CI16) by_energy(static_cast<const int16_t *>(x));
+    else by_energy(static_cast<const float *>(x));
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }

@@ -1,0 +1,388 @@
+// C5 certification, the refinement step: the band / noise dB delta of chosen STFT frames of an I/Q
+// stream recomputed in float64 straight from the samples, for the frames whose detector decision
+// the fp32 spectrogram's error bound cannot settle (and the frames of the windows their thresholds
+// come from).  The quantity is the float64 reference's: scipy.signal.spectrogram of complex128
+// input (periodic Hann, constant detrend, density) summed over the fftfreq band masks, 10*log10(E
+// + 1e-12), band - noise (dsp/src/main.py:380-393 per frame).
+//
+// Only the band bins are needed, so no FFT: with the periodic Hann window w[n] = 1/2 - 1/4
+// e^{2 pi i n/N} - 1/4 e^{-2 pi i n/N}, the windowed DFT of the detrended frame v = z - mean is
+//   Y[k] = 1/2 V[k] - 1/4 V[k-1] - 1/4 V[k+1],   V[k] = Z[k] - N mean [k = 0 mod N],
+// and a frame of N samples at hop H is R = N/D blocks of D = gcd(N, H) samples, so
+//   Z_t[k] = sum_{j<R} e^{-2 pi i k j D / N} B_{tH/D + j}[k],  B_m[k] = sum_{n<D} z[mD + n] e^{-2 pi i k n/N}.
+// Each block's B at the needed bins (band and noise bins +-1) is computed once (block_kernel: one
+// wave per block, a float64 Goertzel recurrence over a contiguous segment per lane, rotated to the
+// block origin and summed over the wave), then every frame combines its R blocks (frame_kernel).
+// At C5 (N 4096, H 1024: D 1024, R 4) that is 1024 samples x 9 bins per frame instead of 4096 x 5
+// for a per-frame DFT.
+//
+// The error bound written beside each delta (ed) covers both float64 computations (ours: the
+// Goertzel chains and the combination; the reference's: pocketfft's 4 log2 N + 8 and the detrend /
+// window roundings), against sum |v_n w_n| <= sum |z_n| + N |mean|: ~1e-12 dB, so a decision that
+// stays uncertain after refinement is a genuine float64 near tie.
+#include <cmath>
+#include <numeric>
+#include <vector>
+
+#include "msd_internal.h"
+
+namespace msd {
+namespace {
+
+constexpr int RF_MAXK = 32;  // needed bins (band and noise bins +- 1)
+
+struct RefineBins {
+    int nk;                   // needed bins k' (signed, -N/2 <= k' < N/2 + 1, taken mod N)
+    int k[RF_MAXK];
+    int nb, nn;               // band / noise bins, in np.sum order (ascending FFT index)
+    int bidx[RF_MAXK / 2][3]; // per band bin: indices into k[] of k-1, k, k+1
+    int nidx[RF_MAXK / 2][3];
+    int dc;                   // index into k[] of bin 0, or -1
+};
+
+struct RefineGeom {
+    int N, D, R, L;           // frame, block, blocks per frame, samples per lane (D >= 64: D / 64)
+    int64_t hop;
+    double scale;             // density: 1 / (fs sum w^2)
+    double chain;             // our float64 rounding chain + the reference's, in units of u
+    int nr;                   // frame ranges
+};
+
+template <typename T>
+struct Samp;
+template <>
+struct Samp<int16_t> {
+    __device__ static double2 at(const int16_t *x, int64_t i) {
+        const uint32_t r = reinterpret_cast<const uint32_t *>(x)[i];
+        return make_double2((double)(int16_t)(r & 0xffffu), (double)(int16_t)(r >> 16));
+    }
+};
+template <>
+struct Samp<float> {
+    __device__ static double2 at(const float *x, int64_t i) {
+        const float2 v = reinterpret_cast<const float2 *>(x)[i];
+        return make_double2((double)v.x, (double)v.y);
+    }
+};
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// the range holding compact index g: ranges' compact starts cs[0..nr] (cs[nr] = total)
+__device__ __forceinline__ int find_range(const int64_t *cs, int nr, int64_t g) {
+    int lo = 0, hi = nr - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (cs[mid] <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// one wave per block (D >= 64): lane L runs the Goertzel recurrence of every needed bin over
+// samples [L*S, (L+1)*S) of the block (S = D/64), rotates the segment's DFT to the block origin
+// with two table twiddles, and the wave sums the 64 partials.  out[g]: [nk] B values, then the
+// block's sample sum and sum of |re| + |im| (as .x of one more double2).
+template <typename T>
+__global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, RefineGeom G, RefineBins K,
+                                                    const int64_t *__restrict__ bstart, const int64_t *__restrict__ bcs,
+                                                    int64_t nblocks, const double2 *__restrict__ W,
+                                                    double2 *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= nblocks) return;
+    const int r = find_range(bcs, G.nr, g);
+    const int64_t m = bstart[r] + (g - bcs[r]);
+    const int S = G.L;
+    const int64_t n0 = (int64_t)lane * S;
+    const int64_t base = m * (int64_t)G.D + n0;
+    double2 sum = make_double2(0.0, 0.0);
+    double l1 = 0.0;
+    for (int q = 0; q < S; ++q) {
+        const double2 z = Samp<T>::at(x, base + q);
+        sum = cadd(sum, z);
+        l1 += fabs(z.x) + fabs(z.y);
+    }
+    double2 *o = out + g * (K.nk + 2);
+    for (int b = 0; b < K.nk; ++b) {
+        const int kk = K.k[b];
+        const int km = ((kk % G.N) + G.N) % G.N;
+        double2 contrib;
+        if (km == 0) {
+            contrib = sum;
+        } else {
+            const double c2 = 2.0 * W[km].x;  // 2 cos(theta)
+            double2 s1 = make_double2(0.0, 0.0), s2 = make_double2(0.0, 0.0);
+            for (int q = 0; q < S; ++q) {
+                const double2 z = Samp<T>::at(x, base + q);
+                const double2 s0 = make_double2(z.x + c2 * s1.x - s2.x, z.y + c2 * s1.y - s2.y);
+                s2 = s1;
+                s1 = s0;
+            }
+            // sum_q z[n0 + q] W^{k (n0 + q)} = W^{k (n0 + S - 1)} s_{S-1} - W^{k (n0 + S)} s_{S-2}
+            const double2 t1 = W[(int)(((int64_t)km * (n0 + S - 1)) % G.N)];
+            const double2 t2 = W[(int)(((int64_t)km * (n0 + S)) % G.N)];
+            contrib = csub(cmul(t1, s1), cmul(t2, s2));
+        }
+        const double rx = wave_sum_d(contrib.x), ry = wave_sum_d(contrib.y);
+        if (lane == 0) o[b] = make_double2(rx, ry);
+    }
+    const double sx = wave_sum_d(sum.x), sy = wave_sum_d(sum.y), sl = wave_sum_d(l1);
+    if (lane == 0) {
+        o[K.nk] = make_double2(sx, sy);
+        o[K.nk + 1] = make_double2(sl, 0.0);
+    }
+}
+
+// D < 64: one lane per block (a Goertzel recurrence over its D samples)
+template <typename T>
+__global__ __launch_bounds__(256) void block_small_kernel(const T *__restrict__ x, RefineGeom G, RefineBins K,
+                                                          const int64_t *__restrict__ bstart,
+                                                          const int64_t *__restrict__ bcs, int64_t nblocks,
+                                                          const double2 *__restrict__ W, double2 *__restrict__ out) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nblocks) return;
+    const int r = find_range(bcs, G.nr, g);
+    const int64_t m = bstart[r] + (g - bcs[r]);
+    const int64_t base = m * (int64_t)G.D;
+    double2 sum = make_double2(0.0, 0.0);
+    double l1 = 0.0;
+    for (int q = 0; q < G.D; ++q) {
+        const double2 z = Samp<T>::at(x, base + q);
+        sum = cadd(sum, z);
+        l1 += fabs(z.x) + fabs(z.y);
+    }
+    double2 *o = out + g * (K.nk + 2);
+    for (int b = 0; b < K.nk; ++b) {
+        const int km = ((K.k[b] % G.N) + G.N) % G.N;
+        if (km == 0) {
+            o[b] = sum;
+            continue;
+        }
+        double2 acc = make_double2(0.0, 0.0);
+        for (int q = 0; q < G.D; ++q) acc = cadd(acc, cmul(Samp<T>::at(x, base + q), W[(int)(((int64_t)km * q) % G.N)]));
+        o[b] = acc;
+    }
+    o[K.nk] = sum;
+    o[K.nk + 1] = make_double2(l1, 0.0);
+}
+
+// dB error of a band of n bins with energy E when every bin's amplitude is off by at most d
+// (float64 computations on both sides)
+__device__ __forceinline__ double band_db_bound64(double E, int n, double d) {
+    if (n <= 0) return 0.0;
+    const double u = 0x1p-53;
+    const double dE = 2.0 * d * sqrt((double)n * E) + 3.0 * (double)n * d * d + 2.0 * ((double)n + 4.0) * u * E;
+    const double den = E + 1e-12 - dE;
+    if (!(den > 0.0)) return __builtin_inf();
+    return 4.342944819032518 * dE / den * (1.0 + 1e-9);
+}
+
+// one thread per frame: combine the R blocks, the Hann taps, |Y|^2 * scale, the band sums in
+// np.sum order, 10 log10(E + 1e-12); delta and its bound
+__global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, const int64_t *__restrict__ fstart,
+                                                    const int64_t *__restrict__ fcs, const int64_t *__restrict__ bstart,
+                                                    const int64_t *__restrict__ bcs, int64_t nframes,
+                                                    const double2 *__restrict__ W, const double2 *__restrict__ blk,
+                                                    double *__restrict__ delta, double *__restrict__ ed) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    const int r = find_range(fcs, G.nr, f);
+    const int64_t t = fstart[r] + (f - fcs[r]);
+    const int64_t m0 = t * G.hop / G.D;               // first block of the frame
+    const int64_t g0 = bcs[r] + (m0 - bstart[r]);     // its compact index
+    const int stride = K.nk + 2;
+    // mean and L1 of the frame
+    double2 sum = make_double2(0.0, 0.0);
+    double l1 = 0.0;
+    for (int j = 0; j < G.R; ++j) {
+        sum = cadd(sum, blk[(g0 + j) * stride + K.nk]);
+        l1 += blk[(g0 + j) * stride + K.nk + 1].x;
+    }
+    const double2 mean = make_double2(sum.x / G.N, sum.y / G.N);
+    double2 V[RF_MAXK];
+    for (int b = 0; b < K.nk; ++b) {
+        const int km = ((K.k[b] % G.N) + G.N) % G.N;
+        double2 z = make_double2(0.0, 0.0);
+        for (int j = 0; j < G.R; ++j) {
+            const double2 bv = blk[(g0 + j) * stride + b];
+            z = cadd(z, j == 0 ? bv : cmul(W[(int)(((int64_t)km * j * G.D) % G.N)], bv));
+        }
+        if (km == 0) z = csub(z, make_double2(mean.x * G.N, mean.y * G.N));
+        V[b] = z;
+    }
+    auto energy = [&](const int (*idx)[3], int n) {
+        double E = 0.0;
+        for (int q = 0; q < n; ++q) {
+            const double2 a = V[idx[q][0]], c = V[idx[q][1]], e = V[idx[q][2]];
+            const double2 y = make_double2(0.5 * c.x - 0.25 * a.x - 0.25 * e.x, 0.5 * c.y - 0.25 * a.y - 0.25 * e.y);
+            E += (y.x * y.x + y.y * y.y) * G.scale;
+        }
+        return E;
+    };
+    const double Eb = energy(K.bidx, K.nb), En = energy(K.nidx, K.nn);
+    delta[t] = 10.0 * log10(Eb + 1e-12) - 10.0 * log10(En + 1e-12);
+    // sum |v w| <= sum |z| + N |mean| (w <= 1); amplitude scale sqrt(scale) as P = |Y|^2 scale
+    const double amp = (l1 + (double)G.N * (fabs(mean.x) + fabs(mean.y))) * sqrt(G.scale);
+    const double d = G.chain * 0x1p-53 * amp;
+    ed[t] = band_db_bound64(Eb, K.nb, d) + band_db_bound64(En, K.nn, d) + 1e-13;
+}
+
+}  // namespace
+}  // namespace msd
+
+using namespace msd;
+
+extern "C" {
+
+int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg, int64_t hop,
+                       double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo, int32_t noise_hi,
+                       const int64_t *ranges, int64_t nranges, double *delta, double *ed) {
+    if (!ctx || (!x && n_samples) || !delta || !ed || (!ranges && nranges) || nranges < 0 || nperseg < 4 ||
+        hop <= 0 || !(fs > 0))
+        return fail(MSD_ERR_INVALID, "msd_iq_delta64_dev: bad args");
+    if (dtype != MSD_CI16 && dtype != MSD_CF32) return fail(MSD_ERR_UNSUPPORTED, "msd_iq_delta64_dev: CI16 or CF32");
+    const int N = nperseg;
+    const int h = N / 2;
+    auto ok = [&](int lo, int hi) { return hi < lo || (lo >= -h && hi <= N - h - 1); };
+    if (!ok(band_lo, band_hi) || !ok(noise_lo, noise_hi))
+        return fail(MSD_ERR_INVALID, "msd_iq_delta64_dev: band outside -N/2 .. N/2-1");
+    // needed bins: every band / noise bin and its two neighbours (mod N), each once
+    RefineBins K{};
+    K.dc = -1;
+    auto slot = [&](int kk) -> int {
+        const int km = ((kk % N) + N) % N;
+        for (int i = 0; i < K.nk; ++i)
+            if (((K.k[i] % N) + N) % N == km) return i;
+        if (K.nk >= RF_MAXK) return -1;
+        K.k[K.nk] = kk;
+        return K.nk++;
+    };
+    // np.sum order over the boolean mask: ascending FFT index (bins >= 0 first, then the negative ones)
+    auto fill = [&](int lo, int hi, int (*idx)[3], int &n) -> bool {
+        n = 0;
+        if (hi < lo) return true;
+        std::vector<int> order;
+        for (int b = lo; b <= hi; ++b)
+            if (b >= 0) order.push_back(b);
+        for (int b = lo; b <= hi; ++b)
+            if (b < 0) order.push_back(b);
+        if ((int)order.size() > RF_MAXK / 2) return false;
+        for (int b : order) {
+            const int a = slot(b - 1), c = slot(b), e = slot(b + 1);
+            if (a < 0 || c < 0 || e < 0) return false;
+            idx[n][0] = a;
+            idx[n][1] = c;
+            idx[n][2] = e;
+            ++n;
+        }
+        return true;
+    };
+    if (!fill(band_lo, band_hi, K.bidx, K.nb) || !fill(noise_lo, noise_hi, K.nidx, K.nn))
+        return fail(MSD_ERR_UNSUPPORTED, "msd_iq_delta64_dev: bands too wide for the refinement kernel");
+    RefineGeom G{};
+    G.N = N;
+    G.hop = hop;
+    G.D = (int)std::gcd((int64_t)N, hop);
+    G.R = N / G.D;
+    G.L = G.D >= 64 ? G.D / 64 : 1;
+    // periodic Hann: sum w^2 = 3N/8 exactly; scipy's scale 1/(fs * sum(w^2)) from its float64 window
+    {
+        double sw = 0.0;
+        for (int n = 0; n < N; ++n) {
+            const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * (double)n / (double)N);
+            sw += w * w;
+        }
+        G.scale = 1.0 / (fs * sw);
+    }
+    // rounding chains in units of u = 2^-53: ours -- the Goertzel recurrence over L samples (3 L
+    // Gmax + 8, Gmax = min(1/|sin theta|, L) its error gain), the wave sum (6), the R-block
+    // combination (R + 4), the mean, Hann taps and |Y|^2 (8); the reference's pocketfft chain plus
+    // detrend and window (4 log2 N + 11)
+    double gmax = 1.0;
+    for (int i = 0; i < K.nk; ++i) {
+        const int km = ((K.k[i] % N) + N) % N;
+        if (km == 0) continue;
+        const double sn = std::fabs(std::sin(2.0 * M_PI * km / N));
+        gmax = std::max(gmax, std::min(sn > 0 ? 1.0 / sn : 1e300, (double)(G.D >= 64 ? G.L : G.D)));
+    }
+    const double Lc = G.D >= 64 ? G.L : G.D;
+    G.chain = 3.0 * Lc * gmax + 8.0 + 6.0 + (G.R + 4.0) + 8.0 + 4.0 * std::log2((double)N) + 11.0;
+    if (nranges == 0) return MSD_OK;
+    // frame ranges -> block ranges, compact prefix counts
+    std::vector<int64_t> fstart(nranges), fcs(nranges + 1), bstart(nranges), bcs(nranges + 1);
+    fcs[0] = bcs[0] = 0;
+    for (int64_t r = 0; r < nranges; ++r) {
+        const int64_t a = ranges[2 * r], b = ranges[2 * r + 1];
+        if (a < 0 || b <= a || (b - 1) * hop + N > n_samples || (r > 0 && a < ranges[2 * r - 1]))
+            return fail(MSD_ERR_INVALID, "msd_iq_delta64_dev: ranges must be sorted, disjoint, inside the samples");
+        if ((a * hop) % G.D) return fail(MSD_ERR_INVALID, "msd_iq_delta64_dev: internal block alignment");
+        fstart[r] = a;
+        fcs[r + 1] = fcs[r] + (b - a);
+        bstart[r] = a * hop / G.D;
+        bcs[r + 1] = bcs[r] + ((b - 1) * hop / G.D + G.R - bstart[r]);
+    }
+    if (nranges > 1 << 20) return fail(MSD_ERR_UNSUPPORTED, "msd_iq_delta64_dev: too many ranges");
+    G.nr = (int)nranges;
+    const int64_t nblocks = bcs[nranges], nframes = fcs[nranges];
+    std::vector<double2> W(N);
+    for (int m = 0; m < N; ++m) {
+        const double a = -2.0 * M_PI * (double)m / (double)N;
+        W[m] = make_double2(std::cos(a), std::sin(a));
+    }
+    DeviceGuard g(ctx->device);
+    hipStream_t st = ctx->stream;
+    void *d = nullptr;
+    const size_t nb_blk = sizeof(double2) * (size_t)nblocks * (K.nk + 2);
+    const size_t nb_meta = sizeof(int64_t) * (4 * (size_t)nranges + 2);
+    const size_t nb_w = sizeof(double2) * N;
+    MSD_HIP(hipMalloc(&d, nb_blk + nb_meta + nb_w + 256));
+    auto *blk = static_cast<double2 *>(d);
+    auto *Wd = reinterpret_cast<double2 *>(static_cast<char *>(d) + nb_blk);
+    auto *meta = reinterpret_cast<int64_t *>(static_cast<char *>(d) + nb_blk + nb_w);
+    std::vector<int64_t> hm;
+    hm.insert(hm.end(), fstart.begin(), fstart.end());
+    hm.insert(hm.end(), fcs.begin(), fcs.end());
+    hm.insert(hm.end(), bstart.begin(), bstart.end());
+    hm.insert(hm.end(), bcs.begin(), bcs.end());
+    const int64_t *d_fstart = meta, *d_fcs = meta + nranges, *d_bstart = meta + 2 * nranges + 1,
+                  *d_bcs = meta + 3 * nranges + 1;
+    hipError_t e = hipMemcpyAsync(Wd, W.data(), nb_w, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(meta, hm.data(), sizeof(int64_t) * hm.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        if (G.D >= 64) {
+            const unsigned grid = (unsigned)((nblocks + 3) / 4);
+            if (dtype == MSD_CI16)
+                hipLaunchKernelGGL(block_kernel<int16_t>, dim3(grid), dim3(256), 0, st,
+                                   static_cast<const int16_t *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
+            else
+                hipLaunchKernelGGL(block_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float *>(x),
+                                   G, K, d_bstart, d_bcs, nblocks, Wd, blk);
+        } else {
+            const unsigned grid = (unsigned)((nblocks + 255) / 256);
+            if (dtype == MSD_CI16)
+                hipLaunchKernelGGL(block_small_kernel<int16_t>, dim3(grid), dim3(256), 0, st,
+                                   static_cast<const int16_t *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
+            else
+                hipLaunchKernelGGL(block_small_kernel<float>, dim3(grid), dim3(256), 0, st,
+                                   static_cast<const float *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
+        }
+        hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, G, K, d_fstart,
+                           d_fcs, d_bstart, d_bcs, nframes, Wd, blk, delta, ed);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "msd_iq_delta64_dev");
+    return MSD_OK;
+}
+
+}  // extern "C"

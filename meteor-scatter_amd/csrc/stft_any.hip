@@ -16,6 +16,8 @@
 // (x2 on bins 1..M-1) is stored to out[f][k][t].  These are debug / legacy sizes, not the
 // bandwidth-bound headline path: the column stores are 4- or 8-B per row and rely on L2 to
 // merge the neighbouring columns that concurrent workgroups write.
+#include <type_traits>
+
 #include "msd_internal.h"
 
 namespace msd {
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(SA_THREADS) void stft_any_kernel(
     const T *xf = x + off[f] + t * (int64_t)hop;
 
     // ---- constant detrend: the mean of the nperseg samples, float64 (exact for integer samples)
-    R mean = R(0);
+    double mean = 0.0;
     if (detrend) {
         double s = 0.0;
         for (int i = threadIdx.x; i < nperseg; i += SA_THREADS) s += sample_d(xf, i);
@@ -183,13 +185,21 @@ __global__ __launch_bounds__(SA_THREADS) void stft_any_kernel(
         double tot = 0.0;
 #pragma unroll
         for (int w = 0; w < SA_THREADS / 64; ++w) tot += red[w];
-        mean = static_cast<R>(tot / (double)nperseg);
+        mean = tot / (double)nperseg;
     }
-    // ---- windowed, zero-padded, packed into M complex points
+    // ---- windowed, zero-padded, packed into M complex points.  scipy's constant detrend runs in
+    // float64 for every input but float32 (scipy.signal.detrend casts to 'd'): x - mean in float64,
+    // then rounded to the working precision (a float32 mean of a large DC offset, e.g. uint16 input
+    // around 32768, would leave up to half an ulp of 32768 in bins 0 and 1)
+    constexpr bool f32_detrend = std::is_same<T, float>::value;
+    auto centred = [&](int i) -> R {
+        if constexpr (f32_detrend) return static_cast<R>(xf[i]) - static_cast<R>(mean);
+        else return static_cast<R>(static_cast<double>(xf[i]) - mean);
+    };
     for (int m = threadIdx.x; m < M; m += SA_THREADS) {
         const int i0 = 2 * m, i1 = 2 * m + 1;
-        const R a = i0 < nperseg ? (static_cast<R>(xf[i0]) - mean) * win[i0] : R(0);
-        const R b = i1 < nperseg ? (static_cast<R>(xf[i1]) - mean) * win[i1] : R(0);
+        const R a = i0 < nperseg ? centred(i0) * win[i0] : R(0);
+        const R b = i1 < nperseg ? centred(i1) * win[i1] : R(0);
         A[m] = Cx<R>::make(a, b);
     }
     __syncthreads();

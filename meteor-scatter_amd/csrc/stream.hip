@@ -67,6 +67,19 @@ struct msd_stream_plan {
     uint8_t *d_exact = nullptr;   // [n_local] fresh[j] is numpy-exact
     int32_t *d_list = nullptr;    // [n_local] frames the last marking pass needs exact
     bool decide = false;
+    // certification against the float64 reference (msd_stream_set_certify): a bound on |delta -
+    // delta_ref| per frame, the thresholds' error from it, and per segment the decisions the bounds
+    // cannot settle
+    bool certify = false;
+    double *d_ed = nullptr;       // [n_tail | n_local | head_cap] delta error bound (as d_x)
+    double *d_terr = nullptr;     // [n_local] bound on |numpy threshold(delta) - numpy threshold(delta_ref)|
+    double2 *d_pre_e = nullptr;   // [nblk + 1] prefix sums of (ed, ed^2)
+    longlong2 *d_unc = nullptr;   // [nseg][UCAP] uncertain decisions {local frame, threshold source frame}
+    int32_t *d_ucnt = nullptr;    // [nseg] uncertain decisions of the segment's last scan
+    double2 *d_slack = nullptr;   // [nseg] min over the segment of |delta - thr| - (ed + threshold error), max of
+                                  // ed + threshold error
+    double2 *d_esum = nullptr;    // [nchunk + 1] per-chunk (sum ed, sum ed^2), then the shard's total
+    double terr0 = 0.0;           // bound for thr0 (whole-stream mean + k std)
     int64_t ntiles = 0, nblk = 0;
     int nleaf = 0;
     double thr0 = 0;
@@ -88,8 +101,10 @@ constexpr int64_t CHUNK = NP_BUFSIZE;  // numpy's reduction buffer (8192 element
 struct SState {  // msd_stream_state
     int64_t fz, last_stop;
     double thr;
-    int64_t reserved;
+    int64_t src;  // frame whose threshold `thr` is (-1: thr0)
+    double terr;  // its error bound against the reference's (certification)
 };
+constexpr int UCAP = 32;  // uncertain decisions listed per segment and scan
 
 struct PinHdr {  // head of msd_stream_plan::h_pin, then margins [nseg], then chunk sums
     int32_t changed, overflow;  // copied from d_active[nseg .. nseg + 1]
@@ -98,6 +113,34 @@ struct PinHdr {  // head of msd_stream_plan::h_pin, then margins [nseg], then ch
     SState ex;
 };
 
+
+// ---- the delta error bound of the fp32 spectrogram path (C5): |delta_gpu - delta_ref| <= ed for
+// the float64 reference (scipy.signal.spectrogram of complex128 input, its band sums and dB).
+// Standard model, per bin: the computed spectrum X^ of a linear FFT satisfies
+// |X^_k - X_k| <= c u sum_n |v_n| with c the longest rounding chain from an input to an output
+// (in units of u) and v the detrended, windowed frame.  cstft4096_kernel: detrend, window and its
+// rounding (3), three passes of a 16-point DFT (radix-4 x 4: 2 + 2 adds and an internal twiddle
+// multiply, 2 sqrt 2 u with FMA + sqrt 2 u for the rounded constant: 8.5 each) and the two
+// inter-pass twiddles (4.5 each): 37.5, taken as IQ_CHAIN = 40.  sum |v| <= sqrt(N) ||v||_2 =
+// sqrt(S) with S = sum_k |X_k|^2 (Parseval), S from the kernel's energy partials (an upper bound
+// after the factor 1.001: their own rounding is ~1e-4 relative).  The reference's float64 chain
+// (pocketfft, 4 log2 N + 8, + 3 for detrend / window) adds its own, ~1e-9 of ours.  A band of n
+// bins with computed energy E (fp64 sum of the fp32 powers, each |x|^2 + |y|^2 rounded twice)
+// moves by dE <= 2 d sqrt(n E) + 3 n d^2 + (n + 4) u E, its dB by 10/ln 10 * dE / (E + 1e-12 - dE)
+// (unbounded once dE >= E); delta by the sum of the two bands'.  A band touching bins -1..1 also
+// carries the frame mean's rounding (the DC offset's transform): not bounded here, +inf.
+constexpr double IQ_CHAIN = 40.0;
+
+__device__ __forceinline__ double band_db_bound(double E, int n, double d) {
+    if (n <= 0) return 0.0;  // empty band: 1e-12 on both sides
+    const double u = 0x1p-24;
+    const double dE = 2.0 * d * sqrt((double)n * E) + 3.0 * (double)n * d * d + ((double)n + 4.0) * u * E;
+    const double den = E + 1e-12 - dE;
+    if (!(den > 0.0)) return __builtin_inf();
+    return 4.342944819032518 * dE / den * (1.0 + 1e-12);
+}
+
+__device__ __forceinline__ bool near_dc(int lo, int hi) { return hi >= lo && lo <= 1 && hi >= -1; }
 
 // ------------------------------------------------------------------ band delta per frame
 // one thread per frame: the band bins of a frame are one or two short contiguous runs of its row
@@ -127,12 +170,15 @@ __device__ __forceinline__ double band_energy4(const float *__restrict__ row, in
     return acc;
 }
 
+// etot / ed (both or neither): the frame's 16 energy partials (cstft4096_kernel<EN>) in, the delta
+// error bound out (above)
 __global__ __launch_bounds__(256) void iq_band_delta_kernel(const float *__restrict__ spec, int64_t nstreams,
                                                             int64_t max_frames, const int64_t *__restrict__ frames,
                                                             int N, int blo, int bhi, int nlo, int nhi,
                                                             double *__restrict__ band_db,
                                                             double *__restrict__ noise_db,
-                                                            double *__restrict__ delta, int64_t ld) {
+                                                            double *__restrict__ delta, int64_t ld,
+                                                            const float *__restrict__ etot, double *__restrict__ ed) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nstreams * max_frames) return;
     const int64_t s = g / max_frames, t = g - s * max_frames;
@@ -143,6 +189,22 @@ __global__ __launch_bounds__(256) void iq_band_delta_kernel(const float *__restr
     if (band_db) band_db[s * ld + t] = bd;
     if (noise_db) noise_db[s * ld + t] = nd;
     delta[s * ld + t] = bd - nd;
+    if (ed) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v *ep = reinterpret_cast<const f4v *>(etot + (s * max_frames + t) * 16);
+        double S = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f4v v = __builtin_nontemporal_load(ep + q);
+            S += ((double)v[0] + (double)v[1]) + ((double)v[2] + (double)v[3]);
+        }
+        const double A = sqrt(S * 1.001);
+        const double lg = log2((double)N);
+        const double d = IQ_CHAIN * 0x1p-24 * A + (4.0 * lg + 11.0) * 0x1p-53 * sqrt((double)N) * A;
+        double b = band_db_bound(e0, bhi - blo + 1, d) + band_db_bound(e1, nhi - nlo + 1, d);
+        if (near_dc(blo, bhi) || near_dc(nlo, nhi) || !(S >= 0.0)) b = __builtin_inf();
+        ed[s * ld + t] = b + 1e-12;
+    }
 }
 
 // numpy's pairwise sum of one chunk a(cb .. cb+m), m <= 8192, by one wave.  Lane L follows the
@@ -612,6 +674,79 @@ __global__ __launch_bounds__(256) void approx_kernel(const double *__restrict__ 
     eps[j] = P.eps_scale * 4.0 * (em_a + em_np + ak * es + 4.0 * u * (fabs(thr) + ak * sd));
 }
 
+// certification: the threshold error of every frame from its window's delta error bounds.  mean +
+// k std is (1 + k)-Lipschitz in the sense |mean(a) - mean(b)| <= mean|a - b| and |std(a) - std(b)|
+// <= rms(a - b) (population std: the norm of the centred vector), so with |delta - delta_ref| <= ed
+// per frame, |thr - thr_ref| <= mean(ed) + |k| rms(ed) over the window, plus numpy's own rounding
+// on both sides (1e-10 absolute: ~1e-14 |thr| for these windows).  The window sums come from the
+// prefix sums of (ed, ed^2) as the predictor's do (approx_kernel); their cancellation error
+// (d u (hi + lo), nonnegative terms) is added.
+constexpr double TERR_ABS = 1e-10;
+__global__ __launch_bounds__(256) void terr_kernel(const double *__restrict__ ed, const double2 *__restrict__ pre,
+                                                   FreshParams P, double *__restrict__ terr) {
+    __shared__ double2 sh[256];
+    const int t = threadIdx.x;
+    const int64_t j0 = (int64_t)blockIdx.x * 256;
+    const int64_t e0 = P.n_tail + j0, l0 = e0 - P.W;
+    const double2 base_hi = block_prefix(ed, pre, e0, sh);
+    const double2 base_lo = l0 > 0 ? block_prefix(ed, pre, l0, sh) : make_double2(0.0, 0.0);
+    auto val = [&](int64_t q) {
+        const double v = q >= 0 && q < P.x_len ? ed[q] : 0.0;
+        return make_double2(v, v * v);
+    };
+    const double2 hi = block_exscan(val(e0 + t), base_hi, sh);
+    double2 lo = block_exscan(val(l0 + t), base_lo, sh);
+    const int64_t j = j0 + t;
+    if (j >= P.n_local) return;
+    const int64_t i = P.frame0 + j;
+    const int64_t len = i < P.W ? i : P.W;
+    if (len < P.W) lo = make_double2(0.0, 0.0);
+    if (len <= 0) {  // empty window: NaN threshold on both sides
+        terr[j] = 0.0;
+        return;
+    }
+    const double fl = (double)len, u = 0x1p-53;
+    const double d2 = 2.0 * PB + 20.0 + 2.0 * (double)P.pre_per;
+    const double m1 = fmax(hi.x - lo.x, 0.0) / fl + 2.0 * d2 * u * (hi.x + lo.x) / fl;
+    const double m2 = fmax(hi.y - lo.y, 0.0) / fl + 2.0 * d2 * u * (hi.y + lo.y) / fl;
+    terr[j] = (m1 + fabs(P.k) * sqrt(m2)) * (1.0 + 1e-9) + TERR_ABS;
+}
+
+// sums of (ed, ed^2) over x[a .. b): one 256-thread workgroup per 8192 elements, then one
+// workgroup adds the partials (out[nblocks] = total); deterministic order
+__global__ __launch_bounds__(256) void ed_sums_kernel(const double *__restrict__ ed, int64_t a, int64_t b,
+                                                      double2 *__restrict__ out) {
+    __shared__ double2 sh[256];
+    const int t = threadIdx.x;
+    const int64_t c0 = a + (int64_t)blockIdx.x * CHUNK;
+    double s1 = 0.0, s2 = 0.0;
+    for (int64_t q = c0 + t; q < c0 + CHUNK && q < b; q += 256) {
+        const double v = ed[q];
+        s1 += v;
+        s2 += v * v;
+    }
+    sh[t] = make_double2(s1, s2);
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) sh[t] = d2add(sh[t], sh[t + o]);
+        __syncthreads();
+    }
+    if (t == 0) out[blockIdx.x] = sh[0];
+}
+__global__ __launch_bounds__(256) void ed_total_kernel(double2 *__restrict__ part, int64_t nb) {
+    __shared__ double2 sh[256];
+    const int t = threadIdx.x;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int64_t q = t; q < nb; q += 256) acc = d2add(acc, part[q]);
+    sh[t] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) sh[t] = d2add(sh[t], sh[t + o]);
+        __syncthreads();
+    }
+    if (t == 0) part[nb] = sh[0];
+}
+
 // frames with i < W: window delta[0:i] (only the shard that holds the stream's first W frames)
 // frames with i < W: window delta[0:i], a different tree per frame (only the shard that holds the
 // stream's first W frames); one wave per frame
@@ -687,10 +822,23 @@ struct ScanParams {
     int64_t n_local, frame0, seg_len, nseg, cap, F0, Fa;
     double thr0;
     int32_t write_thr;
+    double terr0;  // certification: thr0's error bound
+};
+
+// certification outputs (ed != nullptr): per segment the uncertain decisions of its last scan
+struct CertOut {
+    const double *ed;    // delta error bound, local frame index (nullptr: no certification)
+    const double *terr;  // fresh threshold error bound, local frame index
+    longlong2 *unc;      // [nseg][UCAP]
+    int32_t *ucnt;       // [nseg]
+    double2 *slack;      // [nseg] (min slack, max error zone)
 };
 
 __device__ __forceinline__ uint64_t bits_from(int p) { return p >= 64 ? 0ull : (~0ull << p); }
 __device__ __forceinline__ uint64_t bits_upto(int e) { return e >= 63 ? ~0ull : ((1ull << (e + 1)) - 1ull); }
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int l) {
+    return __builtin_bit_cast(int64_t, __shfl(__builtin_bit_cast(long long, v), l, 64));
+}
 
 __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ delta, const double *__restrict__ fresh,
                                                   ScanParams P, const SState *__restrict__ in_state,
@@ -700,7 +848,7 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
                                                   int32_t *__restrict__ overflow, int32_t *__restrict__ need,
                                                   const double *__restrict__ eps, uint8_t *__restrict__ exact,
                                                   int32_t *__restrict__ list, int32_t *__restrict__ list_count,
-                                                  int32_t *__restrict__ changed) {
+                                                  int32_t *__restrict__ changed, CertOut cert) {
     const int64_t s = blockIdx.x;
     // the round's change counter, which the propagate kernel after this one increments (zeroed
     // here instead of by a separate memset launch per round)
@@ -712,16 +860,21 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
     const SState in = in_state[s];
     int64_t fz = in.fz, last_stop = in.last_stop;
     double thr_cur = in.thr;
-    const double thr0 = P.thr0;
+    int64_t src_cur = in.src;  // certification: where thr_cur comes from, and its error bound
+    double terr_cur = in.terr;
+    const double thr0 = P.thr0, terr0 = P.terr0;
+    const bool cfy = cert.ed != nullptr;
     msd_det *rs = runs + s * P.cap;
     int64_t nr = 0, cur_start = 0;
     bool have = false;
     double min_margin = __builtin_inf();
+    double min_slack = __builtin_inf(), max_zone = 0.0;
+    int32_t nunc = 0;
 
     // the next step's delta and fresh threshold are loaded one step ahead (the loads do not depend
     // on the state), so the scalar walk of a step overlaps the memory latency of the next
-    // (and, when listing, the bound and the exact flag)
-    auto ld = [&](int64_t k, double &dv, double &fr, double &ep, uint8_t &ex) {
+    // (and, when listing, the bound and the exact flag; when certifying, the two error bounds)
+    auto ld = [&](int64_t k, double &dv, double &fr, double &ep, uint8_t &ex, double &edv, double &trv) {
         const int64_t j = k + lane < b ? k + lane : (k < b ? k : a);
         dv = delta[j];
         fr = fresh[j];
@@ -729,42 +882,68 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
             ep = eps[j];
             ex = exact[j];
         }
+        if (cfy) {
+            edv = cert.ed[j];
+            trv = cert.terr[j];
+        }
     };
     // two steps in flight: the loads of step k + 128 are issued while step k is walked (deeper
     // rings, 8 steps unrolled, measured slower: the walk is bound by its own instruction latency)
-    double dv_n, fr_n, ep_n = 0.0, dv_m, fr_m, ep_m = 0.0;
+    double dv_n, fr_n, ep_n = 0.0, dv_m, fr_m, ep_m = 0.0, ed_n = 0.0, ed_m = 0.0, tr_n = 0.0, tr_m = 0.0;
     uint8_t ex_n = 1, ex_m = 1;
-    ld(a, dv_n, fr_n, ep_n, ex_n);
-    ld(a + 64, dv_m, fr_m, ep_m, ex_m);
+    ld(a, dv_n, fr_n, ep_n, ex_n, ed_n, tr_n);
+    ld(a + 64, dv_m, fr_m, ep_m, ex_m, ed_m, tr_m);
     for (int64_t k = a; k < b; k += 64) {
         const int nvalid = (int)(b - k < 64 ? b - k : 64);
         const bool valid = lane < nvalid;
         const int64_t j = valid ? k + lane : k;
         const int64_t gi = P.frame0 + j;  // global frame of this lane
         const int64_t pos = P.frame0 + k;
-        const double dv = dv_n, fr = fr_n, ep = ep_n;
+        const double dv = dv_n, fr = fr_n, ep = ep_n, edv = ed_n, trv = tr_n;
         const uint8_t ex = ex_n;
         dv_n = dv_m;
         fr_n = fr_m;
         ep_n = ep_m;
         ex_n = ex_m;
-        ld(k + 128, dv_m, fr_m, ep_m, ex_m);
+        ed_n = ed_m;
+        tr_n = tr_m;
+        ld(k + 128, dv_m, fr_m, ep_m, ex_m, ed_m, tr_m);
         const bool init = gi < P.F0;
         const double t_unf = init ? thr0 : fr;
+        // certification: the fresh threshold's error against the reference's -- the window's delta
+        // errors, plus the predictor's bound where the value is a prediction (decisions only)
+        const double e_unf = init ? terr0 : trv + ((list && ex != 1) ? ep : 0.0);
+        const int64_t s_unf = init ? -1 : gi;
         const uint64_t A_unf = __ballot(valid && dv > t_unf);
-        double t_fin = t_unf;
+        double t_fin = t_unf, e_fin = e_unf;
+        int64_t s_fin = s_unf;
         uint64_t D = 0, U = 0;  // detected, unfrozen (fresh threshold used)
         int p = 0;
         while (p < nvalid) {
             const int64_t i = pos + p;
             if (fz >= i) {  // frozen from p on: threshold held (thr0 before the fixed-init end)
                 const int e = (int)(fz - pos < nvalid - 1 ? fz - pos : nvalid - 1);
-                const double held = i < P.F0 ? thr0 : thr_cur;
+                const bool h0 = i < P.F0;
+                const double held = h0 ? thr0 : thr_cur;
+                const double held_e = h0 ? terr0 : terr_cur;
+                const int64_t held_s = h0 ? -1 : src_cur;
                 const double t_h = init ? thr0 : held;
                 const uint64_t rng = bits_from(p) & bits_upto(e);
                 const uint64_t m = __ballot(valid && dv > t_h) & rng;
-                if ((rng >> lane) & 1ull) t_fin = t_h;
-                thr_cur = (pos + e) < P.F0 ? thr0 : held;
+                if ((rng >> lane) & 1ull) {
+                    t_fin = t_h;
+                    e_fin = init ? terr0 : held_e;
+                    s_fin = init ? -1 : held_s;
+                }
+                if ((pos + e) < P.F0) {
+                    thr_cur = thr0;
+                    terr_cur = terr0;
+                    src_cur = -1;
+                } else {
+                    thr_cur = held;
+                    terr_cur = held_e;
+                    src_cur = held_s;
+                }
                 if (m) {
                     const int last = 63 - __builtin_clzll(m);
                     D |= m;
@@ -776,6 +955,8 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
                 if (!m) {
                     U |= bits_from(p);
                     thr_cur = __shfl(t_unf, nvalid - 1);
+                    terr_cur = __shfl(e_unf, nvalid - 1);
+                    src_cur = shfl_i64(s_unf, nvalid - 1);
                     p = nvalid;
                     break;
                 }
@@ -783,6 +964,8 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
                 U |= bits_from(p) & bits_upto(u);
                 D |= 1ull << u;
                 thr_cur = __shfl(t_unf, u);
+                terr_cur = __shfl(e_unf, u);
+                src_cur = shfl_i64(s_unf, u);
                 fz = pos + u + P.Fa;
                 p = u + 1;
             }
@@ -810,6 +993,21 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
             const double mg = fabs(dv - t_fin);
             if (mg < min_margin) min_margin = mg;
             if (P.write_thr) thr_used[j] = t_fin;
+        }
+        if (cfy) {  // the decision dv > t_fin is the reference's when |dv - t_fin| exceeds both errors;
+            // a NaN threshold (empty window) is NaN on both sides: no detection either way
+            const double sl = t_fin != t_fin ? __builtin_inf() : fabs(dv - t_fin) - (edv + e_fin);
+            const bool unc = valid && !(sl > 0.0);
+            if (valid) {
+                min_slack = fmin(min_slack, sl != sl ? -__builtin_inf() : sl);
+                max_zone = fmax(max_zone, edv + e_fin);
+            }
+            const uint64_t mu = __ballot(unc);
+            if (mu) {
+                const int r = __builtin_popcountll(mu & ((1ull << lane) - 1ull));
+                if (unc && nunc + r < UCAP) cert.unc[s * UCAP + nunc + r] = make_longlong2(j, s_fin);
+                nunc += __builtin_popcountll(mu);
+            }
         }
         // runs: maximal groups of consecutive detected frames (a new run iff i > last_stop + 1)
         while (D) {
@@ -845,15 +1043,25 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
         ++nr;
     }
     for (int o = 32; o >= 1; o >>= 1) min_margin = fmin(min_margin, __shfl_xor(min_margin, o, 64));
+    if (cfy)
+        for (int o = 32; o >= 1; o >>= 1) {
+            min_slack = fmin(min_slack, __shfl_xor(min_slack, o, 64));
+            max_zone = fmax(max_zone, __shfl_xor(max_zone, o, 64));
+        }
     if (lane == 0) {
         nruns[s] = (int32_t)(nr < P.cap ? nr : P.cap);
         if (nr > P.cap) atomicOr(overflow, 1);
         seg_margin[s] = min_margin;
+        if (cfy) {
+            cert.ucnt[s] = nunc;
+            cert.slack[s] = make_double2(min_slack, max_zone);
+        }
         SState o;
         o.fz = fz;
         o.last_stop = last_stop;
         o.thr = thr_cur;
-        o.reserved = 0;
+        o.src = src_cur;
+        o.terr = terr_cur;
         out_state[s] = o;
     }
 }
@@ -863,11 +1071,11 @@ __global__ __launch_bounds__(64) void scan_kernel(const double *__restrict__ del
 // every segment re-scans from its fixed-point entry state; 0 (the shard's entry changed): the
 // others keep their states and only segment 0 is active
 __global__ void scan_entry_kernel(SState *__restrict__ in_state, int32_t *__restrict__ active, int64_t nseg,
-                                  SState entry, double thr0, int32_t reset) {
+                                  SState entry, double thr0, double terr0, int32_t reset) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s < nseg) {
         if (s == 0) in_state[0] = entry;
-        else if (reset == 1) in_state[s] = SState{-1, -2, thr0, 0};
+        else if (reset == 1) in_state[s] = SState{-1, -2, thr0, -1, terr0};
         active[s] = (s == 0 || reset) ? 1 : 0;
     } else if (s < nseg + 2) {
         active[s] = 0;  // change counter, overflow flag
@@ -880,7 +1088,8 @@ __device__ __forceinline__ bool same_state(const SState &x, const SState &y, int
     if (fx != fy) return false;
     if (fx) {
         if (x.fz != y.fz) return false;
-        if (a >= F0 && __builtin_bit_cast(long long, x.thr) != __builtin_bit_cast(long long, y.thr)) return false;
+        if (a >= F0 && (__builtin_bit_cast(long long, x.thr) != __builtin_bit_cast(long long, y.thr) || x.src != y.src))
+            return false;
     }
     return (x.last_stop == a - 1) == (y.last_stop == a - 1);
 }
@@ -1003,7 +1212,16 @@ extern "C" {
 int msd_iq_band_delta_dev(msd_ctx *ctx, const float *spec, int64_t nstreams, int64_t max_frames,
                           const int64_t *frames, int32_t nperseg, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
                           int32_t noise_hi, double *band_db, double *noise_db, double *delta, int64_t ld) {
-    if (!ctx || !spec || !frames || !delta || nstreams < 0 || max_frames < 0 || nperseg <= 0 || ld < max_frames)
+    return msd_iq_band_delta_bound_dev(ctx, spec, nullptr, nstreams, max_frames, frames, nperseg, band_lo, band_hi,
+                                       noise_lo, noise_hi, band_db, noise_db, delta, nullptr, ld);
+}
+
+int msd_iq_band_delta_bound_dev(msd_ctx *ctx, const float *spec, const float *etot, int64_t nstreams,
+                                int64_t max_frames, const int64_t *frames, int32_t nperseg, int32_t band_lo,
+                                int32_t band_hi, int32_t noise_lo, int32_t noise_hi, double *band_db, double *noise_db,
+                                double *delta, double *ed, int64_t ld) {
+    if (!ctx || !spec || !frames || !delta || nstreams < 0 || max_frames < 0 || nperseg <= 0 || ld < max_frames ||
+        (!etot) != (!ed))
         return fail(MSD_ERR_INVALID, "msd_iq_band_delta_dev: bad args");
     const int h = nperseg / 2;
     auto ok = [&](int lo, int hi) { return hi < lo || (lo >= -h && hi <= nperseg - h - 1); };
@@ -1015,7 +1233,7 @@ int msd_iq_band_delta_dev(msd_ctx *ctx, const float *spec, int64_t nstreams, int
     const int64_t blocks = (nstreams * max_frames + 255) / 256;
     hipLaunchKernelGGL(iq_band_delta_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, spec, nstreams,
                        max_frames, frames, (int)nperseg, band_lo, band_hi, noise_lo, noise_hi, band_db, noise_db,
-                       delta, ld);
+                       delta, ld, etot, ed);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }
@@ -1068,7 +1286,7 @@ int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total
     if ((e = hipMalloc(&p->d_pos, sizeof(int64_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc pos");
     if ((e = hipMalloc(&p->d_chunks, sizeof(double) * (nchunk + 2))) != hipSuccess)
         return cleanup(e, "hipMalloc chunks");
-    if ((e = hipHostMalloc(&p->h_pin, sizeof(PinHdr) + sizeof(double) * (nseg1 + nchunk), hipHostMallocDefault)) !=
+    if ((e = hipHostMalloc(&p->h_pin, sizeof(PinHdr) + sizeof(double) * (nseg1 + nchunk + 4), hipHostMallocDefault)) !=
         hipSuccess)
         return cleanup(e, "hipHostMalloc stream readbacks");
     p->ntiles = (nl1 + FR_FRAMES - 1) / FR_FRAMES;
@@ -1080,6 +1298,19 @@ int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total
     if ((e = hipMalloc(&p->d_eps, sizeof(double) * nl1)) != hipSuccess) return cleanup(e, "hipMalloc eps");
     if ((e = hipMalloc(&p->d_exact, nl1)) != hipSuccess) return cleanup(e, "hipMalloc exact");
     if ((e = hipMalloc(&p->d_list, sizeof(int32_t) * nl1)) != hipSuccess) return cleanup(e, "hipMalloc list");
+    // certification buffers (used after msd_stream_set_certify); ed starts at 0 (delta exact)
+    const int64_t xl = p->n_tail + nl1 + p->head_cap;
+    if ((e = hipMalloc(&p->d_ed, sizeof(double) * xl)) != hipSuccess) return cleanup(e, "hipMalloc ed");
+    if ((e = hipMemset(p->d_ed, 0, sizeof(double) * xl)) != hipSuccess) return cleanup(e, "hipMemset ed");
+    if ((e = hipMalloc(&p->d_terr, sizeof(double) * nl1)) != hipSuccess) return cleanup(e, "hipMalloc terr");
+    if ((e = hipMalloc(&p->d_pre_e, sizeof(double2) * (p->nblk + 1))) != hipSuccess)
+        return cleanup(e, "hipMalloc pre_e");
+    if ((e = hipMalloc(&p->d_unc, sizeof(longlong2) * nseg1 * UCAP)) != hipSuccess) return cleanup(e, "hipMalloc unc");
+    if ((e = hipMalloc(&p->d_ucnt, sizeof(int32_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc ucnt");
+    if ((e = hipMemset(p->d_ucnt, 0, sizeof(int32_t) * nseg1)) != hipSuccess) return cleanup(e, "hipMemset ucnt");
+    if ((e = hipMalloc(&p->d_slack, sizeof(double2) * nseg1)) != hipSuccess) return cleanup(e, "hipMalloc slack");
+    if ((e = hipMalloc(&p->d_esum, sizeof(double2) * (xl / CHUNK + 2))) != hipSuccess)
+        return cleanup(e, "hipMalloc esum");
     if (W > 0) {
         std::vector<int4> prog;
         build_program(W, prog);
@@ -1098,7 +1329,8 @@ void msd_stream_plan_destroy(msd_stream_plan *p) {
     hipStreamSynchronize(p->ctx->stream);
     void *bufs[] = {p->d_x, p->d_fresh, p->d_thr, p->d_state, p->d_active, p->d_runs, p->d_out, p->d_nruns,
                     p->d_margin, p->d_count, p->d_pos, p->d_chunks, p->d_prog, p->d_need, p->d_done, p->d_pre,
-                    p->d_eps, p->d_exact, p->d_list};
+                    p->d_eps, p->d_exact, p->d_list, p->d_ed, p->d_terr, p->d_pre_e, p->d_unc, p->d_ucnt,
+                    p->d_slack, p->d_esum};
     for (void *b : bufs)
         if (b) hipFree(b);
     if (p->h_pin) hipHostFree(p->h_pin);
@@ -1215,7 +1447,106 @@ int msd_stream_fresh(msd_stream_plan *p) {
         hipLaunchKernelGGL(approx_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, p->d_x, p->d_pre, P,
                            jshort, p->d_fresh, p->decide ? p->d_eps : nullptr);
     }
+    if (p->certify) {  // the thresholds' error bounds from the windows' delta error bounds
+        const int64_t nb = P.x_len / PB + 1;
+        hipLaunchKernelGGL(blocksum_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, st, p->d_ed, P.x_len, nb,
+                           p->d_pre_e);
+        hipLaunchKernelGGL(blockscan_kernel, dim3(1), dim3(1024), 0, st, p->d_pre_e, nb);
+        hipLaunchKernelGGL(terr_kernel, dim3((unsigned)((p->n_local + 255) / 256)), dim3(256), 0, st, p->d_ed,
+                           p->d_pre_e, P, p->d_terr);
+    }
     MSD_HIP(hipGetLastError());
+    return MSD_OK;
+}
+
+int msd_stream_set_certify(msd_stream_plan *p, int32_t on) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_set_certify: null plan");
+    p->certify = on != 0;
+    return MSD_OK;
+}
+
+int msd_stream_error_buffers(msd_stream_plan *p, double **ed, double **tail, double **head) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_error_buffers: null plan");
+    if (ed) *ed = p->d_ed + p->n_tail;
+    if (tail) *tail = p->d_ed;
+    if (head) *head = p->d_ed + p->n_tail + p->n_local;
+    return MSD_OK;
+}
+
+// (sum ed, sum ed^2) over [x0, x1) of the plan's x indexing, on the device at d_esum[nb]; returns nb
+static int64_t ed_sums_async(msd_stream_plan *p, int64_t x0, int64_t x1) {
+    const int64_t nb = x1 > x0 ? (x1 - x0 + CHUNK - 1) / CHUNK : 0;
+    hipStream_t st = p->ctx->stream;
+    if (nb > 0)
+        hipLaunchKernelGGL(ed_sums_kernel, dim3((unsigned)nb), dim3(256), 0, st, p->d_ed, x0, x1, p->d_esum);
+    hipLaunchKernelGGL(ed_total_kernel, dim3(1), dim3(256), 0, st, p->d_esum, nb);
+    return nb;
+}
+
+int msd_stream_ed_sums(msd_stream_plan *p, double *s1, double *s2) {
+    if (!p || !s1 || !s2) return fail(MSD_ERR_INVALID, "msd_stream_ed_sums: null");
+    DeviceGuard g(p->ctx->device);
+    const int64_t nb = ed_sums_async(p, p->n_tail, p->n_tail + p->n_local);
+    MSD_HIP(hipGetLastError());
+    double2 r;
+    MSD_HIP(hipMemcpyAsync(pin_chunks(p), p->d_esum + nb, sizeof(double2), hipMemcpyDeviceToHost, p->ctx->stream));
+    MSD_HIP(hipStreamSynchronize(p->ctx->stream));
+    std::memcpy(&r, pin_chunks(p), sizeof(r));
+    *s1 = r.x;
+    *s2 = r.y;
+    return MSD_OK;
+}
+
+// thr0's error bound from the whole stream's (sum ed, sum ed^2) over n frames
+static double terr0_from(double s1, double s2, int64_t n, double k) {
+    if (n <= 0) return 0.0;
+    const double fl = (double)n;
+    return (s1 / fl + fabs(k) * sqrt(s2 / fl)) * (1.0 + 1e-9) + TERR_ABS;
+}
+
+int msd_stream_set_terr0(msd_stream_plan *p, double s1, double s2) {
+    if (!p) return fail(MSD_ERR_INVALID, "msd_stream_set_terr0: null plan");
+    p->terr0 = terr0_from(s1, s2, p->n_total, p->cfg.k_std);
+    return MSD_OK;
+}
+
+int msd_stream_certificate(msd_stream_plan *p, int64_t *uncertain, double *min_slack, double *max_zone,
+                           int64_t *frames, int64_t *srcs, int64_t cap, int64_t *listed) {
+    if (!p || !uncertain || !min_slack || !max_zone || !listed)
+        return fail(MSD_ERR_INVALID, "msd_stream_certificate: null");
+    *uncertain = 0;
+    *listed = 0;
+    *min_slack = __builtin_inf();
+    *max_zone = 0.0;
+    if (!p->certify) return fail(MSD_ERR_INVALID, "msd_stream_certificate: certification is off");
+    if (p->nseg == 0) return MSD_OK;
+    if (!p->scanned) return fail(MSD_ERR_INVALID, "msd_stream_certificate: call msd_stream_scan first");
+    DeviceGuard g(p->ctx->device);
+    std::vector<int32_t> cnt(p->nseg);
+    std::vector<double2> sl(p->nseg);
+    MSD_HIP(hipMemcpy(cnt.data(), p->d_ucnt, sizeof(int32_t) * p->nseg, hipMemcpyDeviceToHost));
+    MSD_HIP(hipMemcpy(sl.data(), p->d_slack, sizeof(double2) * p->nseg, hipMemcpyDeviceToHost));
+    int64_t tot = 0;
+    std::vector<int64_t> segs;
+    for (int64_t q = 0; q < p->nseg; ++q) {
+        tot += cnt[q];
+        *min_slack = sl[q].x < *min_slack || sl[q].x != sl[q].x ? sl[q].x : *min_slack;
+        *max_zone = sl[q].y > *max_zone ? sl[q].y : *max_zone;
+        if (cnt[q] > 0) segs.push_back(q);
+    }
+    *uncertain = tot;
+    if (tot == 0 || !frames || !srcs || cap <= 0) return MSD_OK;
+    std::vector<longlong2> u(UCAP);
+    int64_t n = 0;
+    for (int64_t q : segs) {
+        const int32_t m = cnt[q] < UCAP ? cnt[q] : UCAP;
+        MSD_HIP(hipMemcpy(u.data(), p->d_unc + q * UCAP, sizeof(longlong2) * m, hipMemcpyDeviceToHost));
+        for (int32_t r = 0; r < m && n < cap; ++r, ++n) {
+            frames[n] = p->frame0 + u[r].x;  // global frame index
+            srcs[n] = u[r].y;
+        }
+    }
+    *listed = n;
     return MSD_OK;
 }
 
@@ -1271,7 +1602,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
         std::memcpy(&e0, entry, sizeof(SState));
         const int32_t mode = !p->scanned ? 1 : (reset == 1 || reset == 2 ? reset : 0);
         hipLaunchKernelGGL(scan_entry_kernel, dim3((unsigned)((p->nseg + 2 + 255) / 256)), dim3(256), 0, st, st_in(p),
-                           p->d_active, p->nseg, e0, thr0, mode);
+                           p->d_active, p->nseg, e0, thr0, p->terr0, mode);
         MSD_HIP(hipGetLastError());
     }
     p->thr0 = thr0;
@@ -1285,6 +1616,9 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
     P.Fa = p->cfg.adaptive ? p->cfg.freeze_after_blocks : 0;
     P.thr0 = thr0;
     P.write_thr = p->decide ? 0 : 1;  // decisions only: the thresholds buffer is not an output
+    P.terr0 = p->terr0;
+    CertOut cert{nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (p->certify) cert = CertOut{p->d_ed + p->n_tail, p->d_terr, p->d_unc, p->d_ucnt, p->d_slack};
     int32_t *changed = p->d_active + p->nseg;
     int32_t *overflow = p->d_active + p->nseg + 1;
     // rounds are enqueued three at a time (a round with no active segment costs two empty
@@ -1299,7 +1633,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
                 hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail,
                                    p->d_fresh, P, st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns,
                                    p->d_margin, p->d_thr, overflow, nullptr, p->d_eps, p->d_exact,
-                                   p->decide ? p->d_list : nullptr, p->d_done + p->ntiles, changed);
+                                   p->decide ? p->d_list : nullptr, p->d_done + p->ntiles, changed, cert);
             }
             MSD_HIP(hipGetLastError());
             ++nround;
@@ -1331,7 +1665,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
             KernelTimer timer(p->ctx, K_SSCAN);
             hipLaunchKernelGGL(scan_kernel, dim3((unsigned)p->nseg), dim3(64), 0, st, p->d_x + p->n_tail, p->d_fresh, P,
                                st_in(p), st_out(p), p->d_active, p->d_runs, p->d_nruns, p->d_margin, p->d_thr,
-                               overflow, p->d_need, nullptr, nullptr, nullptr, nullptr, nullptr);
+                               overflow, p->d_need, nullptr, nullptr, nullptr, nullptr, nullptr, cert);
         }
         MSD_HIP(hipGetLastError());
         MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));
@@ -1431,14 +1765,19 @@ int msd_stream_detect_local(msd_stream_plan *p, int32_t exact_thresholds, msd_de
         hipLaunchKernelGGL(chunk_sums_kernel<true>, dim3(blocks), dim3(256), 0, st, p->d_x, (int64_t)0, (int64_t)0, nc,
                            n, 0.0, stats, p->d_chunks);
         hipLaunchKernelGGL(stream_stats_kernel<1>, dim3(1), dim3(256), 0, st, p->d_chunks, nc, n, p->cfg.k_std, stats);
+        int64_t nbe = 0;
+        if (p->certify) nbe = ed_sums_async(p, 0, n);  // thr0's error bound from the whole stream's ed
         MSD_HIP(hipGetLastError());
         MSD_HIP(hipMemcpyAsync(pin_chunks(p), stats + 1, sizeof(double), hipMemcpyDeviceToHost, st));
+        if (p->certify)
+            MSD_HIP(hipMemcpyAsync(pin_chunks(p) + 1, p->d_esum + nbe, sizeof(double2), hipMemcpyDeviceToHost, st));
         MSD_HIP(hipStreamSynchronize(st));
         thr0 = pin_chunks(p)[0];
+        if (p->certify) p->terr0 = terr0_from(pin_chunks(p)[1], pin_chunks(p)[2], n, p->cfg.k_std);
     }
     *thr0_out = thr0;
     // the freeze / run scan to its fixed point, refined until it reads exact thresholds only
-    const msd_stream_state clean{-1, -2, thr0, 0};
+    const msd_stream_state clean{-1, -2, thr0, -1, p->terr0};
     msd_stream_state ex{};
     int32_t r = 0;
     if ((rc = msd_stream_scan(p, thr0, &clean, 1, &ex, &r))) return rc;

@@ -116,9 +116,10 @@ METEOR_DTYPE = np.dtype([("start_block", np.int64), ("stop_block", np.int64), ("
 
 
 class MsdStreamState(C.Structure):
-    """msd_stream_state: the detector state entering a frame (main.py:455-493 variables)."""
+    """msd_stream_state: the detector state entering a frame (main.py:455-493 variables), plus the
+    frame whose fresh threshold ``thr`` is (-1: thr0) and its error bound (certification)."""
     _fields_ = [("freeze_until", C.c_int64), ("last_stop", C.c_int64), ("thr", C.c_double),
-                ("reserved", C.c_int64)]
+                ("src", C.c_int64), ("thr_err", C.c_double)]
 
 
 class MsdWavInfo(C.Structure):
@@ -182,6 +183,7 @@ _SIGS = [
     ("msd_cstft_frames", C.c_int64, [_P, C.c_int64]),
     ("msd_cstft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P]),
     ("msd_cstft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
+    ("msd_cstft_psd_energy_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, _P]),
     ("msd_spec_band_sum_dev", C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
     ("msd_spec_band_sum_f64_dev", C.c_int,
      [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
@@ -210,6 +212,12 @@ _SIGS = [
     ("msd_iq_band_delta_dev", C.c_int,
      [_P, _P, C.c_int64, C.c_int64, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P,
       C.c_int64]),
+    ("msd_iq_band_delta_bound_dev", C.c_int,
+     [_P, _P, _P, C.c_int64, C.c_int64, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P,
+      C.c_int64]),
+    ("msd_iq_delta64_dev", C.c_int,
+     [_P, _P, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_double, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+      _P, C.c_int64, _P, _P]),
     ("msd_stream_plan_create", C.c_int,
      [_P, C.POINTER(MsdDetCfg), C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.POINTER(_P)]),
     ("msd_stream_plan_destroy", None, [_P]),
@@ -229,6 +237,13 @@ _SIGS = [
      [_P, C.c_double, C.POINTER(MsdStreamState), C.c_int32, C.POINTER(MsdStreamState), C.POINTER(C.c_int32)]),
     ("msd_stream_runs", C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     ("msd_stream_db", C.c_int, [_P, _P, C.c_int64]),
+    ("msd_stream_set_certify", C.c_int, [_P, C.c_int32]),
+    ("msd_stream_error_buffers", C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P)]),
+    ("msd_stream_ed_sums", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    ("msd_stream_set_terr0", C.c_int, [_P, C.c_double, C.c_double]),
+    ("msd_stream_certificate", C.c_int,
+     [_P, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double), _P, _P, C.c_int64,
+      C.POINTER(C.c_int64)]),
 ]
 SYMBOLS = [s[0] for s in _SIGS]
 
@@ -620,9 +635,11 @@ class CStftPlan:
         return out
 
     def run_dev(self, x: DeviceBuffer, dtype_code_iq: int, off: DeviceBuffer, length: DeviceBuffer, nstreams: int,
-                max_frames: int, out: DeviceBuffer):
-        check(self.ctx.lib.msd_cstft_psd_dev(self.h, x.ptr, int(dtype_code_iq), off.ptr, length.ptr, int(nstreams),
-                                             int(max_frames), out.ptr))
+                max_frames: int, out: DeviceBuffer, etot: DeviceBuffer | None = None):
+        """etot: also each frame's 16 total-power partials (msd_cstft_psd_energy_dev)"""
+        check(self.ctx.lib.msd_cstft_psd_energy_dev(self.h, x.ptr, int(dtype_code_iq), off.ptr, length.ptr,
+                                                    int(nstreams), int(max_frames), out.ptr,
+                                                    None if etot is None else etot.ptr))
 
 
 class StreamPlan:
@@ -646,6 +663,10 @@ class StreamPlan:
         self.d_delta, self.d_tail, self.d_head, self.d_thr = d, t, hd, thr
         self.n_tail, self.n_head = nt.value, nh.value
         self.nseg = -(-self.n_local // self.seg_len) if self.n_local else 0
+        e, et, eh = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        check(ctx.lib.msd_stream_error_buffers(h, C.byref(e), C.byref(et), C.byref(eh)))
+        self.d_ed, self.d_ed_tail, self.d_ed_head = e, et, eh
+        self.certify = False
 
     def close(self):
         if getattr(self, "h", None) and self.ctx.h:  # a plan outliving its context leaks, never crashes
@@ -684,6 +705,46 @@ class StreamPlan:
             raise ValueError(f"halos must hold {self.n_tail} / {self.n_head} frames")
         self._put(self.d_tail, tail)
         self._put(self.d_head, head)
+
+    # ---- certification against the float64 reference (include/msdsp.h msd_stream_set_certify)
+    def set_certify(self, on: bool):
+        check(self.ctx.lib.msd_stream_set_certify(self.h, 1 if on else 0))
+        self.certify = bool(on)
+
+    def set_ed(self, ed: np.ndarray):
+        """the shard's delta error bounds (n_local; 0 = exact)"""
+        if np.asarray(ed).shape != (self.n_local,):
+            raise ValueError("ed must hold the shard's n_local frames")
+        self._put(self.d_ed, ed)
+
+    def ed(self, lo: int = 0, hi: int | None = None) -> np.ndarray:
+        hi = self.n_local if hi is None else hi
+        return self._get(C.c_void_p(self.d_ed.value + 8 * lo), hi - lo) if hi > lo else np.zeros(0)
+
+    def set_ed_halos(self, tail: np.ndarray, head: np.ndarray):
+        if np.asarray(tail).shape != (self.n_tail,) or np.asarray(head).shape != (self.n_head,):
+            raise ValueError(f"halos must hold {self.n_tail} / {self.n_head} frames")
+        self._put(self.d_ed_tail, tail)
+        self._put(self.d_ed_head, head)
+
+    def ed_sums(self) -> tuple[float, float]:
+        a, b = C.c_double(0), C.c_double(0)
+        check(self.ctx.lib.msd_stream_ed_sums(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def set_terr0(self, s1: float, s2: float):
+        check(self.ctx.lib.msd_stream_set_terr0(self.h, float(s1), float(s2)))
+
+    def certificate(self, cap: int = 4096):
+        """after the last scan: (uncertain decisions, min slack, max error zone, listed [(global frame,
+        threshold source frame)])"""
+        n, ms, mz, nl = C.c_int64(0), C.c_double(0), C.c_double(0), C.c_int64(0)
+        fr = np.zeros(cap, np.int64)
+        sr = np.zeros(cap, np.int64)
+        check(self.ctx.lib.msd_stream_certificate(self.h, C.byref(n), C.byref(ms), C.byref(mz), ptr(fr), ptr(sr),
+                                                  int(cap), C.byref(nl)))
+        k = nl.value
+        return n.value, ms.value, mz.value, np.stack([fr[:k], sr[:k]], 1)
 
     exact_thresholds = True
 
@@ -755,13 +816,25 @@ class StreamPlan:
         return d
 
 
+def _dp(b):
+    return b.ptr if isinstance(b, DeviceBuffer) else b
+
+
 def iq_band_delta_dev(ctx: Context, spec: DeviceBuffer, nstreams: int, max_frames: int, frames: DeviceBuffer,
                       nperseg: int, band: tuple[int, int], noise: tuple[int, int], delta, ld: int,
-                      band_db=None, noise_db=None):
-    """delta (device pointer or DeviceBuffer) [s*ld + t] from the frame-major I/Q spectrogram."""
-    dp = delta.ptr if isinstance(delta, DeviceBuffer) else delta
-    bp = band_db.ptr if isinstance(band_db, DeviceBuffer) else band_db
-    np_ = noise_db.ptr if isinstance(noise_db, DeviceBuffer) else noise_db
-    check(ctx.lib.msd_iq_band_delta_dev(ctx.h, spec.ptr, int(nstreams), int(max_frames), frames.ptr, int(nperseg),
-                                        int(band[0]), int(band[1]), int(noise[0]), int(noise[1]), bp, np_, dp,
-                                        int(ld)))
+                      band_db=None, noise_db=None, etot=None, ed=None):
+    """delta (device pointer or DeviceBuffer) [s*ld + t] from the frame-major I/Q spectrogram; with
+    etot (the spectrogram's energy partials) also the delta error bound ed [s*ld + t]."""
+    check(ctx.lib.msd_iq_band_delta_bound_dev(ctx.h, spec.ptr, _dp(etot), int(nstreams), int(max_frames), frames.ptr,
+                                              int(nperseg), int(band[0]), int(band[1]), int(noise[0]), int(noise[1]),
+                                              _dp(band_db), _dp(noise_db), _dp(delta), _dp(ed), int(ld)))
+
+
+def iq_delta64_dev(ctx: Context, x, dtype_code_iq: int, n_samples: int, nperseg: int, hop: int, fs: float,
+                   band: tuple[int, int], noise: tuple[int, int], ranges: np.ndarray, delta, ed):
+    """float64 delta of the frames in ranges ([n][2] frame [first, end), frame t at sample t*hop of
+    x) and its error bound, into delta[t] / ed[t] (device pointers)"""
+    r = np.ascontiguousarray(ranges, dtype=np.int64).reshape(-1, 2)
+    check(ctx.lib.msd_iq_delta64_dev(ctx.h, _dp(x), int(dtype_code_iq), int(n_samples), int(nperseg), int(hop),
+                                     float(fs), int(band[0]), int(band[1]), int(noise[0]), int(noise[1]), ptr(r),
+                                     r.shape[0], _dp(delta), _dp(ed)))

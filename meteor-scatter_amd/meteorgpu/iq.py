@@ -84,8 +84,9 @@ class IQBatch:
         iq = np.ascontiguousarray(iq, dtype=self.dtype)
         self.d_x.upload(iq, byte_offset=(s * 2 * self.n_pad + 2 * sample_offset) * self.dtype.itemsize)
 
-    def run(self):
-        self.plan.run_dev(self.d_x, self.code, self.d_off, self.d_len, self.ns, self.T, self.d_out)
+    def run(self, etot: _lib.DeviceBuffer | None = None):
+        """etot: also each frame's 16 energy partials (float32 [ns][T][16], the error bound's input)"""
+        self.plan.run_dev(self.d_x, self.code, self.d_off, self.d_len, self.ns, self.T, self.d_out, etot)
 
     def close(self):
         self.plan.close()
@@ -120,15 +121,53 @@ def frame_shard(n_samples: int, nperseg: int, hop: int, rank: int, world: int):
     return T, f0, f1, f0 * hop, ((f1 - 1) * hop + nperseg) if f1 > f0 else f0 * hop
 
 
+def _merge(iv):
+    """sorted, merged [a, b) intervals"""
+    out = []
+    for a, b in sorted((int(a), int(b)) for a, b in iv if b > a):
+        if out and a <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], b)
+        else:
+            out.append([a, b])
+    return out
+
+
+def _subtract(iv, done):
+    """intervals iv minus the (merged) intervals done"""
+    out = []
+    for a, b in iv:
+        cur = a
+        for c, d in done:
+            if d <= cur or c >= b:
+                continue
+            if c > cur:
+                out.append([cur, c])
+            cur = max(cur, d)
+            if cur >= b:
+                break
+        if cur < b:
+            out.append([cur, b])
+    return out
+
+
 class IQShardDetector:
     """One rank's time shard of an I/Q stream on the GPU: spectrogram (frame-major, kept in HBM) →
-    per-frame band delta written straight into the stream plan → detector over the whole stream."""
+    per-frame band delta written straight into the stream plan → detector over the whole stream.
+
+    Certification (``certify``, default on): the spectrogram kernel also writes each frame's energy,
+    the band delta kernel a bound on |delta - delta_ref| against the float64 reference (scipy's
+    spectrogram of complex128 input), and every decision of the detector is checked against its
+    bounds (include/msdsp.h, msd_stream_set_certify).  ``detect(exact_decisions=True)`` then
+    recomputes in float64 (msd_iq_delta64_dev, from the samples) the delta of every frame an
+    uncertain decision depends on -- the frame itself and the window its threshold comes from -- and
+    runs the detector again, until no decision is uncertain (or only float64-level near ties are
+    left, flagged as ``near_tie``).  The detections are then the float64 reference's."""
 
     def __init__(self, ctx: _lib.Context, n_samples_total: int, fs, nperseg, noverlap, freq_band, noise_band,
                  threshold_std_factor=4.0, flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                  threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                  threshold_fixed_init_duration_sec=10, rank: int = 0, world: int = 1, dtype=np.int16,
-                 seg_len: int = 8192, chunk_frames: int | None = None):
+                 seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = True):
         """chunk_frames: keep only that many frames of spectrogram in HBM and stream the shard through
         it (``process_host``); the detector still sees the whole shard's delta.  A 24 h 192 kHz
         stream (66 GB of int16 I/Q, 265 GB of spectrogram) then runs on one GPU."""
@@ -154,6 +193,13 @@ class IQShardDetector:
         cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
         self.plan = _lib.StreamPlan(ctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
         self.ops = _stream.DeviceStreamOps(self.plan)
+        self.certify = bool(certify)
+        self.d_etot = ctx.alloc(max(self.batch.T, 1) * 16 * 4) if self.certify else None
+        if self.certify:
+            self.plan.set_certify(True)
+        self.fs_ = float(fs)
+        self._read = None      # the shard's sample source when chunked (refinement re-reads samples)
+        self._refined = []     # global frame ranges whose delta is float64 already
 
     def upload(self, iq: np.ndarray, sample_offset: int = 0):
         """interleaved I/Q of this shard's samples, starting at shard sample `sample_offset`"""
@@ -161,10 +207,12 @@ class IQShardDetector:
 
     def spectrogram_and_delta(self):
         """async: spectrogram of the shard and its per-frame band delta (into the stream plan)"""
+        self._refined = []
         if self.f1 > self.f0:
-            self.batch.run()
+            self.batch.run(self.d_etot)
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
-                                   self.noise, self.plan.d_delta, self.batch.T)
+                                   self.noise, self.plan.d_delta, self.batch.T, etot=self.d_etot,
+                                   ed=self.plan.d_ed if self.certify else None)
 
     def process_host(self, iq_shard: np.ndarray):
         """interleaved I/Q of the shard's samples [s0, s1) on the host → the shard's delta in the
@@ -182,33 +230,103 @@ class IQShardDetector:
                 self.upload(np.ascontiguousarray(read(0, self.s1 - self.s0)))
             self.spectrogram_and_delta()
             return
+        self._read = read
+        self._refined = []
         for c0 in range(0, nloc, self.chunk):
             nf = min(self.chunk, nloc - c0)
             a = c0 * self.hop
             b = a + (nf - 1) * self.hop + self.N
             self.batch.upload(0, np.ascontiguousarray(read(a, b)))
             self.d_frames.upload(np.array([nf], np.int64))
-            self.batch.run()  # frames past nf read stale samples; their powers are not used
+            self.batch.run(self.d_etot)  # frames past nf read stale samples; their powers are not used
+            ed = _lib.C.c_void_p(self.plan.d_ed.value + 8 * c0) if self.certify else None
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
-                                   self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T)
+                                   self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T,
+                                   etot=self.d_etot, ed=ed)
 
-    def detect(self, comm=None, thresholds: bool = True) -> _stream.StreamResult:
-        return _stream.StreamDetector(self.ops, comm or _stream.LocalComm(), self.adaptive, self.k, self.W,
-                                      self.F0).run(thresholds)
+    MAX_REFINE = 8
+
+    def detect(self, comm=None, thresholds: bool = True, exact_decisions: bool = True) -> _stream.StreamResult:
+        """The detector over the whole stream (every rank gets the same result).  Certifying, each
+        decision is checked against its error bounds; exact_decisions refines the uncertain ones
+        (class docstring)."""
+        comm = comm or _stream.LocalComm()
+        refined, first, passes = 0, None, 0
+        for _ in range(self.MAX_REFINE + 1):
+            res = _stream.StreamDetector(self.ops, comm, self.adaptive, self.k, self.W, self.F0).run(thresholds)
+            passes += 1
+            if first is None:
+                first = res.uncertain
+            if not self.certify or not exact_decisions or res.certified:
+                break
+            need = self._dependencies(res.uncertain_frames)
+            if not need:  # every uncertain decision already reads float64 values: a float64 near tie
+                break
+            self._refined = _merge(self._refined + need)
+            refined += sum(b - a for a, b in need)
+        if self.certify:
+            res.refined_delta_frames = refined
+            res.near_tie = not res.certified
+            res.uncertain_initial = first
+            res.detector_passes = passes
+        return res
+
+    def _dependencies(self, uncertain) -> list:
+        """global frame ranges the uncertain decisions (frame, threshold source) depend on, and
+        refines this rank's part of them"""
+        iv = []
+        for f, src in np.asarray(uncertain, np.int64).reshape(-1, 2):
+            if src < 0:  # thr0: the whole stream's mean and std
+                iv.append((0, self.T))
+            else:
+                iv.append((max(0, int(src) - self.W), int(src)))  # the window delta[src - W : src]
+            iv.append((int(f), int(f) + 1))
+        need = _subtract(_merge(iv), self._refined)
+        self._refine_local(need)
+        return need
+
+    def _refine_local(self, ranges):
+        """float64 delta (and its bound) of this rank's frames in the global ranges, from the samples"""
+        loc = []
+        for a, b in ranges:
+            a, b = max(a, self.f0), min(b, self.f1)
+            if b > a:
+                loc.append((a - self.f0, b - self.f0))
+        if not loc:
+            return
+        if not self.chunk:  # the shard's samples are resident: frame j at sample j * hop
+            _lib.iq_delta64_dev(self.ctx, self.batch.d_x, self.batch.code, self.batch.n, self.N, self.hop, self.fs_,
+                                self.band, self.noise, np.array(loc, np.int64), self.plan.d_delta, self.plan.d_ed)
+            return
+        # chunked: re-read each range's samples (<= chunk frames at a time) into the batch buffer
+        for a, b in loc:
+            for c in range(a, b, self.chunk):
+                e = min(b, c + self.chunk)
+                s0, s1 = c * self.hop, (e - 1) * self.hop + self.N
+                self.batch.upload(0, np.ascontiguousarray(self._read(s0, s1)))
+                _lib.iq_delta64_dev(self.ctx, self.batch.d_x, self.batch.code, s1 - s0, self.N, self.hop, self.fs_,
+                                    self.band, self.noise, np.array([[0, e - c]], np.int64),
+                                    _lib.C.c_void_p(self.plan.d_delta.value + 8 * c),
+                                    _lib.C.c_void_p(self.plan.d_ed.value + 8 * c))
 
     def close(self):
         self.plan.close()
         self.batch.close()
+        if self.d_etot is not None:
+            self.d_etot.free()
 
 
 def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072, threshold_std_factor=4.0,
                     flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                     threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                     threshold_fixed_init_duration_sec=10, wav_start_date_time=None, out_csv_file=None,
-                    device: int = 0, chunk_sec: float | None = None):
+                    device: int = 0, chunk_sec: float | None = None, exact_decisions: bool = True):
     """The batch detector of dsp/src/main.py (:380-527, :640-658) over an I/Q recording with the STFT
     frame as the block.  Returns (detections [OutputDetection], thresholds, delta, result).
-    chunk_sec: stream the spectrogram through HBM in chunks of that many seconds (long recordings)."""
+    chunk_sec: stream the spectrogram through HBM in chunks of that many seconds (long recordings).
+    exact_decisions: every detector decision certified against the float64 reference, the uncertain
+    ones recomputed in float64 (IQShardDetector); result.certified / near_tie / decision_bound /
+    refined_delta_frames report it."""
     buf, code = interleave(i, q)
     n = buf.size // 2
     det = IQShardDetector(context(device), n, fs, nperseg, noverlap, freq_band, noise_band, threshold_std_factor,
@@ -218,7 +336,7 @@ def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072
                           chunk_frames=int(chunk_sec * fs / (nperseg - noverlap)) if chunk_sec else None)
     try:
         det.process_host(buf[2 * det.s0: 2 * det.s1])
-        res = det.detect()
+        res = det.detect(exact_decisions=exact_decisions)
         delta = det.plan.delta()
     finally:
         det.close()

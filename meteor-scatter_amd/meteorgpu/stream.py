@@ -93,9 +93,10 @@ class RcclComm:
 
 
 # ---------------------------------------------------------------- detector state
-def clean_state(thr0: float) -> tuple[int, int, float]:
-    """(freeze_until_idx, last run's stop, threshold) before block 0 (main.py:454-468)."""
-    return (-1, -2, float(thr0))
+def clean_state(thr0: float, terr0: float = 0.0) -> tuple[int, int, float, int, float]:
+    """(freeze_until_idx, last run's stop, threshold) before block 0 (main.py:454-468), plus the
+    threshold's source frame (-1: thr0) and its error bound (certification)."""
+    return (-1, -2, float(thr0), -1, float(terr0))
 
 
 def same_state(x, y, a: int, F0: int) -> bool:
@@ -106,17 +107,28 @@ def same_state(x, y, a: int, F0: int) -> bool:
     if fx:
         if x[0] != y[0]:
             return False
-        if a >= F0 and np.float64(x[2]).view(np.int64) != np.float64(y[2]).view(np.int64):
+        if a >= F0 and (np.float64(x[2]).view(np.int64) != np.float64(y[2]).view(np.int64) or x[3] != y[3]):
             return False
     return (x[1] == a - 1) == (y[1] == a - 1)
 
 
+NSTATE = 5  # int64 words of a packed state
+
+
 def _pack(s) -> np.ndarray:
-    return np.array([s[0], s[1], np.float64(s[2]).view(np.int64)], np.int64)
+    return np.array([s[0], s[1], np.float64(s[2]).view(np.int64), s[3], np.float64(s[4]).view(np.int64)], np.int64)
 
 
 def _unpack(a: np.ndarray):
-    return (int(a[0]), int(a[1]), float(np.int64(a[2]).view(np.float64)))
+    return (int(a[0]), int(a[1]), float(np.int64(a[2]).view(np.float64)), int(a[3]),
+            float(np.int64(a[4]).view(np.float64)))
+
+
+def terr0_from(s1: float, s2: float, n: int, k: float) -> float:
+    """thr0's error bound from the whole stream's sum ed and sum ed^2 (stream.hip terr0_from)"""
+    if n <= 0:
+        return 0.0
+    return (s1 / n + abs(k) * math.sqrt(s2 / n)) * (1.0 + 1e-9) + 1e-10
 
 
 @dataclass
@@ -129,6 +141,16 @@ class StreamResult:
     rounds: int                # state-exchange rounds
     refined: int = 0           # this rank's exact-threshold work units (tiles; frames without the
                                # thresholds output)
+    # certification against the float64 reference (plans with certify on; None / 0 otherwise):
+    certified: bool | None = None   # every decision's |delta - thr| exceeds its error bounds
+    uncertain: int = 0              # decisions the bounds cannot settle (the whole stream)
+    min_slack: float = math.inf     # min over decisions of |delta - thr| - (ed + threshold bound)
+    decision_bound: float = 0.0     # max over decisions of ed + threshold bound (dB)
+    uncertain_frames: np.ndarray | None = None  # [(global frame, threshold source frame or -1)]
+    refined_delta_frames: int = 0   # frames whose delta was recomputed in float64 (iq refinement)
+    near_tie: bool = False          # uncertain decisions left after refinement (float64 near ties)
+    uncertain_initial: int = 0      # uncertain decisions of the first pass (before any refinement)
+    detector_passes: int = 1        # detector runs (1 + refinement rounds)
 
 
 class StreamDetector:
@@ -142,21 +164,39 @@ class StreamDetector:
         self.W, self.F0 = int(window_blocks), int(fixed_init_blocks)
         self.H = int(head_frames)
 
-    # 1. halos
+    @property
+    def certify(self) -> bool:
+        return bool(getattr(self.ops, "certify", False))
+
+    # 1. halos (and, certifying, the same halos of the delta error bounds, in the same message)
     def exchange_halos(self):
         ops, r, n = self.ops, self.comm.rank, self.ops.n_local
+        cf = self.certify
         if self.comm.world == 1:  # nothing before or after the only shard
             ops.set_halos(np.zeros(0), np.zeros(0))
+            if cf:
+                ops.set_ed_halos(np.zeros(0), np.zeros(0))
             return
-        tail = ops.delta(max(0, n - self.W), n) if self.W > 0 else np.zeros(0)
-        head = ops.delta(0, min(self.H, n))
-        got = self.comm.allgather(np.concatenate([[float(tail.size)], tail, head]))  # one exchange
-        tails = [g[1: 1 + int(g[0])] for g in got]
-        heads = [g[1 + int(g[0]):] for g in got]
-        before = np.concatenate([np.zeros(0)] + tails[:r])
-        after = np.concatenate([np.zeros(0)] + heads[r + 1:])
-        tail = before[before.size - ops.n_tail:] if ops.n_tail else before[:0]
-        ops.set_halos(tail, after[: ops.n_head])
+        lo_t, hi_h = max(0, n - self.W) if self.W > 0 else n, min(self.H, n)
+        tail, head = ops.delta(lo_t, n), ops.delta(0, hi_h)
+        parts = [[float(tail.size)], tail, head]
+        if cf:
+            parts += [ops.ed(lo_t, n), ops.ed(0, hi_h)]
+        got = self.comm.allgather(np.concatenate(parts))  # one exchange
+        nts = [int(g[0]) for g in got]
+        nhs = [(g.size - 1) // (2 if cf else 1) - nts[q] for q, g in enumerate(got)]
+
+        def halos(off):  # off 0: delta, 1: ed
+            tails = [g[1 + off * (nts[q] + nhs[q]): 1 + off * (nts[q] + nhs[q]) + nts[q]] for q, g in enumerate(got)]
+            heads = [g[1 + off * (nts[q] + nhs[q]) + nts[q]: 1 + (off + 1) * (nts[q] + nhs[q])]
+                     for q, g in enumerate(got)]
+            before = np.concatenate([np.zeros(0)] + tails[:r])
+            after = np.concatenate([np.zeros(0)] + heads[r + 1:])
+            return (before[before.size - ops.n_tail:] if ops.n_tail else before[:0]), after[: ops.n_head]
+
+        ops.set_halos(*halos(0))
+        if cf:
+            ops.set_ed_halos(*halos(1))
 
     # 2. numpy's sum over the whole stream from the ranks' chunk sums
     def _global_sum(self, mean=None) -> float:
@@ -173,21 +213,49 @@ class StreamDetector:
         std = math.sqrt(self._global_sum(mean) / n)
         return mean + self.k * std
 
+    def global_threshold_error(self) -> float:
+        """certifying: thr0's error bound from every rank's sum ed, sum ed^2 (set on the plan too)"""
+        s1, s2 = self.ops.ed_sums()
+        tot = np.sum(np.stack(self.comm.allgather_fixed(np.array([s1, s2], np.float64))), axis=0)
+        self.ops.set_terr0(float(tot[0]), float(tot[1]))
+        return terr0_from(float(tot[0]), float(tot[1]), self.ops.n_total, self.k)
+
+    def certificate(self) -> tuple[int, float, float, np.ndarray]:
+        """every rank's uncertain decisions after the last scan, merged (identical on every rank)"""
+        n, ms, mz, lst = self.ops.certificate()
+        msg = np.concatenate([[n, np.float64(ms).view(np.int64), np.float64(mz).view(np.int64)],
+                              lst.reshape(-1)]).astype(np.int64)
+        got = self.comm.allgather(msg)
+        tot = sum(int(g[0]) for g in got)
+        mslack = min(float(np.int64(g[1]).view(np.float64)) for g in got)
+        mzone = max(float(np.int64(g[2]).view(np.float64)) for g in got)
+        frames = np.concatenate([np.zeros((0, 2), np.int64)] + [g[3:].reshape(-1, 2) for g in got])
+        return tot, mslack, mzone, frames
+
+    def _certified(self, res: StreamResult) -> StreamResult:
+        if not self.certify:
+            return res
+        tot, mslack, mzone, frames = self.certificate()
+        res.certified, res.uncertain, res.min_slack = tot == 0, tot, mslack
+        res.decision_bound, res.uncertain_frames, res.near_tie = mzone, frames, tot > 0
+        return res
+
     # 3. the state at the shard edges
     def scan(self, thr0: float, refined: bool = False) -> int:
         """refined: thresholds changed since the last fixed point -- every segment re-scans from its
         converged entry state instead of a clean restart"""
         ops, comm, r = self.ops, self.comm, self.comm.rank
         F0 = self.F0 if self.adaptive else ops.n_total
-        entry = self._entry if refined else clean_state(thr0)
+        entry = self._entry if refined else clean_state(thr0, getattr(self, "terr0", 0.0))
         exit_, _ = ops.scan(thr0, entry, 2 if refined else 1)
         rounds = 1
         while True:
             # one exchange per round: every rank's exit and entry state and first frame, so each
             # rank decides every rank's "entry changed" alike
             got = comm.allgather_fixed(np.concatenate([_pack(exit_), _pack(entry), [ops.frame0]]))
-            exits = [_unpack(g[0:3]) for g in got]
-            changed = [q > 0 and not same_state(exits[q - 1], _unpack(got[q][3:6]), int(got[q][6]), F0)
+            S = NSTATE
+            exits = [_unpack(g[0:S]) for g in got]
+            changed = [q > 0 and not same_state(exits[q - 1], _unpack(got[q][S:2 * S]), int(got[q][2 * S]), F0)
                        for q in range(comm.world)]
             if not any(changed):
                 self._entry = entry
@@ -207,7 +275,7 @@ class StreamDetector:
             # (a one-rank RCCL or gloo group keeps the exchange protocol below)
             dets, thr0, margin, rounds, refined = ops.detect_local(thresholds if self.adaptive else True)
             thr = None if not thresholds else (ops.thresholds() if self.adaptive else np.array([thr0]))
-            return StreamResult(dets, thr0, thr, margin, rounds, refined)
+            return self._certified(StreamResult(dets, thr0, thr, margin, rounds, refined))
         self.exchange_halos()
         if self.adaptive:  # state-free, independent of thr0: queued before the chunk-sum round trips
             # without the thresholds output only the decisions need exact thresholds: predicted
@@ -215,6 +283,7 @@ class StreamDetector:
             ops.set_exact_thresholds(thresholds)
             ops.fresh()
         thr0 = self.global_threshold()
+        self.terr0 = self.global_threshold_error() if self.certify else 0.0
         rounds = self.scan(thr0)
         refined = 0
         while self.adaptive:  # until the last scan read exact thresholds only, on every rank
@@ -252,7 +321,7 @@ class StreamDetector:
             db_all[g[:m]] = g[m:].view(np.float64)
         dets["db"] = db_all
         thr = None if not thresholds else (ops.thresholds() if self.adaptive else np.array([thr0]))
-        return StreamResult(dets, thr0, thr, margin, rounds, refined)
+        return self._certified(StreamResult(dets, thr0, thr, margin, rounds, refined))
 
 
 class DeviceStreamOps:
@@ -263,6 +332,25 @@ class DeviceStreamOps:
         self.n_total, self.frame0, self.n_local = plan.n_total, plan.frame0, plan.n_local
         self.n_tail, self.n_head = plan.n_tail, plan.n_head
         self.last_rounds = 0
+
+    @property
+    def certify(self) -> bool:
+        return self.plan.certify
+
+    def ed(self, lo=0, hi=None):
+        return self.plan.ed(lo, hi)
+
+    def set_ed_halos(self, tail, head):
+        self.plan.set_ed_halos(tail, head)
+
+    def ed_sums(self):
+        return self.plan.ed_sums()
+
+    def set_terr0(self, s1, s2):
+        self.plan.set_terr0(s1, s2)
+
+    def certificate(self):
+        return self.plan.certificate()
 
     def delta(self, lo=0, hi=None):
         return self.plan.delta(lo, hi)
@@ -293,9 +381,9 @@ class DeviceStreamOps:
         return self.plan.refine()
 
     def scan(self, thr0, entry, reset):
-        ex, rounds = self.plan.scan(thr0, _lib.MsdStreamState(entry[0], entry[1], entry[2], 0), reset)
+        ex, rounds = self.plan.scan(thr0, _lib.MsdStreamState(*entry), reset)
         self.last_rounds += rounds
-        return (ex.freeze_until, ex.last_stop, ex.thr), rounds
+        return (ex.freeze_until, ex.last_stop, ex.thr, ex.src, ex.thr_err), rounds
 
     def runs(self):
         return self.plan.runs()

@@ -73,15 +73,15 @@ class NumpyStreamOps:
         return 0  # fresh() is exact already
 
     def scan(self, thr0, entry, reset):
-        fz, last, thr = entry
+        fz, last, thr, src = entry[:4]
         runs = []
         margin = np.inf
         for j in range(self.n_local):
             i = self.frame0 + j
             if i < self.F0:
-                thr = thr0
+                thr, src = thr0, -1
             elif i > fz:
-                thr = self.fr[j]
+                thr, src = self.fr[j], i
             self.thr[j] = thr
             v = self.d[j]
             margin = min(margin, abs(v - thr)) if not np.isnan(thr) else margin
@@ -95,7 +95,7 @@ class NumpyStreamOps:
                 last = i
                 fz = max(i + self.Fa, max(0, i))
         self._runs, self._margin = runs, margin
-        return (fz, last, thr), 1
+        return (fz, last, thr, src, 0.0), 1
 
     def runs(self):
         out = np.zeros(len(self._runs), [("start", np.int64), ("stop", np.int64), ("db", np.float64)])

@@ -42,8 +42,8 @@ def test_struct_layouts():
     assert ctypes.sizeof(_lib.MsdDet) == 24 == _lib.DET_DTYPE.itemsize
     assert ctypes.sizeof(_lib.MsdDetCfg) == 48
     assert ctypes.sizeof(_lib.MsdHistCfg) == 48
-    # msd_stream_state {i64 freeze_until, i64 last_stop, f64 thr, i64 reserved}
-    assert ctypes.sizeof(_lib.MsdStreamState) == 32
+    # msd_stream_state {i64 freeze_until, i64 last_stop, f64 thr, i64 src, f64 thr_err}
+    assert ctypes.sizeof(_lib.MsdStreamState) == 40
 
 
 def test_invalid_args_fail_without_gpu():

@@ -102,12 +102,15 @@ def test_global_mode_and_end_quirk():
 
 
 def test_state_helpers():
-    assert stream.same_state((-1, -2, 1.0), (5, -2, 2.0), 10, 0)       # both unfrozen
-    assert not stream.same_state((12, -2, 1.0), (12, -2, 2.0), 10, 0)  # frozen, thresholds differ
-    assert stream.same_state((12, -2, 1.0), (12, -2, 2.0), 10, 50)     # before F0 thr0 rules
-    assert not stream.same_state((-1, 9, 1.0), (-1, -2, 1.0), 10, 0)   # adjacency of the last run
-    s = (123, -2, float("nan"))
-    assert stream._unpack(stream._pack(s))[:2] == s[:2]
+    assert stream.same_state((-1, -2, 1.0, 3, 0.0), (5, -2, 2.0, 4, 0.0), 10, 0)       # both unfrozen
+    assert not stream.same_state((12, -2, 1.0, 3, 0.0), (12, -2, 2.0, 3, 0.0), 10, 0)  # frozen, thresholds differ
+    assert not stream.same_state((12, -2, 1.0, 3, 0.0), (12, -2, 1.0, 4, 0.0), 10, 0)  # same value, other window
+    assert stream.same_state((12, -2, 1.0, 3, 0.0), (12, -2, 2.0, -1, 0.0), 10, 50)    # before F0 thr0 rules
+    assert not stream.same_state((-1, 9, 1.0, 3, 0.0), (-1, -2, 1.0, 3, 0.0), 10, 0)   # adjacency of the last run
+    s = (123, -2, float("nan"), 77, 1.5e-3)
+    u = stream._unpack(stream._pack(s))
+    assert u[:2] == s[:2] and u[3:] == s[3:]
+    assert stream.clean_state(2.5, 1e-3) == (-1, -2, 2.5, -1, 1e-3)
 
 
 def _gloo_rank(rank, world, port, out):
