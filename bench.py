@@ -64,6 +64,9 @@ def parse():
                     "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 run appended to the line (key \"c5\")")
+    ap.add_argument("--c5-mode", choices=("exact", "flag", "off"), default="exact",
+                    help="C5 decisions: exact = certified against the float64 reference, uncertain ones refined "
+                         "(the product default); flag = certified, not refined; off = no certification (A/B)")
     ap.add_argument("--shard-day", action="store_true",
                     help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
                          "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "
@@ -263,7 +266,8 @@ def run_c5(a, ctx, job, rank, world):
     shard = int(C5_FS * a.c5_seconds)
     n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
-                             rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")))
+                             rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")),
+                             certify=a.c5_mode != "off")
     chunk = C5_FS * 60
     pool = []
     for j in range(4):  # seeded 1-minute chunks: noise + meteor pings at +1 kHz, int16 I/Q interleaved
@@ -283,7 +287,7 @@ def run_c5(a, ctx, job, rank, world):
 
     def step():
         det.spectrogram_and_delta()
-        return det.detect(comm, thresholds=False)
+        return det.detect(comm, thresholds=False, exact_decisions=a.c5_mode == "exact")
 
     def sync_all():
         ctx.synchronize()
@@ -314,7 +318,7 @@ def run_c5(a, ctx, job, rank, world):
     sync_all()
     kms = {}
     for name, kid in (("cstft", _lib.K_CSTFT), ("band_delta", _lib.K_IQDELTA), ("fresh_thresholds", _lib.K_FRESH),
-                      ("scan", _lib.K_SSCAN)):
+                      ("scan", _lib.K_SSCAN), ("refine_delta64", _lib.K_REFINE)):
         ms, cnt = ctx.timing_get(kid)
         kms[name] = round(ms, 4)
     kms["cstft"] = round(k_ms / max(k_n, 1), 4)  # the timed region's average
@@ -343,11 +347,11 @@ def run_c5(a, ctx, job, rank, world):
         "exact_threshold_frames": int(res.refined),
         # every step certifies each decision against the float64 reference and recomputes in float64
         # the delta the uncertain ones depend on (meteorgpu.iq.IQShardDetector.detect)
-        "certification": {"certified": bool(res.certified), "near_tie": bool(res.near_tie),
-                          "uncertain_before_refinement": int(res.uncertain_initial),
-                          "refined_delta_frames": int(res.refined_delta_frames),
-                          "detector_passes": int(res.detector_passes),
-                          "decision_bound_db": float(res.decision_bound), "min_slack_db": float(res.min_slack)},
+        "certification": None if res.certified is None else {
+            "mode": a.c5_mode, "certified": bool(res.certified), "near_tie": bool(res.near_tie),
+            "uncertain_before_refinement": int(res.uncertain_initial),
+            "refined_delta_frames": int(res.refined_delta_frames), "detector_passes": int(res.detector_passes),
+            "decision_bound_db": float(res.decision_bound), "min_slack_db": float(res.min_slack)},
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": c5_traffic[0], "traffic_source": c5_traffic[1],

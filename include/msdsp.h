@@ -210,11 +210,14 @@ int msd_cstft_set_detrend(msd_cstft_plan *plan, int detrend);
 int64_t msd_cstft_frames(const msd_cstft_plan *plan, int64_t n);
 int msd_cstft_psd_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                       int64_t nstreams, int64_t max_frames, float *out);
-/* the same, plus (etot != NULL) each frame's total power sum_k out[k] as 16 float32 partial sums,
- * etot[(s*max_frames + t)*16 + i] (device): Parseval's input norm for the fp32 FFT's per-bin error
- * bound (msd_iq_band_delta_bound_dev) */
+/* the same, plus (etot != NULL) an upper bound of each frame's total power sum_k out[k] as 16
+ * float32 partials, etot[i*stride + s*max_frames + t] (device, stride =
+ * msd_cstft_energy_stride(nstreams, max_frames)): Parseval's input norm for the fp32 FFT's
+ * per-bin error bound (msd_iq_band_delta_bound_dev); each partial is the max over a group of up to
+ * 4 consecutive frames */
 int msd_cstft_psd_energy_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                              int64_t nstreams, int64_t max_frames, float *out, float *etot);
+int64_t msd_cstft_energy_stride(int64_t nstreams, int64_t max_frames);
 /* one stream, host buffers: n complex samples in, out float32 [T][N] */
 int msd_cstft_psd(msd_cstft_plan *plan, const void *x, int dtype, int64_t n, float *out, int64_t *frames);
 

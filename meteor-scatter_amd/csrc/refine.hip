@@ -22,6 +22,7 @@
 // stays uncertain after refinement is a genuine float64 near tie.
 #include <cmath>
 #include <numeric>
+#include <type_traits>
 #include <vector>
 
 #include "msd_internal.h"
@@ -41,7 +42,7 @@ struct RefineBins {
 };
 
 struct RefineGeom {
-    int N, D, R, L;           // frame, block, blocks per frame, samples per lane (D >= 64: D / 64)
+    int N, D, R, L;           // frame, block, blocks per frame, samples per Goertzel segment
     int64_t hop;
     double scale;             // density: 1 / (fs sum w^2)
     double chain;             // our float64 rounding chain + the reference's, in units of u
@@ -71,11 +72,6 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
 // the range holding compact index g: ranges' compact starts cs[0..nr] (cs[nr] = total)
 __device__ __forceinline__ int find_range(const int64_t *cs, int nr, int64_t g) {
     int lo = 0, hi = nr - 1;
@@ -87,62 +83,121 @@ __device__ __forceinline__ int find_range(const int64_t *cs, int nr, int64_t g) 
     return lo;
 }
 
-// one wave per block (D >= 64): lane L runs the Goertzel recurrence of every needed bin over
-// samples [L*S, (L+1)*S) of the block (S = D/64), rotates the segment's DFT to the block origin
-// with two table twiddles, and the wave sums the 64 partials.  out[g]: [nk] B values, then the
-// block's sample sum and sum of |re| + |im| (as .x of one more double2).
+// double DPP moves (both halves), for row reductions of float64 values
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    const long long v = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(v & 0xffffffffll), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), CTRL, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+// every lane of a row of 16 gets the row's sum
+__device__ __forceinline__ double row_sum_d(double v) {
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    v += dpp_d<0x140>(v);
+    return v;
+}
+
 template <typename T>
+struct Quad;  // four consecutive complex samples per load
+template <>
+struct Quad<int16_t> {
+    __device__ static void load(const int16_t *x, int64_t i, double2 (&z)[4]) {
+        const uint4 r = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(x) + i);
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] = make_double2((double)(int16_t)(w[e] & 0xffffu), (double)(int16_t)(w[e] >> 16));
+    }
+};
+template <>
+struct Quad<float> {
+    __device__ static void load(const float *x, int64_t i, double2 (&z)[4]) {
+        const float4 a = *reinterpret_cast<const float4 *>(x + 2 * i);
+        const float4 b = *reinterpret_cast<const float4 *>(x + 2 * i + 4);
+        z[0] = make_double2(a.x, a.y);
+        z[1] = make_double2(a.z, a.w);
+        z[2] = make_double2(b.x, b.y);
+        z[3] = make_double2(b.z, b.w);
+    }
+};
+
+// D >= 64: sixteen lanes per block (a row of the wave), lane L the D/16 consecutive samples from
+// L D/16; one pass over the samples runs the Goertzel recurrence of every needed bin (up to NK),
+// each segment's DFT is rotated to the block origin with two table twiddles, and the row sums the
+// 16 partials.  out[g]: [nk] B values, then the block's sample sum and sum of |re| + |im| (.x).
+template <typename T, int NK>
 __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, RefineGeom G, RefineBins K,
                                                     const int64_t *__restrict__ bstart, const int64_t *__restrict__ bcs,
                                                     int64_t nblocks, const double2 *__restrict__ W,
                                                     double2 *__restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (g >= nblocks) return;
+    const int l16 = threadIdx.x & 15;
+    int64_t g = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+    const bool live = g < nblocks;
+    if (!live) g = nblocks - 1;  // the row still takes part in nothing but its own DPP sums
     const int r = find_range(bcs, G.nr, g);
     const int64_t m = bstart[r] + (g - bcs[r]);
-    const int S = G.L;
-    const int64_t n0 = (int64_t)lane * S;
+    const int S = G.D / 16;  // samples per lane (a multiple of 4)
+    const int64_t n0 = (int64_t)l16 * S;
     const int64_t base = m * (int64_t)G.D + n0;
+    double c2[NK];
+    double2 s1[NK], s2[NK];
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+        const int km = b < K.nk ? ((K.k[b] % G.N) + G.N) % G.N : 0;
+        c2[b] = 2.0 * W[km].x;  // 2 cos(theta)
+        s1[b] = make_double2(0.0, 0.0);
+        s2[b] = make_double2(0.0, 0.0);
+    }
     double2 sum = make_double2(0.0, 0.0);
     double l1 = 0.0;
-    for (int q = 0; q < S; ++q) {
-        const double2 z = Samp<T>::at(x, base + q);
-        sum = cadd(sum, z);
-        l1 += fabs(z.x) + fabs(z.y);
+    // the recurrence s_n = z_n + 2 cos(theta) s_{n-1} - s_{n-2}, two samples per step with the roles
+    // of s1 / s2 alternating (no register moves): s2 <- fma(c2, s1, z0 - s2), s1 <- fma(c2, s2, z1 - s1)
+    for (int q = 0; q < S; q += 4) {
+        double2 z[4];
+        Quad<T>::load(x, base + q, z);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sum = cadd(sum, z[e]);
+            l1 += fabs(z[e].x) + fabs(z[e].y);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+#pragma unroll
+            for (int b = 0; b < NK; ++b) {
+                if (b < K.nk) {
+                    s2[b] = make_double2(fma(c2[b], s1[b].x, z[e].x - s2[b].x), fma(c2[b], s1[b].y, z[e].y - s2[b].y));
+                    s1[b] = make_double2(fma(c2[b], s2[b].x, z[e + 1].x - s1[b].x),
+                                         fma(c2[b], s2[b].y, z[e + 1].y - s1[b].y));
+                }
+            }
+        }
     }
     double2 *o = out + g * (K.nk + 2);
-    for (int b = 0; b < K.nk; ++b) {
-        const int kk = K.k[b];
-        const int km = ((kk % G.N) + G.N) % G.N;
-        double2 contrib;
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+        if (b >= K.nk) continue;
+        const int km = ((K.k[b] % G.N) + G.N) % G.N;
+        double2 c;
         if (km == 0) {
-            contrib = sum;
-        } else {
-            const double c2 = 2.0 * W[km].x;  // 2 cos(theta)
-            double2 s1 = make_double2(0.0, 0.0), s2 = make_double2(0.0, 0.0);
-            for (int q = 0; q < S; ++q) {
-                const double2 z = Samp<T>::at(x, base + q);
-                const double2 s0 = make_double2(z.x + c2 * s1.x - s2.x, z.y + c2 * s1.y - s2.y);
-                s2 = s1;
-                s1 = s0;
-            }
-            // sum_q z[n0 + q] W^{k (n0 + q)} = W^{k (n0 + S - 1)} s_{S-1} - W^{k (n0 + S)} s_{S-2}
+            c = sum;
+        } else {  // sum_q z[n0 + q] W^{k (n0 + q)} = W^{k (n0 + S - 1)} s_{S-1} - W^{k (n0 + S)} s_{S-2}
             const double2 t1 = W[(int)(((int64_t)km * (n0 + S - 1)) % G.N)];
             const double2 t2 = W[(int)(((int64_t)km * (n0 + S)) % G.N)];
-            contrib = csub(cmul(t1, s1), cmul(t2, s2));
+            c = csub(cmul(t1, s1[b]), cmul(t2, s2[b]));
         }
-        const double rx = wave_sum_d(contrib.x), ry = wave_sum_d(contrib.y);
-        if (lane == 0) o[b] = make_double2(rx, ry);
+        c = make_double2(row_sum_d(c.x), row_sum_d(c.y));
+        if (live && l16 == 0) o[b] = c;
     }
-    const double sx = wave_sum_d(sum.x), sy = wave_sum_d(sum.y), sl = wave_sum_d(l1);
-    if (lane == 0) {
+    const double sx = row_sum_d(sum.x), sy = row_sum_d(sum.y), sl = row_sum_d(l1);
+    if (live && l16 == 0) {
         o[K.nk] = make_double2(sx, sy);
         o[K.nk + 1] = make_double2(sl, 0.0);
     }
 }
 
-// D < 64: one lane per block (a Goertzel recurrence over its D samples)
+// D < 64: one lane per block (a direct DFT over its D samples)
 template <typename T>
 __global__ __launch_bounds__(256) void block_small_kernel(const T *__restrict__ x, RefineGeom G, RefineBins K,
                                                           const int64_t *__restrict__ bstart,
@@ -197,32 +252,28 @@ __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, 
     if (f >= nframes) return;
     const int r = find_range(fcs, G.nr, f);
     const int64_t t = fstart[r] + (f - fcs[r]);
-    const int64_t m0 = t * G.hop / G.D;               // first block of the frame
-    const int64_t g0 = bcs[r] + (m0 - bstart[r]);     // its compact index
+    const int64_t m0 = t * G.hop / G.D;            // first block of the frame
+    const double2 *b0 = blk + (bcs[r] + (m0 - bstart[r])) * (int64_t)(K.nk + 2);
     const int stride = K.nk + 2;
-    // mean and L1 of the frame
     double2 sum = make_double2(0.0, 0.0);
     double l1 = 0.0;
     for (int j = 0; j < G.R; ++j) {
-        sum = cadd(sum, blk[(g0 + j) * stride + K.nk]);
-        l1 += blk[(g0 + j) * stride + K.nk + 1].x;
+        sum = cadd(sum, b0[j * stride + K.nk]);
+        l1 += b0[j * stride + K.nk + 1].x;
     }
     const double2 mean = make_double2(sum.x / G.N, sum.y / G.N);
-    double2 V[RF_MAXK];
-    for (int b = 0; b < K.nk; ++b) {
+    // V[k'] of the detrended frame at needed bin b
+    auto V = [&](int b) {
         const int km = ((K.k[b] % G.N) + G.N) % G.N;
-        double2 z = make_double2(0.0, 0.0);
-        for (int j = 0; j < G.R; ++j) {
-            const double2 bv = blk[(g0 + j) * stride + b];
-            z = cadd(z, j == 0 ? bv : cmul(W[(int)(((int64_t)km * j * G.D) % G.N)], bv));
-        }
+        double2 z = b0[b];
+        for (int j = 1; j < G.R; ++j) z = cadd(z, cmul(W[(int)(((int64_t)km * j * G.D) % G.N)], b0[j * stride + b]));
         if (km == 0) z = csub(z, make_double2(mean.x * G.N, mean.y * G.N));
-        V[b] = z;
-    }
+        return z;
+    };
     auto energy = [&](const int (*idx)[3], int n) {
         double E = 0.0;
         for (int q = 0; q < n; ++q) {
-            const double2 a = V[idx[q][0]], c = V[idx[q][1]], e = V[idx[q][2]];
+            const double2 a = V(idx[q][0]), c = V(idx[q][1]), e = V(idx[q][2]);
             const double2 y = make_double2(0.5 * c.x - 0.25 * a.x - 0.25 * e.x, 0.5 * c.y - 0.25 * a.y - 0.25 * e.y);
             E += (y.x * y.x + y.y * y.y) * G.scale;
         }
@@ -293,7 +344,7 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     G.hop = hop;
     G.D = (int)std::gcd((int64_t)N, hop);
     G.R = N / G.D;
-    G.L = G.D >= 64 ? G.D / 64 : 1;
+    G.L = G.D >= 64 ? G.D / 16 : G.D;  // samples per Goertzel segment
     // periodic Hann: sum w^2 = 3N/8 exactly; scipy's scale 1/(fs * sum(w^2)) from its float64 window
     {
         double sw = 0.0;
@@ -312,10 +363,11 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
         const int km = ((K.k[i] % N) + N) % N;
         if (km == 0) continue;
         const double sn = std::fabs(std::sin(2.0 * M_PI * km / N));
-        gmax = std::max(gmax, std::min(sn > 0 ? 1.0 / sn : 1e300, (double)(G.D >= 64 ? G.L : G.D)));
+        gmax = std::max(gmax, std::min(sn > 0 ? 1.0 / sn : 1e300, (double)G.L));
     }
-    const double Lc = G.D >= 64 ? G.L : G.D;
-    G.chain = 3.0 * Lc * gmax + 8.0 + 6.0 + (G.R + 4.0) + 8.0 + 4.0 * std::log2((double)N) + 11.0;
+    // the D < 64 path sums D direct products (D + 4); the Goertzel path 3 L Gmax + 8 and the 16-lane sum
+    const double own = G.D >= 64 ? 3.0 * G.L * gmax + 8.0 + 4.0 : (double)G.D + 4.0;
+    G.chain = own + (G.R + 4.0) + 8.0 + 4.0 * std::log2((double)N) + 11.0;
     if (nranges == 0) return MSD_OK;
     // frame ranges -> block ranges, compact prefix counts
     std::vector<int64_t> fstart(nranges), fcs(nranges + 1), bstart(nranges), bcs(nranges + 1);
@@ -358,14 +410,23 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     hipError_t e = hipMemcpyAsync(Wd, W.data(), nb_w, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(meta, hm.data(), sizeof(int64_t) * hm.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
-        if (G.D >= 64) {
-            const unsigned grid = (unsigned)((nblocks + 3) / 4);
-            if (dtype == MSD_CI16)
-                hipLaunchKernelGGL(block_kernel<int16_t>, dim3(grid), dim3(256), 0, st,
-                                   static_cast<const int16_t *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
-            else
-                hipLaunchKernelGGL(block_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float *>(x),
-                                   G, K, d_bstart, d_bcs, nblocks, Wd, blk);
+        KernelTimer timer(ctx, K_REFINE);
+        if (G.D >= 64) {  // rows of 16 lanes, S = D/16 (a multiple of 4) samples per lane
+            const unsigned grid = (unsigned)((nblocks + 15) / 16);
+            auto go = [&](auto nkc, const auto *xp) {
+                constexpr int NKC = decltype(nkc)::value;
+                using T = std::remove_cv_t<std::remove_pointer_t<decltype(xp)>>;
+                auto kern = block_kernel<T, NKC>;
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, xp, G, K, d_bstart, d_bcs, nblocks, Wd, blk);
+            };
+            auto by_nk = [&](const auto *xp) {  // register arrays sized to the bins (C5: 9)
+                if (K.nk <= 5) go(std::integral_constant<int, 5>{}, xp);
+                else if (K.nk <= 9) go(std::integral_constant<int, 9>{}, xp);
+                else if (K.nk <= 12) go(std::integral_constant<int, 12>{}, xp);
+                else go(std::integral_constant<int, RF_MAXK>{}, xp);
+            };
+            if (dtype == MSD_CI16) by_nk(static_cast<const int16_t *>(x));
+            else by_nk(static_cast<const float *>(x));
         } else {
             const unsigned grid = (unsigned)((nblocks + 255) / 256);
             if (dtype == MSD_CI16)

@@ -91,6 +91,8 @@ struct msd_stream_plan {
     // pageable destination costs a staged, host-synchronous copy each (≈ 18 µs per copy in the C5
     // step's timeline)
     void *h_pin = nullptr;
+    void *h_cert = nullptr;  // pinned staging of msd_stream_certificate
+    size_t h_cert_bytes = 0;
 };
 
 namespace msd {
@@ -118,10 +120,12 @@ struct PinHdr {  // head of msd_stream_plan::h_pin, then margins [nseg], then ch
 // the float64 reference (scipy.signal.spectrogram of complex128 input, its band sums and dB).
 // Standard model, per bin: the computed spectrum X^ of a linear FFT satisfies
 // |X^_k - X_k| <= c u sum_n |v_n| with c the longest rounding chain from an input to an output
-// (in units of u) and v the detrended, windowed frame.  cstft4096_kernel: detrend, window and its
-// rounding (3), three passes of a 16-point DFT (radix-4 x 4: 2 + 2 adds and an internal twiddle
-// multiply, 2 sqrt 2 u with FMA + sqrt 2 u for the rounded constant: 8.5 each) and the two
-// inter-pass twiddles (4.5 each): 37.5, taken as IQ_CHAIN = 40.  sum |v| <= sqrt(N) ||v||_2 =
+// (in units of u) and v the detrended, windowed frame: every operation multiplies the path terms
+// through it by (1 + theta), |theta| <= u for an add, <= 2 sqrt 2 u for a complex multiply with FMA
+// and sqrt 2 u more for a rounded twiddle, and each input reaches each bin by one path of unit
+// weight.  cstft4096_kernel: detrend, window and its rounding (3), three passes of a 16-point DFT
+// (radix-4 x 4: 2 + 2 adds and an internal twiddle multiply, 4 + 2.83 + 1.41 = 8.24 each) and the
+// two inter-pass twiddles (4.24 each): 36.2, taken as IQ_CHAIN = 37 (second-order terms).  sum |v| <= sqrt(N) ||v||_2 =
 // sqrt(S) with S = sum_k |X_k|^2 (Parseval), S from the kernel's energy partials (an upper bound
 // after the factor 1.001: their own rounding is ~1e-4 relative).  The reference's float64 chain
 // (pocketfft, 4 log2 N + 8, + 3 for detrend / window) adds its own, ~1e-9 of ours.  A band of n
@@ -129,7 +133,7 @@ struct PinHdr {  // head of msd_stream_plan::h_pin, then margins [nseg], then ch
 // moves by dE <= 2 d sqrt(n E) + 3 n d^2 + (n + 4) u E, its dB by 10/ln 10 * dE / (E + 1e-12 - dE)
 // (unbounded once dE >= E); delta by the sum of the two bands'.  A band touching bins -1..1 also
 // carries the frame mean's rounding (the DC offset's transform): not bounded here, +inf.
-constexpr double IQ_CHAIN = 40.0;
+constexpr double IQ_CHAIN = 37.0;
 
 __device__ __forceinline__ double band_db_bound(double E, int n, double d) {
     if (n <= 0) return 0.0;  // empty band: 1e-12 on both sides
@@ -170,8 +174,8 @@ __device__ __forceinline__ double band_energy4(const float *__restrict__ row, in
     return acc;
 }
 
-// etot / ed (both or neither): the frame's 16 energy partials (cstft4096_kernel<EN>) in, the delta
-// error bound out (above)
+// etot / ed (both or neither): the frame's 16 energy partials (cstft4096_kernel<EN>, [16][stride]) in,
+// the delta error bound out (above)
 __global__ __launch_bounds__(256) void iq_band_delta_kernel(const float *__restrict__ spec, int64_t nstreams,
                                                             int64_t max_frames, const int64_t *__restrict__ frames,
                                                             int N, int blo, int bhi, int nlo, int nhi,
@@ -190,14 +194,10 @@ __global__ __launch_bounds__(256) void iq_band_delta_kernel(const float *__restr
     if (noise_db) noise_db[s * ld + t] = nd;
     delta[s * ld + t] = bd - nd;
     if (ed) {
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v *ep = reinterpret_cast<const f4v *>(etot + (s * max_frames + t) * 16);
+        const int64_t es = (nstreams * max_frames + 3) / 4 * 4;  // msd_cstft_energy_stride
         double S = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f4v v = __builtin_nontemporal_load(ep + q);
-            S += ((double)v[0] + (double)v[1]) + ((double)v[2] + (double)v[3]);
-        }
+        for (int q = 0; q < 16; ++q) S += (double)__builtin_nontemporal_load(etot + q * es + s * max_frames + t);
         const double A = sqrt(S * 1.001);
         const double lg = log2((double)N);
         const double d = IQ_CHAIN * 0x1p-24 * A + (4.0 * lg + 11.0) * 0x1p-53 * sqrt((double)N) * A;
@@ -1334,6 +1334,7 @@ void msd_stream_plan_destroy(msd_stream_plan *p) {
     for (void *b : bufs)
         if (b) hipFree(b);
     if (p->h_pin) hipHostFree(p->h_pin);
+    if (p->h_cert) hipHostFree(p->h_cert);
     delete p;
 }
 
@@ -1522,28 +1523,40 @@ int msd_stream_certificate(msd_stream_plan *p, int64_t *uncertain, double *min_s
     if (p->nseg == 0) return MSD_OK;
     if (!p->scanned) return fail(MSD_ERR_INVALID, "msd_stream_certificate: call msd_stream_scan first");
     DeviceGuard g(p->ctx->device);
-    std::vector<int32_t> cnt(p->nseg);
-    std::vector<double2> sl(p->nseg);
-    MSD_HIP(hipMemcpy(cnt.data(), p->d_ucnt, sizeof(int32_t) * p->nseg, hipMemcpyDeviceToHost));
-    MSD_HIP(hipMemcpy(sl.data(), p->d_slack, sizeof(double2) * p->nseg, hipMemcpyDeviceToHost));
+    hipStream_t st = p->ctx->stream;
+    // pinned staging (grown once): counts and slacks in one round trip, the lists in a second one
+    // only when something is uncertain
+    const size_t need =
+        sizeof(double2) * p->nseg + sizeof(int32_t) * (p->nseg + 1) + sizeof(longlong2) * p->nseg * UCAP;
+    if (p->h_cert_bytes < need) {
+        if (p->h_cert) (void)hipHostFree(p->h_cert);
+        p->h_cert = nullptr;
+        p->h_cert_bytes = 0;
+        MSD_HIP(hipHostMalloc(&p->h_cert, need, hipHostMallocDefault));
+        p->h_cert_bytes = need;
+    }
+    auto *sl = static_cast<double2 *>(p->h_cert);
+    auto *cnt = reinterpret_cast<int32_t *>(sl + p->nseg);
+    auto *u = reinterpret_cast<longlong2 *>(cnt + p->nseg + (p->nseg & 1));
+    MSD_HIP(hipMemcpyAsync(sl, p->d_slack, sizeof(double2) * p->nseg, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(cnt, p->d_ucnt, sizeof(int32_t) * p->nseg, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
     int64_t tot = 0;
-    std::vector<int64_t> segs;
     for (int64_t q = 0; q < p->nseg; ++q) {
         tot += cnt[q];
         *min_slack = sl[q].x < *min_slack || sl[q].x != sl[q].x ? sl[q].x : *min_slack;
         *max_zone = sl[q].y > *max_zone ? sl[q].y : *max_zone;
-        if (cnt[q] > 0) segs.push_back(q);
     }
     *uncertain = tot;
     if (tot == 0 || !frames || !srcs || cap <= 0) return MSD_OK;
-    std::vector<longlong2> u(UCAP);
+    MSD_HIP(hipMemcpyAsync(u, p->d_unc, sizeof(longlong2) * p->nseg * UCAP, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipStreamSynchronize(st));
     int64_t n = 0;
-    for (int64_t q : segs) {
+    for (int64_t q = 0; q < p->nseg && n < cap; ++q) {
         const int32_t m = cnt[q] < UCAP ? cnt[q] : UCAP;
-        MSD_HIP(hipMemcpy(u.data(), p->d_unc + q * UCAP, sizeof(longlong2) * m, hipMemcpyDeviceToHost));
         for (int32_t r = 0; r < m && n < cap; ++r, ++n) {
-            frames[n] = p->frame0 + u[r].x;  // global frame index
-            srcs[n] = u[r].y;
+            frames[n] = p->frame0 + u[q * UCAP + r].x;  // global frame index
+            srcs[n] = u[q * UCAP + r].y;
         }
     }
     *listed = n;

