@@ -434,8 +434,9 @@ int msd_live_detect(msd_ctx *ctx, const double *band_db /* [3][nb] */, int64_t n
                     msd_meteor *out, int64_t cap, int64_t *count, double *thresholds, double *over);
 
 /* ------------------------------------------- a1 / §8(f)1: WAV ingest and uploads
- * scipy.io.wavfile.read semantics for the reference's files (dsp/src/main.py:249): RIFF
- * little-endian; PCM 8 → u8, 16 → i16, 24 → i32 (sample in the top 3 bytes), 32 → i32;
+ * scipy.io.wavfile.read semantics for the reference's files (dsp/src/main.py:249; the rules in
+ * csrc/wav_parse.h): RIFF little-endian; the sample container is nBlockAlign / nChannels; PCM
+ * 1..8 bits → u8, 2-byte → i16, 3-byte → i32 (sample in the top 3 bytes), 4-byte → i32;
  * IEEE float 32 / 64; WAVE_FORMAT_EXTENSIBLE.  msd_wav_read decodes frames
  * [frame0, frame0+nframes) of one channel (channel >= 0) or all (channel = -1, interleaved)
  * with pread straight into dst (host memory; pinned memory from msd_host_alloc lets the
@@ -443,7 +444,7 @@ int msd_live_detect(msd_ctx *ctx, const double *band_db /* [3][nb] */, int64_t n
 typedef struct {
     int32_t rate, channels, bits, format; /* format: 1 PCM, 3 IEEE float */
     int32_t dtype;                        /* MSD_* of the decoded samples */
-    int32_t reserved;
+    int32_t reserved;                     /* the file's bytes per sample (container) */
     int64_t frames;                       /* frames (samples per channel) */
     int64_t data_offset, data_bytes;
 } msd_wav_info;

@@ -28,6 +28,7 @@
 //   runs_kernel, db_kernel the shard's runs (merged over segment edges) and np.mean dB of each
 // FP contraction is off: numpy rounds every add / multiply separately.
 #include "msd_internal.h"
+#include "np_program.h"
 #include "np_reduce.h"
 
 #include <algorithm>
@@ -1172,30 +1173,6 @@ __global__ void db_kernel(const double *__restrict__ x, int64_t x0, msd_det *__r
     d[j].db = np_sum(ArrRef{x}, a - x0, m) / (double)m;
 }
 
-// numpy's np.sum association over n elements (8192-element chunks, each a pairwise tree with
-// leaves of <= 128) as leaf records for fresh_kernel
-void build_program(int64_t n, std::vector<int4> &rec) {
-    rec.clear();
-    struct Rec {
-        static void tree(int64_t base, int64_t m, std::vector<int4> &r) {
-            if (m <= 128) {
-                r.push_back(make_int4((int)base, (int)m, 0, 0));
-                return;
-            }
-            int64_t m2 = m / 2;
-            m2 -= m2 % 8;
-            tree(base, m2, r);
-            tree(base + m2, m - m2, r);
-            r.back().z += 1;  // the add combining the two halves follows the right half's last leaf
-        }
-    };
-    for (int64_t c = 0; c < n; c += CHUNK) {
-        const int64_t m = n - c < CHUNK ? n - c : CHUNK;
-        Rec::tree(c, m, rec);
-        rec.back().w = 1;
-    }
-}
-
 }  // namespace
 }  // namespace msd
 
@@ -1312,7 +1289,8 @@ int msd_stream_plan_create(msd_ctx *ctx, const msd_det_cfg *cfg, int64_t n_total
     if ((e = hipMalloc(&p->d_esum, sizeof(double2) * (xl / CHUNK + 2))) != hipSuccess)
         return cleanup(e, "hipMalloc esum");
     if (W > 0) {
-        std::vector<int4> prog;
+        std::vector<LeafRec> prog;  // np_program.h; LeafRec has int4's layout
+        static_assert(sizeof(LeafRec) == sizeof(int4), "leaf record layout");
         build_program(W, prog);
         p->nleaf = (int)prog.size();
         if ((e = hipMalloc(&p->d_prog, sizeof(int4) * prog.size())) != hipSuccess) return cleanup(e, "hipMalloc prog");

@@ -1,10 +1,10 @@
-"""WAV ingest/egress: the subset of ``scipy.io.wavfile.read`` the
-reference relies on (dsp/src/main.py:249), restated on numpy.
+"""WAV ingest/egress: ``scipy.io.wavfile.read`` as the reference uses it
+(dsp/src/main.py:249) and a writer.
 
-``read(path) -> (rate, data)`` returns the dtype scipy returns for the format:
-8-bit PCM → uint8, 16-bit → int16, 24-bit → int32 (sample in the top 3 bytes,
-like scipy), 32-bit PCM → int32, IEEE float 32/64 → float32/float64; one
-channel → shape (n,), several → (n, channels).  ``write`` emits PCM16 / float32.
+``read(path) -> (rate, data)`` is libmsdsp's native reader (meteorgpu.ingest.read): the dtype scipy
+returns for the format -- 8-bit PCM → uint8, 16-bit → int16, 24-bit → int32 (sample in the top 3
+bytes, like scipy), 32-bit PCM → int32, IEEE float 32/64 → float32/float64; one channel → shape
+(n,), several → (n, channels).  ``write`` emits PCM 8/16/32 or IEEE float 32/64.
 ``start_datetime_from_name`` restates the reference's file-name → UTC parsers
 (dsp/src/main.py:858-863 gqrx names, :917-923 BRAMS MESZ names).
 """
@@ -20,73 +20,12 @@ _PCM, _IEEE_FLOAT, _EXTENSIBLE = 0x0001, 0x0003, 0xFFFE
 
 
 def read(path: str | os.PathLike, mmap: bool = False):
-    with open(path, "rb") as fh:
-        head = fh.read(12)
-        if len(head) < 12 or head[8:12] != b"WAVE" or head[:4] not in (b"RIFF", b"RIFX", b"RF64"):
-            raise ValueError("File format {!r}... not understood. Only 'RIFF' WAV files are supported."
-                             .format(head[:4]))
-        if head[:4] == b"RIFX":
-            raise ValueError("big-endian RIFX files are not supported")
-        fmt = None
-        while True:
-            ch = fh.read(8)
-            if len(ch) < 8:
-                raise ValueError("Unexpected end of file: no data chunk")
-            cid, size = ch[:4], struct.unpack("<I", ch[4:8])[0]
-            if cid == b"fmt ":
-                raw = fh.read(size)
-                tag, channels, rate, _, block_align, bits = struct.unpack("<HHIIHH", raw[:16])
-                if tag == _EXTENSIBLE and len(raw) >= 26:
-                    tag = struct.unpack("<H", raw[24:26])[0]
-                fmt = (tag, channels, rate, block_align, bits)
-                if size % 2:
-                    fh.read(1)
-            elif cid == b"data":
-                if fmt is None:
-                    raise ValueError("No fmt chunk before data")
-                tag, channels, rate, block_align, bits = fmt
-                start = fh.tell()
-                fsize = os.fstat(fh.fileno()).st_size
-                size = min(size, fsize - start)
-                break
-            else:
-                fh.seek(size + (size % 2), 1)
-    tag, channels, rate, block_align, bits = fmt
-    bytes_per = bits // 8
-    if tag == _PCM:
-        if bits == 8:
-            dt = np.dtype(np.uint8)
-        elif bits == 16:
-            dt = np.dtype("<i2")
-        elif bits == 32:
-            dt = np.dtype("<i4")
-        elif bits == 24:
-            dt = None
-        else:
-            raise ValueError(f"Unsupported bit depth: the WAV file has {bits}-bit integer data.")
-    elif tag == _IEEE_FLOAT:
-        if bits == 32:
-            dt = np.dtype("<f4")
-        elif bits == 64:
-            dt = np.dtype("<f8")
-        else:
-            raise ValueError(f"Unsupported bit depth: the WAV file has {bits}-bit floating-point data.")
-    else:
-        raise ValueError(f"Unknown wave file format: {tag:#06x}. Supported formats: PCM, IEEE_FLOAT")
-    n_frames = size // (bytes_per * channels) if bytes_per and channels else 0
-    if dt is None:  # 24-bit: pad each sample into the top 3 bytes of an int32
-        raw = np.fromfile(path, dtype=np.uint8, count=n_frames * channels * 3, offset=start)
-        a = np.zeros((n_frames * channels, 4), dtype=np.uint8)
-        a[:, 1:] = raw.reshape(-1, 3)
-        data = a.view("<i4").reshape(-1)
-    elif mmap:
-        data = np.memmap(path, dtype=dt, mode="c", offset=start, shape=(n_frames * channels,))
-    else:
-        data = np.fromfile(path, dtype=dt, count=n_frames * channels, offset=start)
-    data = data.astype(data.dtype.newbyteorder("="), copy=False)
-    if channels > 1:
-        data = data.reshape(-1, channels)
-    return rate, data
+    """scipy.io.wavfile.read(path) through libmsdsp's native reader (msd_wav_probe / msd_wav_read:
+    csrc/wav_parse.h, scipy's header rules, checked against scipy on well-formed and malformed files
+    under AddressSanitizer in tests/test_sanitize.py).  Host code only, no GPU.  ``mmap`` is
+    accepted for signature parity; the samples are always read into memory."""
+    from . import ingest
+    return ingest.read(path)
 
 
 def write(path: str | os.PathLike, rate: int, data: np.ndarray) -> None:
