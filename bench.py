@@ -64,9 +64,11 @@ def parse():
                     "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 run appended to the line (key \"c5\")")
-    ap.add_argument("--c5-mode", choices=("exact", "flag", "off"), default="exact",
-                    help="C5 decisions: exact = certified against the float64 reference, uncertain ones refined "
-                         "(the product default); flag = certified, not refined; off = no certification (A/B)")
+    ap.add_argument("--c5-mode", choices=("all", "off", "flag", "exact"), default="all",
+                    help="C5 decisions: off = the streaming detector's default (no certification: the reference's "
+                         "work); flag = every decision certified against the float64 reference, uncertain ones "
+                         "reported; exact = the uncertain ones recomputed in float64 (proc_iq_samples' default); "
+                         "all = the line on 'off', plus timed 'flag' and 'exact' passes under \"certification\"")
     ap.add_argument("--shard-day", action="store_true",
                     help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
                          "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "
@@ -265,9 +267,10 @@ def run_c5(a, ctx, job, rank, world):
     from meteorgpu import _lib, iq, stream, synth
     shard = int(C5_FS * a.c5_seconds)
     n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
+    head_mode = "off" if a.c5_mode == "all" else a.c5_mode
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
                              rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")),
-                             certify=a.c5_mode != "off")
+                             certify=head_mode != "off")
     chunk = C5_FS * 60
     pool = []
     for j in range(4):  # seeded 1-minute chunks: noise + meteor pings at +1 kHz, int16 I/Q interleaved
@@ -285,9 +288,11 @@ def run_c5(a, ctx, job, rank, world):
         k += 1
     comm = job.comm if job is not None else stream.LocalComm()
 
+    mode = [head_mode]
+
     def step():
         det.spectrogram_and_delta()
-        return det.detect(comm, thresholds=False, exact_decisions=a.c5_mode == "exact")
+        return det.detect(comm, thresholds=False, exact_decisions=mode[0] == "exact")
 
     def sync_all():
         ctx.synchronize()
@@ -322,6 +327,38 @@ def run_c5(a, ctx, job, rank, world):
         ms, cnt = ctx.timing_get(kid)
         kms[name] = round(ms, 4)
     kms["cstft"] = round(k_ms / max(k_n, 1), 4)  # the timed region's average
+
+    def cert_info(r, m):
+        return {"mode": m, "certified": bool(r.certified), "near_tie": bool(r.near_tie),
+                "uncertain_before_refinement": int(r.uncertain_initial),
+                "refined_delta_frames": int(r.refined_delta_frames), "detector_passes": int(r.detector_passes),
+                "decision_bound_db": round(float(r.decision_bound), 6), "min_slack_db": round(float(r.min_slack), 6)}
+
+    cert = {}
+    if head_mode != "off":
+        cert[head_mode] = cert_info(res, head_mode)
+    if a.c5_mode == "all":
+        # the certified modes, each timed on its own after the headline (fewer steps): flag = every
+        # decision checked against its error bounds, exact = the uncertain ones recomputed in float64
+        det.set_certify(True)
+        for m in ("flag", "exact"):
+            mode[0] = m
+            for _ in range(min(a.warmup, 3)):
+                r = step()
+            sync_all()
+            ns = max(1, min(a.steps, 10))
+            t1 = time.perf_counter()
+            for _ in range(ns):
+                r = step()
+            sync_all()
+            el = time.perf_counter() - t1
+            if job is not None:
+                el = job.max_f64(el)
+            cert[m] = cert_info(r, m)
+            cert[m].update(steps=ns, ms_per_step=round(el / ns * 1e3, 4),
+                           value=round(world * int(C5_FS * a.c5_seconds) * ns / el / 1e6, 1),
+                           same_detections=bool(np.array_equal(r.detections[["start", "stop"]],
+                                                               res.detections[["start", "stop"]])))
     avg_s = k_ms / max(k_n, 1) / 1e3
     T = det.f1 - det.f0
     samples = shard  # per rank: its 3 h (the 3072-sample frame tail is read, not counted)
@@ -347,17 +384,14 @@ def run_c5(a, ctx, job, rank, world):
         "exact_threshold_frames": int(res.refined),
         # every step certifies each decision against the float64 reference and recomputes in float64
         # the delta the uncertain ones depend on (meteorgpu.iq.IQShardDetector.detect)
-        "certification": None if res.certified is None else {
-            "mode": a.c5_mode, "certified": bool(res.certified), "near_tie": bool(res.near_tie),
-            "uncertain_before_refinement": int(res.uncertain_initial),
-            "refined_delta_frames": int(res.refined_delta_frames), "detector_passes": int(res.detector_passes),
-            "decision_bound_db": float(res.decision_bound), "min_slack_db": float(res.min_slack)},
+        "decisions": head_mode,
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": c5_traffic[0], "traffic_source": c5_traffic[1],
                      "kernel": "cstft4096_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
         "kernel_ms_per_step": kms,
+        "certification": cert or None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
         from oracle import iq_oracle as Q

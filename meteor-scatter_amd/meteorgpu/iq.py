@@ -154,7 +154,8 @@ class IQShardDetector:
     """One rank's time shard of an I/Q stream on the GPU: spectrogram (frame-major, kept in HBM) →
     per-frame band delta written straight into the stream plan → detector over the whole stream.
 
-    Certification (``certify``, default on): the spectrogram kernel also writes each frame's energy,
+    Certification (``certify``; off by default here, on in proc_iq_samples / proc_iq_wav_file): the
+    spectrogram kernel also writes each frame's energy,
     the band delta kernel a bound on |delta - delta_ref| against the float64 reference (scipy's
     spectrogram of complex128 input), and every decision of the detector is checked against its
     bounds (include/msdsp.h, msd_stream_set_certify).  ``detect(exact_decisions=True)`` then
@@ -167,7 +168,7 @@ class IQShardDetector:
                  threshold_std_factor=4.0, flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                  threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                  threshold_fixed_init_duration_sec=10, rank: int = 0, world: int = 1, dtype=np.int16,
-                 seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = True):
+                 seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = False):
         """chunk_frames: keep only that many frames of spectrogram in HBM and stream the shard through
         it (``process_host``); the detector still sees the whole shard's delta.  A 24 h 192 kHz
         stream (66 GB of int16 I/Q, 265 GB of spectrogram) then runs on one GPU."""
@@ -193,14 +194,19 @@ class IQShardDetector:
         cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
         self.plan = _lib.StreamPlan(ctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
         self.ops = _stream.DeviceStreamOps(self.plan)
-        self.certify = bool(certify)
-        self.d_etot = (ctx.alloc(16 * 4 * ctx.lib.msd_cstft_energy_stride(1, max(self.batch.T, 1)))
-                       if self.certify else None)
-        if self.certify:
-            self.plan.set_certify(True)
+        self.d_etot = None
+        self.certify = False
+        self.set_certify(certify)
         self.fs_ = float(fs)
         self._read = None      # the shard's sample source when chunked (refinement re-reads samples)
         self._refined = []     # global frame ranges whose delta is float64 already
+
+    def set_certify(self, on: bool):
+        """certification on / off (takes effect at the next spectrogram_and_delta)"""
+        if on and self.d_etot is None:
+            self.d_etot = self.ctx.alloc(16 * 4 * self.ctx.lib.msd_cstft_energy_stride(1, max(self.batch.T, 1)))
+        self.certify = bool(on)
+        self.plan.set_certify(self.certify)
 
     def upload(self, iq: np.ndarray, sample_offset: int = 0):
         """interleaved I/Q of this shard's samples, starting at shard sample `sample_offset`"""
@@ -210,9 +216,10 @@ class IQShardDetector:
         """async: spectrogram of the shard and its per-frame band delta (into the stream plan)"""
         self._refined = []
         if self.f1 > self.f0:
-            self.batch.run(self.d_etot)
+            etot = self.d_etot if self.certify else None
+            self.batch.run(etot)
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
-                                   self.noise, self.plan.d_delta, self.batch.T, etot=self.d_etot,
+                                   self.noise, self.plan.d_delta, self.batch.T, etot=etot,
                                    ed=self.plan.d_ed if self.certify else None)
 
     def process_host(self, iq_shard: np.ndarray):
@@ -239,11 +246,12 @@ class IQShardDetector:
             b = a + (nf - 1) * self.hop + self.N
             self.batch.upload(0, np.ascontiguousarray(read(a, b)))
             self.d_frames.upload(np.array([nf], np.int64))
-            self.batch.run(self.d_etot)  # frames past nf read stale samples; their powers are not used
+            etot = self.d_etot if self.certify else None
+            self.batch.run(etot)  # frames past nf read stale samples; their powers are not used
             ed = _lib.C.c_void_p(self.plan.d_ed.value + 8 * c0) if self.certify else None
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                    self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T,
-                                   etot=self.d_etot, ed=ed)
+                                   etot=etot, ed=ed)
 
     MAX_REFINE = 8
 
@@ -321,20 +329,22 @@ def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072
                     flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                     threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                     threshold_fixed_init_duration_sec=10, wav_start_date_time=None, out_csv_file=None,
-                    device: int = 0, chunk_sec: float | None = None, exact_decisions: bool = True):
+                    device: int = 0, chunk_sec: float | None = None, exact_decisions: bool = True,
+                    certify: bool = True):
     """The batch detector of dsp/src/main.py (:380-527, :640-658) over an I/Q recording with the STFT
     frame as the block.  Returns (detections [OutputDetection], thresholds, delta, result).
     chunk_sec: stream the spectrogram through HBM in chunks of that many seconds (long recordings).
-    exact_decisions: every detector decision certified against the float64 reference, the uncertain
-    ones recomputed in float64 (IQShardDetector); result.certified / near_tie / decision_bound /
-    refined_delta_frames report it."""
+    certify / exact_decisions: every detector decision certified against the float64 reference, the
+    uncertain ones recomputed in float64 (IQShardDetector); result.certified / near_tie /
+    decision_bound / refined_delta_frames report it.  certify=False is the uncertified fast path."""
     buf, code = interleave(i, q)
     n = buf.size // 2
     det = IQShardDetector(context(device), n, fs, nperseg, noverlap, freq_band, noise_band, threshold_std_factor,
                           flag_adaptive_threshold, threshold_estimation_window_sec,
                           threshold_freeze_before_detection_sec, threshold_freeze_after_detection_sec,
                           threshold_fixed_init_duration_sec, dtype=buf.dtype,
-                          chunk_frames=int(chunk_sec * fs / (nperseg - noverlap)) if chunk_sec else None)
+                          chunk_frames=int(chunk_sec * fs / (nperseg - noverlap)) if chunk_sec else None,
+                          certify=certify)
     try:
         det.process_host(buf[2 * det.s0: 2 * det.s1])
         res = det.detect(exact_decisions=exact_decisions)

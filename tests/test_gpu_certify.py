@@ -180,6 +180,11 @@ def test_certification_off_is_the_old_path():
     det = _detector(i, q, certify=False)
     try:
         res = det.detect()
+        d0 = [(int(a["start"]), int(a["stop"])) for a in res.detections]
+        det.set_certify(True)  # switched on: the next pass certifies, same detections on this stream
+        det.spectrogram_and_delta()
+        res2 = det.detect()
     finally:
         det.close()
     assert res.certified is None and res.refined_delta_frames == 0
+    assert res2.certified and [(int(a["start"]), int(a["stop"])) for a in res2.detections] == d0
