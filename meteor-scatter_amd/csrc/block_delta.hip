@@ -121,6 +121,7 @@ __global__ __launch_bounds__(BD_WAVES * 64) void block_delta_kernel(
 // in LDS.  Bins are carried 8 per sweep over the samples, the remainder in one sized sweep.
 constexpr int BD2_GROUPS = 16;  // blocks per 256-thread workgroup
 constexpr int BD2_MAXBINS = 64;
+constexpr int bd2_pitch(int spl) { return spl | 1; }  // odd window pitch in doubles (see the kernel)
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double x) {
@@ -212,9 +213,12 @@ __global__ __launch_bounds__(256) void block_delta2_kernel(
     int nband, int nnoise, double *__restrict__ band_db, double *__restrict__ noise_db, double *__restrict__ delta,
     int64_t ld) {
     extern __shared__ double smem_d[];
-    // window [16 segments][SPL + 2]: the pad puts segment s at bank offset 4s (conflict-free
-    // reads across the 16 lanes of a block; the 4 blocks of a wave read the same addresses)
-    constexpr int WP = SPL + 2;
+    // window [16 segments][SPL + 1]: the window reads are ds_read2_b64 (two accesses of 4 x 16
+    // lanes, bank = dword mod 32), so with an odd pitch segment s starts at bank 2s mod 32 and the
+    // 16 lanes of a block cover the 32 banks once (the 4 blocks of a wave read the same addresses).
+    // The rounds 1-2 pitch SPL + 2 put s and s + 8 on one bank: 8 extra LDS cycles per read, the
+    // 2.8e7 SQ_LDS_BANK_CONFLICT per C2 launch that tools/lds_bank_model.py reproduces.
+    constexpr int WP = bd2_pitch(SPL);
     double *win_all = smem_d;                    // [16][WP]
     double *pbuf = smem_d + 16 * WP;             // [16][nbins]
     const int tid = threadIdx.x;
@@ -284,7 +288,7 @@ int launch_bd2(msd_block_plan *p, const void *x, const int64_t *off, const int64
     const int64_t blocks = nfiles * max_blocks;
     // persistent grid: a few workgroups per CU, each walking groups of 16 blocks
     const int64_t grid = std::min<int64_t>((blocks + BD2_GROUPS - 1) / BD2_GROUPS, (int64_t)p->ctx->num_cu * 8);
-    const size_t lds = sizeof(double) * (16 * (SPL + 2) + BD2_GROUPS * (size_t)(p->nbins > 0 ? p->nbins : 1));
+    const size_t lds = sizeof(double) * (16 * bd2_pitch(SPL) + BD2_GROUPS * (size_t)(p->nbins > 0 ? p->nbins : 1));
     hipLaunchKernelGGL((block_delta2_kernel<T, SPL>), dim3((unsigned)grid), dim3(256), lds, p->ctx->stream,
                        static_cast<const T *>(x), off, len, nfiles, max_blocks, p->block_size, p->L, p->d_window,
                        p->d_bconst, p->band_hi - p->band_lo + 1 > 0 ? p->band_hi - p->band_lo + 1 : 0,

@@ -12,7 +12,9 @@ The instruction forms are the ones the compiler emits (hipcc -O3 -S of stft1024.
   tile writes              8 x ds_write_b64    rows pi + 64 r and 512 - pi - 64 r, column wcol
   write-out reads (per wave, 1/16 of the tile) 10 x b64 (paired into ds_read2_b64)
 Usage: python3 tools/lds_bank_model.py  -> extra conflict cycles per wave-iteration, with and
-without the tile row rotation (tile_rot in stft1024.hip).  Round 2 PMC, before the rotation:
+without the tile row rotation (tile_rot in stft1024.hip), then the same for block_delta2_kernel
+(block_delta.hip, per 16-block group sweep of one wave) at the window pitches SPL + 2 (rounds 1-2)
+and SPL + 1 (round 3).  Round 2 PMC, before the rotation:
 SQ_LDS_BANK_CONFLICT 1.298e8 per launch / 4.05 M wave-iterations = 32.0, the model's figure."""
 
 PI = [0, 32, 1, 63, 3, 61, 5, 59, 6, 58, 7, 57, 12, 52, 14, 50, 13, 51, 15, 49, 16, 48, 18, 46, 25, 39, 26, 38, 27,
@@ -36,9 +38,9 @@ def extra(addr, groups, nbanks):
     for g in groups:
         banks = {}
         for lane in g:
-            for a in addr[lane]:
+            for a in addr.get(lane, ()):  # inactive lanes take no part
                 banks.setdefault(a % nbanks, set()).add(a)
-        c += max(len(s) for s in banks.values()) - 1
+        c += max((len(s) for s in banks.values()), default=1) - 1
     return c
 
 
@@ -76,6 +78,38 @@ def model(rot):
     return out
 
 
+def bd2_model(spl, pitch, nband=5, nnoise=7, elem=8):
+    """block_delta2_kernel, one wave (4 blocks of 16 lanes, lane sub = l & 15) per group of blocks,
+    per sweep over the samples, in the forms hipcc -O3 emits for block_delta.hip:
+      window reads   SPL/2 x ds_read2_b64   win_all[sub * pitch + m], [.. + m + 1] (two accesses,
+                     each 4 x 16 contiguous lanes, bank (a/4) mod 32); the wave's 4 blocks read the
+                     same 16 addresses (broadcast)
+      |X|^2 writes   per bin ds_write_b64 by lane sub == 0 of each block (one lane per 16-lane group)
+      np_sum reads   ds_read_b64 by lanes sub 0 (band) and 1 (noise), pbuf[grp * nbins + i]"""
+    nb = nband + nnoise
+    out = {}
+    w = 0
+    for m in range(0, spl, 2):
+        for mm in (m, m + 1):
+            w += extra({l: [2 * ((l & 15) * pitch + mm) + i for i in range(2)] for l in range(64)}, G16, 32)
+    out["window reads"] = w
+    base = 16 * pitch  # pbuf after the window, in doubles
+    out["|X|^2 writes"] = sum(extra({l: [2 * (base + (l >> 4) * nb + j) + i for i in range(2)] for l in range(64)
+                                     if l & 15 == 0}, G16, 32) for j in range(nb))
+    r = 0
+    for i in range(max(nband, nnoise)):
+        addr = {}
+        for l in range(64):
+            sub, grp = l & 15, l >> 4
+            if sub == 0 and i < nband:
+                addr[l] = [2 * (base + grp * nb + i) + k for k in range(2)]
+            if sub == 1 and i < nnoise:
+                addr[l] = [2 * (base + grp * nb + nband + i) + k for k in range(2)]
+        r += extra(addr, G32, 64)
+    out["np_sum reads"] = r
+    return out
+
+
 if __name__ == "__main__":
     for name, rot in (("pitch 34, no rotation (round 2 before)", lambda k: 0),
                       ("pitch 34, tile_rot (rows 32/40/48/56 mod 64 by 16)", lambda k: 16 if (k & 39) == 32 else 0)):
@@ -83,3 +117,8 @@ if __name__ == "__main__":
         print(f"{name}: {sum(m.values()):g} extra cycles per wave-iteration")
         for k, v in m.items():
             print(f"    {k:16s} {v:g}")
+    for spl in (16, 32, 64, 128, 256):
+        for name, pitch in (("SPL + 2", spl + 2), ("SPL + 1", spl + 1)):
+            m = bd2_model(spl, pitch)
+            print(f"block_delta2 SPL {spl:3d}, window pitch {name}: {sum(m.values()):g} extra cycles per sweep "
+                  f"(" + ", ".join(f"{k} {v:g}" for k, v in m.items()) + ")")
