@@ -20,7 +20,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import _lib, wav
+from . import _lib, margin, wav
 from .dsp import context, hann_periodic
 
 
@@ -96,6 +96,16 @@ class DetectedMeteor:
     db_max: float
     db_mean: float
     db_std: float
+
+
+class LiveMeteors(list):
+    """``wav_file_process``'s meteors, with the near-tie guard's verdict (margin.py, live part):
+    ``near_tie`` is True when a detector decision lies within the over-noise error bound of its
+    threshold (a meteor boundary may then differ from the scipy reference; otherwise none can),
+    ``min_margin`` = min |db2 - thr| over the decisions, ``decision_bound`` the bound."""
+    near_tie: bool = False
+    min_margin: float = float("inf")
+    decision_bound: float = 0.0
 
 
 # ------------------------------------------------------------------ configuration
@@ -190,6 +200,30 @@ def live_detect(band_db: np.ndarray, fs, config_detection: ConfigDetection, devi
     return mets, thr, over
 
 
+def _first_decision_block(nb: int, fs, cfg: ConfigDetection) -> int:
+    """the block at which Init ends (processor.py:452-455: block start >= the wait)"""
+    bs = int(cfg.proc_block_sec * fs)
+    for b in range(nb):
+        if (b * bs) / fs >= cfg.init_detection_wait_sec:
+            return b
+    return nb
+
+
+def near_tie_check(band_db: np.ndarray, thr: np.ndarray, over: np.ndarray, span: np.ndarray, fs,
+                   cfg: ConfigDetection, what: str = "", warn: bool = True):
+    """(near_tie, min_margin, bound) of one recording from the device's band dB rows, the
+    thresholds used and the over-noise values (live_detect), and each block's sample span
+    (margin.block_span); a NearTieWarning when near."""
+    c, win = welch_cfg(fs, cfg)
+    bands = [(int(c.band_lo[j]), int(c.band_hi[j])) for j in range(3)]
+    err = margin.live_over_error(band_db, block_size=int(c.block_size), nperseg=int(c.nperseg),
+                                 noverlap=int(c.noverlap), nfft=int(c.nfft), window=win, span=span, bands=bands,
+                                 scale=float(c.scale))
+    W = int(cfg.avg_win_sec / cfg.proc_block_sec)
+    return margin.live_decision_check(over, thr, err, k_std=cfg.threshold_std_factor, W=W,
+                                      first_block=_first_decision_block(len(over), fs, cfg), what=what, warn=warn)
+
+
 def wav_file_process(wav_file_path: str,
                      config_detection: ConfigDetection,
                      config_visualization: ConfigVisualization,
@@ -200,7 +234,9 @@ def wav_file_process(wav_file_path: str,
                      required_sample_rate=4000,
                      device: int = 0):
     """GPU drop-in for processor.py:14-543 (same arguments, asserts and printed results).
-    Returns the detected meteors (the reference returns None and only prints them)."""
+    Returns the detected meteors as a ``LiveMeteors`` list (the reference returns None and only
+    prints them) carrying the near-tie guard's verdict; a NearTieWarning when a decision lies
+    within the error bound of the scipy reference."""
     assert os.path.exists(wav_file_path), f"File not found: {wav_file_path}"
     if config_spec_export.output_dir != "":
         assert os.path.exists(config_spec_export.output_dir), \
@@ -234,7 +270,11 @@ def wav_file_process(wav_file_path: str,
     print("Process Loop")
     print("###############")
     bdb = welch_band_db(x, file_sample_rate, config_detection, sample_scale, device)
-    meteors, _, _ = live_detect(bdb, file_sample_rate, config_detection, device)
+    found, thr, over = live_detect(bdb, file_sample_rate, config_detection, device)
+    meteors = LiveMeteors(found)
+    span = margin.block_span(x, block_size, sample_scale)[: bdb.shape[1]]
+    meteors.near_tie, meteors.min_margin, meteors.decision_bound = near_tie_check(
+        bdb, thr, over, span, file_sample_rate, config_detection, what=f"{wav_file_path}: ")
     for i, m in enumerate(meteors):
         print("Detected Meteor:", m, "Now Detected Meteors:", i + 1)
     not_exported = list(meteors)
@@ -386,11 +426,18 @@ class LiveBatch:
         self.d_met = ctx.alloc(F * self.cap * _lib.METEOR_DTYPE.itemsize)
         self.d_counts = ctx.alloc(F * 8)
         self.d_status = ctx.alloc(F * 4)
+        self.cfg = cfg
+        self.sample_scale = float(sample_scale)
+        self.span = np.zeros((F, self.nb))  # per-block sample span, for the near-tie guard
+        self.near_tie = np.zeros(F, bool)
+        self.min_margins = np.full(F, np.inf)
+        self.decision_bounds = np.zeros(F)
 
     def upload_file(self, i: int, x: np.ndarray):
         x = np.ascontiguousarray(x, dtype=self.dtype)
         if x.shape != (self.n,):
             raise ValueError("file length differs from the batch's")
+        self.span[i] = margin.block_span(x, int(self.lcfg.block_size), self.sample_scale)[: self.nb]
         self.d_x.upload(x, byte_offset=i * self.n_pad * self.dtype.itemsize)
 
     def run(self):
@@ -416,6 +463,26 @@ class LiveBatch:
         out = np.empty((self.nfiles, self.ld), np.float64)
         self.d_thr.download(out)
         return out[:, : self.nb]
+
+    def over_noise(self) -> np.ndarray:
+        out = np.empty((self.nfiles, self.ld), np.float64)
+        self.d_over.download(out)
+        return out[:, : self.nb]
+
+    def check_near_ties(self, warn: bool = True) -> np.ndarray:
+        """The near-tie guard per recording (``near_tie_check``): sets ``near_tie``,
+        ``min_margins`` and ``decision_bounds``; one NearTieWarning naming the flagged files."""
+        bdb, thr, over = self.band_db(), self.thresholds(), self.over_noise()
+        for i in range(self.nfiles):
+            self.near_tie[i], self.min_margins[i], self.decision_bounds[i] = near_tie_check(
+                bdb[i], thr[i], over[i], self.span[i], self.fs, self.cfg, warn=False)
+        if warn and self.near_tie.any():
+            import warnings
+            idx = np.nonzero(self.near_tie)[0]
+            warnings.warn(margin.NearTieWarning(
+                f"{idx.size} file(s) {idx.tolist()[:10]} have a decision within the over-noise error bound of "
+                f"their threshold: a meteor boundary may differ from the scipy reference"), stacklevel=2)
+        return self.near_tie
 
 
 def welch_psd(x, fs, nperseg=256, noverlap=None, nfft=None, sample_scale: float = 1.0, device: int = 0):

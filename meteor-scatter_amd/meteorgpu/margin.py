@@ -28,6 +28,25 @@ The bound (standard floating-point error model, u = 2^-53):
 
 ``tests/test_near_tie.py`` checks the per-block bound against numpy on random and adversarial
 blocks and the flag on a constructed near-tie stream.
+
+The live detector (processor.py:206, :349-412) gets the same guard (``live_*`` below): its band
+powers are scipy's Welch PSD (pocketfft over each detrended, windowed segment zero-padded to
+nfft; segments averaged) against the device's float64 Goertzel over the segment
+(csrc/live.hip welch_bands_kernel, one lane per bin over all nperseg samples).  The detrended
+and windowed samples are bit-identical on both sides (numpy's pairwise mean is reproduced), so
+only the transform differs:
+
+* per segment and bin |dX| <= (c_fft + c_goertzel) u S, S = sum |w (x - mean)| <= span sum w with
+  span = max x - min x over the block (a constant block is exactly 0 on both sides),
+  c_fft = 4 log2(nfft) + 8, c_goertzel = 3 nperseg G + 24;
+* a band energy E = scale / nseg * sum_s sum_k c_k |X_sk|^2 (c_k = 2 off DC / Nyquist) moves by
+  at most dE = 2 dX sqrt(C scale E) + C scale dX^2 + (n + nseg + 10) u E, C = 2n (Cauchy-Schwarz
+  over the n bins and nseg segments);
+* the over-noise value sig_dB - mean(noise1_dB, noise2_dB) (processor.py:391) by
+  e_sig + (e_n1 + e_n2) / 2 plus its own rounding;
+* the history threshold mean + k std of the previous W values (:397-402), held while tracking or
+  locked (:404-410), by (1 + k) max e plus rounding, so a decision (``db2 > thr`` :464,
+  ``db2 < thr`` :478) can only flip where |db2 - thr| <= (2 + k) max e.
 """
 from __future__ import annotations
 
@@ -44,14 +63,20 @@ class NearTieWarning(UserWarning):
     """A detection decision lies within the delta error bound of its threshold."""
 
 
-def _chain(nfft: int, L: int, bins: np.ndarray) -> float:
-    """c: longest rounding chain of a bin (pocketfft + the device's Goertzel segments)."""
-    l_seg = max(1, -(-int(L) // 16))  # samples per lane: the block_delta kernel's 16 lanes
+def _goertzel_chain(l_seg: int, bins, nfft: int) -> float:
+    """3 L G + 24: a Goertzel recurrence over l_seg samples at the bins' angles (G = the error
+    gain min(1/|sin theta|, l_seg)), its rotation and the lane sums."""
     theta = 2.0 * np.pi * np.asarray(bins, dtype=np.float64) / float(nfft)
     s = np.abs(np.sin(theta))
     gain = np.minimum(np.where(s > 0, 1.0 / np.maximum(s, 1e-300), np.inf), float(l_seg))
     g = float(gain.max()) if gain.size else 1.0
-    return 4.0 * math.log2(nfft) + 8.0 + 3.0 * l_seg * g + 24.0
+    return 3.0 * l_seg * g + 24.0
+
+
+def _chain(nfft: int, L: int, bins: np.ndarray) -> float:
+    """c: longest rounding chain of a bin (pocketfft + the device's Goertzel segments)."""
+    l_seg = max(1, -(-int(L) // 16))  # samples per lane: the block_delta kernel's 16 lanes
+    return 4.0 * math.log2(nfft) + 8.0 + _goertzel_chain(l_seg, bins, nfft)
 
 
 def band_db_error(e_db: np.ndarray, nbins: int, dx: float) -> np.ndarray:
@@ -92,3 +117,73 @@ def check(min_margin: float, bound: float, what: str = "") -> bool:
                                      f"bound {bound:.3e} dB: a detection boundary may differ from the "
                                      f"float64 numpy reference"), stacklevel=3)
     return near
+
+
+# ------------------------------------------------------------------ live detector (module doc)
+def welch_band_db_error(e_db: np.ndarray, nbins: int, dx, scale: float, nseg: int) -> np.ndarray:
+    """Per-block bound on |10 log10 E_gpu - 10 log10 E_scipy| for a Welch band energy of nbins
+    bins averaged over nseg segments (dx: the per-segment, per-bin transform bound, per block)."""
+    e_db = np.asarray(e_db, dtype=np.float64)
+    dx = np.broadcast_to(np.asarray(dx, dtype=np.float64), e_db.shape)
+    if nbins <= 0:
+        return np.zeros_like(e_db)
+    e = np.power(10.0, e_db / 10.0)
+    c = 2.0 * nbins
+    de = 2.0 * dx * np.sqrt(c * scale * e) + c * scale * dx * dx + (nbins + nseg + 10) * U * e
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        r = de / e
+        out = np.where(r < 1.0, DB * r / (1.0 - r) + 4.0 * U * (np.abs(e_db) + 1.0), np.inf)
+    # a band with no power at all: exactly 0 on both sides when the samples are (dx == 0)
+    return np.where(e > 0, out, np.where(dx == 0, 0.0, np.inf))
+
+
+def block_span(x: np.ndarray, block_size: int, sample_scale: float = 1.0) -> np.ndarray:
+    """max - min of each whole processing block's samples, times the sample scale."""
+    x = np.asarray(x)
+    nb = len(x) // block_size if block_size > 0 else 0
+    if nb == 0:
+        return np.zeros(0)
+    v = x[: nb * block_size].reshape(nb, block_size)
+    return (v.max(axis=1).astype(np.float64) - v.min(axis=1).astype(np.float64)) * abs(float(sample_scale))
+
+
+def live_over_error(band_db: np.ndarray, *, block_size: int, nperseg: int, noverlap: int, nfft: int,
+                    window: np.ndarray, span, bands, scale: float) -> np.ndarray:
+    """Per-block bound on |db2_gpu - db2_scipy| (processor.py:391) from the device's band dB rows
+    band_db [3][nb] (signal, noise 1, noise 2); ``bands``: their inclusive bin ranges, ``span``:
+    max - min of each block's (scaled) samples (``block_span``), ``window``: the nperseg window."""
+    band_db = np.asarray(band_db, dtype=np.float64)
+    step = nperseg - noverlap
+    nseg = (block_size - nperseg) // step + 1
+    s = np.asarray(span, dtype=np.float64) * float(np.abs(np.asarray(window, dtype=np.float64)).sum())
+    bins = np.concatenate([np.arange(lo, hi + 1) for lo, hi in bands]) if bands else np.zeros(0)
+    chain = 4.0 * math.log2(nfft) + 8.0 + _goertzel_chain(nperseg, bins, nfft)
+    dx = chain * U * s
+    e = [welch_band_db_error(band_db[j], max(0, hi - lo + 1), dx, scale, nseg) for j, (lo, hi) in enumerate(bands)]
+    with np.errstate(invalid="ignore"):
+        rnd = 4.0 * U * (np.abs(band_db[0]) + np.abs(band_db[1]) + np.abs(band_db[2]))
+        out = e[0] + 0.5 * (e[1] + e[2]) + np.where(np.isfinite(rnd), rnd, 0.0)
+    return out
+
+
+def live_decision_check(over: np.ndarray, thr: np.ndarray, over_err: np.ndarray, *, k_std: float, W: int,
+                        first_block: int, what: str = "", warn: bool = True):
+    """(near_tie, min_margin, bound) of one recording: the decisions are the blocks from
+    ``first_block`` on (the first that can leave Init); min |db2 - thr| over those with finite
+    values against (2 + k) max e plus the threshold's own rounding (W-element mean / std)."""
+    over = np.asarray(over, dtype=np.float64)
+    thr = np.asarray(thr, dtype=np.float64)
+    sel = slice(max(0, int(first_block)), None)
+    o, t = over[sel], thr[sel]
+    ok = np.isfinite(o) & np.isfinite(t)
+    m = float(np.min(np.abs(o[ok] - t[ok]))) if ok.any() else math.inf
+    fin = over[np.isfinite(over)]
+    big = float(np.max(np.abs(fin))) if fin.size else 0.0
+    emax = float(np.max(over_err)) if np.size(over_err) else 0.0
+    bound = (2.0 + abs(float(k_std))) * emax * (1.0 + 1e-6) + 8.0 * (W + 8) * U * big
+    near = bool(np.isfinite(m)) and m <= bound
+    if near and warn:
+        warnings.warn(NearTieWarning(f"{what}decision margin {m:.3e} dB is within the over-noise error bound "
+                                     f"{bound:.3e} dB: a meteor boundary may differ from the scipy reference"),
+                      stacklevel=3)
+    return near, m, bound

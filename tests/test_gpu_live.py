@@ -115,6 +115,8 @@ def test_wav_file_process_end_to_end(live, tmp_path):
                                 live.ConfigSpecExport(output_dir=""))
     ref, _, _ = L.wav_file_process_ref(x.astype(np.float64) / 32768.0, 4000, _ref_cfg(cfg))
     assert len(ref) > 0 and len(got) == len(ref)
+    # the near-tie guard (margin.py, live part): no decision within the bound, which is tiny
+    assert not got.near_tie and 0 < got.decision_bound < 1e-6 and got.min_margin > got.decision_bound
     for a, b in zip(got, ref):
         assert (a.time_start, a.time_stop, a.duration) == (b.time_start, b.time_stop, b.duration)
         for f in ("db_min", "db_max", "db_mean", "db_std"):
@@ -153,6 +155,43 @@ def test_live_batch_matches_single(live):
         assert [(r["time_start"], r["time_stop"], r["db_mean"]) for r in rows[i]] == \
                [(a.time_start, a.time_stop, a.db_mean) for a in m]
     assert counts.sum() > 0
+    import warnings
+    from meteorgpu import margin as M
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", M.NearTieWarning)
+        assert not lb.check_near_ties().any()
+    assert (lb.decision_bounds > 0).all() and (lb.decision_bounds < 1e-6).all()
+    assert (lb.min_margins > lb.decision_bounds).all()
+    lb.span[1] = np.inf  # a bound too wide to separate anything: that file is flagged
+    with pytest.warns(M.NearTieWarning, match="1 file"):
+        lb.check_near_ties()
+    assert lb.near_tie.tolist() == [False, True, False, False, False]
+
+
+@pytest.mark.parametrize("fs,bs,nfft,f0", [(4000, 0.2, 4096, 1000), (8000, 0.1, 1024, 1500),
+                                           (4000, 0.05, 512, 1000), (4000, 0.5, 4096, 1020)])
+def test_over_noise_within_bound(live, fs, bs, nfft, f0):
+    """the device's over-noise values (processor.py:391) against scipy's within the per-block
+    bound of margin.live_over_error, on a stream with a DC-offset stretch and digital silence"""
+    from meteorgpu import margin as M, synth
+    x, _ = synth.synth_real(seed=int(fs * bs) + nfft + 5, fs=fs, duration_s=20.0, f0=f0, sigma=300, rate_per_min=20)
+    x[: 3 * fs] = np.clip(x[: 3 * fs].astype(np.int32) + 20000, -32768, 32767)
+    x[5 * fs: 7 * fs] = 0
+    cfg = live.ConfigDetection(proc_block_sec=bs, n_fft=nfft, signal_freq=f0)
+    bdb = live.welch_band_db(x, fs, cfg, sample_scale=1 / 32768)
+    _, thr, over = live.live_detect(bdb, fs, cfg)
+    ref = L.welch_band_db_ref(x.astype(np.float64) / 32768.0, fs, _ref_cfg(cfg))
+    _, _, rover = L.live_detect_ref(ref, fs, int(bs * fs), _ref_cfg(cfg))
+    c, win = live.welch_cfg(fs, cfg)
+    span = M.block_span(x, int(c.block_size), 1 / 32768)[: bdb.shape[1]]
+    err = M.live_over_error(bdb, block_size=int(c.block_size), nperseg=int(c.nperseg), noverlap=int(c.noverlap),
+                            nfft=int(c.nfft), window=win, span=span,
+                            bands=[(int(c.band_lo[j]), int(c.band_hi[j])) for j in range(3)], scale=float(c.scale))
+    fin = np.isfinite(rover)
+    assert np.array_equal(np.isfinite(over), fin) and (~fin).any()  # the silent blocks: NaN on both sides
+    d = np.abs(over[fin] - rover[fin])
+    assert (d <= err[fin]).all() and d.max() > 0, float(np.max(d / err[fin]))
+    assert err[fin].max() < 1e-6  # not vacuous
 
 
 def test_state_machine_long_rows_cross_chunks(live):

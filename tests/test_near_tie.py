@@ -106,3 +106,66 @@ def test_proc_result_and_batch_flags():
     with pytest.warns(M.NearTieWarning, match="1 file"):
         bp.detections()
     assert bp.near_tie.tolist() == [False, True, False]
+
+
+# ------------------------------------------------------------------ live detector (margin.py, live part)
+def test_welch_pocketfft_within_bin_bound():
+    """scipy.signal.welch's segment transform (detrend, periodic Hann, rfft zero-padded to nfft)
+    against an exact long-double DFT at the live bands' bins: within c_fft u S, S <= span sum w"""
+    from scipy.signal import get_window
+    rng = np.random.default_rng(21)
+    nperseg, nfft = 256, 4096
+    w = get_window("hann", nperseg)
+    bins = np.r_[972:1075, 665:768, 1279:1382]  # 1000 Hz +- 50 and the two noise bands at fs 4 kHz
+    for offset, scale in ((0.0, 0.3), (0.9, 0.05), (-0.5, 1e-4)):
+        x = np.clip(offset + scale * rng.standard_normal(nperseg), -1, 1)
+        d = x - np.mean(x)
+        X = np.fft.rfft(w * d, n=nfft)
+        exact = _exact_bins(w * d, nfft, bins)
+        S = float(x.max() - x.min()) * float(w.sum())
+        bound = (4.0 * np.log2(nfft) + 8.0) * M.U * S
+        err = np.abs(X[bins].astype(np.clongdouble) - exact).astype(np.float64)
+        assert (err <= bound).all() and err.max() > 0
+
+
+def test_welch_band_db_error_edges():
+    e = np.array([-np.inf, -120.0, -20.0])
+    b = M.welch_band_db_error(e, 103, np.array([0.0, 1e-14, 1e-14]), 2.6e-6, 5)
+    assert b[0] == 0.0 and np.isfinite(b[1]) and b[2] < b[1]  # silence: exact on both sides
+    assert np.isinf(M.welch_band_db_error(np.array([-np.inf]), 103, 1e-14, 2.6e-6, 5))[0]
+    assert (M.welch_band_db_error(e, 0, 1.0, 2.6e-6, 5) == 0).all()
+
+
+def test_live_flag_on_constructed_near_tie():
+    """a block in the Detection state placed one ulp above its history threshold (processor.py
+    :397-402, :464) is a near tie for the live guard; the unmodified rows are not"""
+    from meteorgpu import live as LV
+    from oracle import live_oracle as L
+    rng = np.random.default_rng(5)
+    nb = 900
+    rows = np.stack([rng.normal(-30, 1, nb), rng.normal(-40, 0.5, nb), rng.normal(-40, 0.5, nb)])
+    cfg = LV.ConfigDetection()
+    rcfg = L.ConfigDetectionRef()
+    span = np.full(nb, 0.1)
+
+    def check(r):
+        _, thr, over = L.live_detect_ref(r, 4000, 800, rcfg)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", M.NearTieWarning)
+            return LV.near_tie_check(r, thr, over, span, 4000, cfg), thr, over
+
+    (near, m, bound), thr, over = check(rows)
+    assert not near and 0 < bound < 1e-8 and m > bound
+    i = 600
+    assert np.isfinite(thr[i]) and over[i] < thr[i]
+    mean_n = np.mean([rows[1, i], rows[2, i]])
+    s = thr[i] + mean_n
+    while s - mean_n <= thr[i]:
+        s = np.nextafter(s, np.inf)
+    r2 = rows.copy()
+    r2[0, i] = s  # db2 = sig - mean(n1, n2) a few ulp above the threshold: a trigger
+    (near2, m2, bound2), thr2, over2 = check(r2)
+    assert thr2[i] == thr[i] and over2[i] > thr2[i] and near2 and m2 <= bound2
+    with pytest.warns(M.NearTieWarning):
+        _, thr3, over3 = L.live_detect_ref(r2, 4000, 800, rcfg)
+        LV.near_tie_check(r2, thr3, over3, span, 4000, cfg)

@@ -18,7 +18,6 @@
 //   hipcc --offload-arch=gfx950 -O3 coissue_xpose.hip -o coissue_xpose
 #include <hip/hip_runtime.h>
 #include <cstdio>
-#include <map>
 #include <algorithm>
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -117,8 +116,9 @@ __global__ __launch_bounds__(1024) void k_xpose(long long *cyc, float *out, int 
     if (r == 1234.5f) out[threadIdx.x] = r;
 }
 
-// (b) NM MFMA + NV FMAs per iteration
-template <int NM, int NV>
+// (b) NM MFMA + NV FMAs per iteration; IL: pin the interleave (1 MFMA, NV/NM FMAs, ...) in the
+// instruction stream with sched_group_barrier (otherwise hipcc groups the MFMAs after the FMAs)
+template <int NM, int NV, bool IL = false>
 __global__ __launch_bounds__(1024) void k_coissue(long long *cyc, float *out, int iters, float a, float b) {
     const int lane = threadIdx.x & 63;
     float v[16];
@@ -136,6 +136,10 @@ __global__ __launch_bounds__(1024) void k_coissue(long long *cyc, float *out, in
             for (int m = 0; m < NM; ++m) {
                 acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(ma, mb, acc[m & 3], 0, 0, 0);
                 valu_block<NV / (NM > 0 ? NM : 1)>(v, a, b);
+                if (IL) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, NV / (NM > 0 ? NM : 1), 0);
+                }
             }
         }
     }
@@ -152,23 +156,18 @@ __global__ __launch_bounds__(1024) void k_coissue(long long *cyc, float *out, in
 
 static double run(void (*kern)(long long *, float *, int, float, float), long long *cyc, float *out, int cus,
                   int iters) {
+    // per workgroup t1 - t0 (all workgroups run at once, one per CU), averaged; best of 3
     static long long h[3 * 4096];
     double best = 1e30;
     for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(kern, dim3(cus), dim3(1024), 0, 0, cyc, out, iters, 1.0001f, 0.5f);
         (void)hipDeviceSynchronize();
         (void)hipMemcpy(h, cyc, sizeof(long long) * 3 * cus, hipMemcpyDeviceToHost);
-        std::map<long long, std::pair<long long, long long>> span;
-        for (int i = 0; i < cus; ++i) {
-            auto it = span.find(h[3 * i + 2]);
-            if (it == span.end()) span[h[3 * i + 2]] = {h[3 * i], h[3 * i + 1]};
-            else it->second = {std::min(it->second.first, h[3 * i]), std::max(it->second.second, h[3 * i + 1])};
-        }
         double m = 0;
-        for (auto &kv : span) m += kv.second.second - kv.second.first;
-        best = std::min(best, m / span.size());
+        for (int i = 0; i < cus; ++i) m += (double)(h[3 * i + 1] - h[3 * i]);
+        best = std::min(best, m / cus);
     }
-    return best / iters / 4.0;  // per iteration per SIMD (4 waves each)
+    return best / iters / 4.0;  // per iteration per wave (4 waves per SIMD share it)
 }
 
 int main() {
@@ -195,8 +194,9 @@ int main() {
     {                                                                                                       \
         const double m = run(k_coissue<NM, 0>, cyc, out, cus, it), v = run(k_coissue<0, NV>, cyc, out, cus, it); \
         const double mv = run(k_coissue<NM, NV>, cyc, out, cus, it);                                       \
-        printf("NM=%3d NV=%4d  mfma alone %7.1f  valu alone %7.1f  both %7.1f  (max %7.1f, sum %7.1f)\n", NM, NV, \
-               m, v, mv, std::max(m, v), m + v);                                                            \
+        const double il = run(k_coissue<NM, NV, true>, cyc, out, cus, it);                                 \
+        printf("NM=%3d NV=%4d  mfma alone %7.1f  valu alone %7.1f  both %7.1f  interleaved %7.1f  (max %7.1f, sum %7.1f)\n", \
+               NM, NV, m, v, mv, il, std::max(m, v), m + v);                                                \
     }
     CO(16, 64) CO(16, 128) CO(16, 256) CO(32, 256) CO(32, 512) CO(64, 512)
     (void)hipFree(cyc);
