@@ -382,8 +382,9 @@ def run_c5(a, ctx, job, rank, world):
         "detections_per_step": int(len(res.detections)),
         "state_rounds": int(res.rounds),
         "exact_threshold_frames": int(res.refined),
-        # every step certifies each decision against the float64 reference and recomputes in float64
-        # the delta the uncertain ones depend on (meteorgpu.iq.IQShardDetector.detect)
+        # the headline's decision mode: off = the reference's arithmetic path uncertified; flag = every
+        # decision checked against its float64 error bounds; exact = the uncertain ones recomputed in
+        # float64 (meteorgpu.iq.IQShardDetector.detect).  "certification" times flag and exact.
         "decisions": head_mode,
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),

@@ -176,8 +176,8 @@ void msd_destroy(msd_ctx *ctx) {
         hipEventDestroy(p.b);
     }
     for (auto e : ctx->pool) hipEventDestroy(e);
-    for (int i = 0; i < 4; ++i)
-        if (ctx->scratch[i]) hipFree(ctx->scratch[i]);
+    for (void *p : ctx->scratch)
+        if (p) hipFree(p);
     if (ctx->copy_stream) {
         hipStreamSynchronize(ctx->copy_stream);
         hipStreamDestroy(ctx->copy_stream);

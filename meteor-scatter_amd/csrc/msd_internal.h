@@ -50,8 +50,9 @@ struct msd_ctx {
     double total_ms[msd::K_COUNT] = {};
     int64_t launches[msd::K_COUNT] = {};
     // scratch device buffers for the host-pointer convenience entry points
-    void *scratch[4] = {nullptr, nullptr, nullptr, nullptr};
-    size_t scratch_bytes[4] = {0, 0, 0, 0};
+    // (slot 4: msd_iq_delta64_dev's block table, rotations and ranges)
+    void *scratch[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t scratch_bytes[5] = {0, 0, 0, 0, 0};
 };
 
 struct msd_stft_plan {

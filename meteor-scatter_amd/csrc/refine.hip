@@ -83,11 +83,14 @@ __device__ __forceinline__ double row_sum_d(double v) {
 }
 
 template <typename T>
-struct Quad;  // four consecutive complex samples per load
+struct Quad;  // four consecutive complex samples per load: raw() fetches, cvt() widens
 template <>
 struct Quad<int16_t> {
-    __device__ static void load(const int16_t *x, int64_t i, double2 (&z)[4]) {
-        const uint4 r = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(x) + i);
+    using Raw = uint4;
+    __device__ static Raw raw(const int16_t *x, int64_t i) {
+        return *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(x) + i);
+    }
+    __device__ static void cvt(const Raw &r, double2 (&z)[4]) {
         const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = make_double2((double)(int16_t)(w[e] & 0xffffu), (double)(int16_t)(w[e] >> 16));
@@ -95,20 +98,26 @@ struct Quad<int16_t> {
 };
 template <>
 struct Quad<float> {
-    __device__ static void load(const float *x, int64_t i, double2 (&z)[4]) {
-        const float4 a = *reinterpret_cast<const float4 *>(x + 2 * i);
-        const float4 b = *reinterpret_cast<const float4 *>(x + 2 * i + 4);
-        z[0] = make_double2(a.x, a.y);
-        z[1] = make_double2(a.z, a.w);
-        z[2] = make_double2(b.x, b.y);
-        z[3] = make_double2(b.z, b.w);
+    struct Raw {
+        float4 a, b;
+    };
+    __device__ static Raw raw(const float *x, int64_t i) {
+        return Raw{*reinterpret_cast<const float4 *>(x + 2 * i), *reinterpret_cast<const float4 *>(x + 2 * i + 4)};
+    }
+    __device__ static void cvt(const Raw &r, double2 (&z)[4]) {
+        z[0] = make_double2(r.a.x, r.a.y);
+        z[1] = make_double2(r.a.z, r.a.w);
+        z[2] = make_double2(r.b.x, r.b.y);
+        z[3] = make_double2(r.b.z, r.b.w);
     }
 };
 
 // D >= 64: sixteen lanes per block (a row of the wave), lane L the D/16 consecutive samples from
-// L D/16; one pass over the samples runs the Goertzel recurrence of every needed bin (up to NK),
-// each segment's DFT is rotated to the block origin with two table twiddles, and the row sums the
-// 16 partials.  out[g]: [nk] B values, then the block's sample sum and sum of |re| + |im| (.x).
+// L D/16; one pass over the samples runs the Goertzel recurrence of NK bins (the nk needed ones,
+// padded with copies of bin 0 whose results are dropped: no per-bin branch in the loop), each
+// segment's DFT is rotated to the block origin with two table twiddles, and the row sums the 16
+// partials.  The next four samples are loaded before the current four are used.  out[g]: [nk] B
+// values, then the block's sample sum and sum of |re| + |im| (.x).
 template <typename T, int NK>
 __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, RefineGeom G, RefineBins K,
                                                     const int64_t *__restrict__ bstart, const int64_t *__restrict__ bcs,
@@ -121,14 +130,13 @@ __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, Ref
     const int r = find_range(bcs, G.nr, g);
     const int64_t m = bstart[r] + (g - bcs[r]);
     const int S = G.D / 16;  // samples per lane (a multiple of 4)
-    const int64_t n0 = (int64_t)l16 * S;
+    const int n0 = l16 * S;
     const int64_t base = m * (int64_t)G.D + n0;
     double c2[NK];
     double2 s1[NK], s2[NK];
 #pragma unroll
     for (int b = 0; b < NK; ++b) {
-        const int km = b < K.nk ? ((K.k[b] % G.N) + G.N) % G.N : 0;
-        c2[b] = 2.0 * W[km].x;  // 2 cos(theta)
+        c2[b] = 2.0 * W[K.km[b < K.nk ? b : 0]].x;  // 2 cos(theta)
         s1[b] = make_double2(0.0, 0.0);
         s2[b] = make_double2(0.0, 0.0);
     }
@@ -136,9 +144,11 @@ __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, Ref
     double l1 = 0.0;
     // the recurrence s_n = z_n + 2 cos(theta) s_{n-1} - s_{n-2}, two samples per step with the roles
     // of s1 / s2 alternating (no register moves): s2 <- fma(c2, s1, z0 - s2), s1 <- fma(c2, s2, z1 - s1)
+    typename Quad<T>::Raw rn = Quad<T>::raw(x, base);
     for (int q = 0; q < S; q += 4) {
         double2 z[4];
-        Quad<T>::load(x, base + q, z);
+        Quad<T>::cvt(rn, z);
+        if (q + 4 < S) rn = Quad<T>::raw(x, base + q + 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             sum = cadd(sum, z[e]);
@@ -148,11 +158,9 @@ __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, Ref
         for (int e = 0; e < 4; e += 2) {
 #pragma unroll
             for (int b = 0; b < NK; ++b) {
-                if (b < K.nk) {
-                    s2[b] = make_double2(fma(c2[b], s1[b].x, z[e].x - s2[b].x), fma(c2[b], s1[b].y, z[e].y - s2[b].y));
-                    s1[b] = make_double2(fma(c2[b], s2[b].x, z[e + 1].x - s1[b].x),
-                                         fma(c2[b], s2[b].y, z[e + 1].y - s1[b].y));
-                }
+                s2[b] = make_double2(fma(c2[b], s1[b].x, z[e].x - s2[b].x), fma(c2[b], s1[b].y, z[e].y - s2[b].y));
+                s1[b] = make_double2(fma(c2[b], s2[b].x, z[e + 1].x - s1[b].x),
+                                     fma(c2[b], s2[b].y, z[e + 1].y - s1[b].y));
             }
         }
     }
@@ -160,13 +168,13 @@ __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, Ref
 #pragma unroll
     for (int b = 0; b < NK; ++b) {
         if (b >= K.nk) continue;
-        const int km = ((K.k[b] % G.N) + G.N) % G.N;
+        const int km = K.km[b];
         double2 c;
         if (km == 0) {
             c = sum;
         } else {  // sum_q z[n0 + q] W^{k (n0 + q)} = W^{k (n0 + S - 1)} s_{S-1} - W^{k (n0 + S)} s_{S-2}
-            const double2 t1 = W[(int)(((int64_t)km * (n0 + S - 1)) % G.N)];
-            const double2 t2 = W[(int)(((int64_t)km * (n0 + S)) % G.N)];
+            const double2 t1 = W[(int)(((uint32_t)km * (uint32_t)(n0 + S - 1)) % (uint32_t)G.N)];
+            const double2 t2 = W[(int)(((uint32_t)km * (uint32_t)(n0 + S)) % (uint32_t)G.N)];
             c = csub(cmul(t1, s1[b]), cmul(t2, s2[b]));
         }
         c = make_double2(row_sum_d(c.x), row_sum_d(c.y));
@@ -199,13 +207,14 @@ __global__ __launch_bounds__(256) void block_small_kernel(const T *__restrict__ 
     }
     double2 *o = out + g * (K.nk + 2);
     for (int b = 0; b < K.nk; ++b) {
-        const int km = ((K.k[b] % G.N) + G.N) % G.N;
+        const int km = K.km[b];
         if (km == 0) {
             o[b] = sum;
             continue;
         }
         double2 acc = make_double2(0.0, 0.0);
-        for (int q = 0; q < G.D; ++q) acc = cadd(acc, cmul(Samp<T>::at(x, base + q), W[(int)(((int64_t)km * q) % G.N)]));
+        for (int q = 0; q < G.D; ++q)
+            acc = cadd(acc, cmul(Samp<T>::at(x, base + q), W[(int)(((uint32_t)km * (uint32_t)q) % (uint32_t)G.N)]));
         o[b] = acc;
     }
     o[K.nk] = sum;
@@ -223,12 +232,12 @@ __device__ __forceinline__ double band_db_bound64(double E, int n, double d) {
     return 4.342944819032518 * dE / den * (1.0 + 1e-9);
 }
 
-// one thread per frame: combine the R blocks, the Hann taps, |Y|^2 * scale, the band sums in
-// np.sum order, 10 log10(E + 1e-12); delta and its bound
+// one thread per frame: combine the R blocks (rot[b][j] = W^{k_b j D}, host table, uniform reads),
+// the Hann taps, |Y|^2 * scale, the band sums in np.sum order, 10 log10(E + 1e-12); delta and its bound
 __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, const int64_t *__restrict__ fstart,
                                                     const int64_t *__restrict__ fcs, const int64_t *__restrict__ bstart,
                                                     const int64_t *__restrict__ bcs, int64_t nframes,
-                                                    const double2 *__restrict__ W, const double2 *__restrict__ blk,
+                                                    const double2 *__restrict__ rot, const double2 *__restrict__ blk,
                                                     double *__restrict__ delta, double *__restrict__ ed) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
@@ -246,10 +255,10 @@ __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, 
     const double2 mean = make_double2(sum.x / G.N, sum.y / G.N);
     // V[k'] of the detrended frame at needed bin b
     auto V = [&](int b) {
-        const int km = ((K.k[b] % G.N) + G.N) % G.N;
+        const double2 *rb = rot + b * G.R;
         double2 z = b0[b];
-        for (int j = 1; j < G.R; ++j) z = cadd(z, cmul(W[(int)(((int64_t)km * j * G.D) % G.N)], b0[j * stride + b]));
-        if (km == 0) z = csub(z, make_double2(mean.x * G.N, mean.y * G.N));
+        for (int j = 1; j < G.R; ++j) z = cadd(z, cmul(rb[j], b0[j * stride + b]));
+        if (b == K.dc) z = csub(z, make_double2(mean.x * G.N, mean.y * G.N));
         return z;
     };
     auto energy = [&](const int (*idx)[3], int n) {
@@ -293,21 +302,26 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     RefineGeom &G = P.G;
     const std::vector<int64_t> &fstart = P.fstart, &fcs = P.fcs, &bstart = P.bstart, &bcs = P.bcs;
     const int64_t nblocks = P.nblocks, nframes = P.nframes;
-    std::vector<double2> W(N);
+    // host tables: W^m (m < N), then the per-bin block rotations rot[b][j] = W^{k_b j D} (j < R)
+    const int R = G.R;
+    std::vector<double2> tab((size_t)N + (size_t)K.nk * R);
     for (int m = 0; m < N; ++m) {
         const double a = -2.0 * M_PI * (double)m / (double)N;
-        W[m] = make_double2(std::cos(a), std::sin(a));
+        tab[m] = make_double2(std::cos(a), std::sin(a));
     }
+    for (int b = 0; b < K.nk; ++b)
+        for (int j = 0; j < R; ++j) tab[(size_t)N + (size_t)b * R + j] = tab[(size_t)G.D * (((int64_t)K.km[b] * j) % R)];
     DeviceGuard g(ctx->device);
     hipStream_t st = ctx->stream;
-    void *d = nullptr;
-    const size_t nb_blk = sizeof(double2) * (size_t)nblocks * (K.nk + 2);
+    const size_t nb_blk = (sizeof(double2) * (size_t)nblocks * (K.nk + 2) + 255) / 256 * 256;
+    const size_t nb_tab = (sizeof(double2) * tab.size() + 255) / 256 * 256;
     const size_t nb_meta = sizeof(int64_t) * (4 * (size_t)nranges + 2);
-    const size_t nb_w = sizeof(double2) * N;
-    MSD_HIP(hipMalloc(&d, nb_blk + nb_meta + nb_w + 256));
+    void *d = nullptr;
+    if (int rc = ctx_scratch(ctx, 4, nb_blk + nb_tab + nb_meta, &d)) return rc;  // grown once, kept
     auto *blk = static_cast<double2 *>(d);
     auto *Wd = reinterpret_cast<double2 *>(static_cast<char *>(d) + nb_blk);
-    auto *meta = reinterpret_cast<int64_t *>(static_cast<char *>(d) + nb_blk + nb_w);
+    const double2 *rot = Wd + N;
+    auto *meta = reinterpret_cast<int64_t *>(static_cast<char *>(d) + nb_blk + nb_tab);
     std::vector<int64_t> hm;
     hm.insert(hm.end(), fstart.begin(), fstart.end());
     hm.insert(hm.end(), fcs.begin(), fcs.end());
@@ -315,7 +329,7 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     hm.insert(hm.end(), bcs.begin(), bcs.end());
     const int64_t *d_fstart = meta, *d_fcs = meta + nranges, *d_bstart = meta + 2 * nranges + 1,
                   *d_bcs = meta + 3 * nranges + 1;
-    hipError_t e = hipMemcpyAsync(Wd, W.data(), nb_w, hipMemcpyHostToDevice, st);
+    hipError_t e = hipMemcpyAsync(Wd, tab.data(), sizeof(double2) * tab.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(meta, hm.data(), sizeof(int64_t) * hm.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         KernelTimer timer(ctx, K_REFINE);
@@ -328,9 +342,13 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, xp, G, K, d_bstart, d_bcs, nblocks, Wd, blk);
             };
             auto by_nk = [&](const auto *xp) {  // register arrays sized to the bins (C5: 9)
-                if (K.nk <= 5) go(std::integral_constant<int, 5>{}, xp);
+                if (K.nk <= 3) go(std::integral_constant<int, 3>{}, xp);
+                else if (K.nk <= 5) go(std::integral_constant<int, 5>{}, xp);
+                else if (K.nk <= 7) go(std::integral_constant<int, 7>{}, xp);
                 else if (K.nk <= 9) go(std::integral_constant<int, 9>{}, xp);
                 else if (K.nk <= 12) go(std::integral_constant<int, 12>{}, xp);
+                else if (K.nk <= 16) go(std::integral_constant<int, 16>{}, xp);
+                else if (K.nk <= 24) go(std::integral_constant<int, 24>{}, xp);
                 else go(std::integral_constant<int, RF_MAXK>{}, xp);
             };
             if (dtype == MSD_CI16) by_nk(static_cast<const int16_t *>(x));
@@ -345,11 +363,11 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
                                    static_cast<const float *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
         }
         hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, G, K, d_fstart,
-                           d_fcs, d_bstart, d_bcs, nframes, Wd, blk, delta, ed);
+                           d_fcs, d_bstart, d_bcs, nframes, rot, blk, delta, ed);
         e = hipGetLastError();
     }
+    // the host tables are pageable: wait for the copies (and the kernels) before they go
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(d);
     if (e != hipSuccess) return hip_fail(e, "msd_iq_delta64_dev");
     return MSD_OK;
 }

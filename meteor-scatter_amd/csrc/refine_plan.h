@@ -19,6 +19,7 @@ constexpr int RF_MAXK = 32;  // needed bins (band and noise bins +- 1)
 struct RefineBins {
     int nk;                   // needed bins k' (signed, -N/2 <= k' < N/2 + 1, taken mod N)
     int k[RF_MAXK];
+    int km[RF_MAXK];          // k' mod N
     int nb, nn;               // band / noise bins, in np.sum order (ascending FFT index)
     int bidx[RF_MAXK / 2][3]; // per band bin: indices into k[] of k-1, k, k+1
     int nidx[RF_MAXK / 2][3];
@@ -90,6 +91,10 @@ inline int plan_refine(int nperseg, int64_t hop, double fs, int band_lo, int ban
     };
     if (!fill(band_lo, band_hi, K.bidx, K.nb) || !fill(noise_lo, noise_hi, K.nidx, K.nn))
         return err(E_UNSUPPORTED, "bands too wide for the refinement kernel");
+    for (int i = 0; i < K.nk; ++i) {
+        K.km[i] = ((K.k[i] % N) + N) % N;
+        if (K.km[i] == 0) K.dc = i;
+    }
     RefineGeom &G = P.G;
     G = RefineGeom{};
     G.N = N;
