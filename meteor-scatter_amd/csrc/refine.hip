@@ -116,8 +116,10 @@ struct Quad<float> {
 // L D/16; one pass over the samples runs the Goertzel recurrence of NK bins (the nk needed ones,
 // padded with copies of bin 0 whose results are dropped: no per-bin branch in the loop), each
 // segment's DFT is rotated to the block origin with two table twiddles, and the row sums the 16
-// partials.  The next four samples are loaded before the current four are used.  out[g]: [nk] B
-// values, then the block's sample sum and sum of |re| + |im| (.x).
+// partials.  The next four samples are loaded before the current four are used.  Output
+// bin-major (the frame kernel's neighbouring frames then read neighbouring addresses):
+// out[b * nblocks + g] = B_g[k_b] for b < nk, then the block's sample sum (b = nk) and its sum of
+// |re| + |im| (b = nk + 1, .x).
 template <typename T, int NK>
 __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, RefineGeom G, RefineBins K,
                                                     const int64_t *__restrict__ bstart, const int64_t *__restrict__ bcs,
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, Ref
             }
         }
     }
-    double2 *o = out + g * (K.nk + 2);
+    double2 *o = out + g;  // bin-major: value b of block g at out[b * nblocks + g]
 #pragma unroll
     for (int b = 0; b < NK; ++b) {
         if (b >= K.nk) continue;
@@ -178,12 +180,12 @@ __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, Ref
             c = csub(cmul(t1, s1[b]), cmul(t2, s2[b]));
         }
         c = make_double2(row_sum_d(c.x), row_sum_d(c.y));
-        if (live && l16 == 0) o[b] = c;
+        if (live && l16 == 0) o[b * nblocks] = c;
     }
     const double sx = row_sum_d(sum.x), sy = row_sum_d(sum.y), sl = row_sum_d(l1);
     if (live && l16 == 0) {
-        o[K.nk] = make_double2(sx, sy);
-        o[K.nk + 1] = make_double2(sl, 0.0);
+        o[K.nk * nblocks] = make_double2(sx, sy);
+        o[(K.nk + 1) * nblocks] = make_double2(sl, 0.0);
     }
 }
 
@@ -205,20 +207,20 @@ __global__ __launch_bounds__(256) void block_small_kernel(const T *__restrict__ 
         sum = cadd(sum, z);
         l1 += fabs(z.x) + fabs(z.y);
     }
-    double2 *o = out + g * (K.nk + 2);
+    double2 *o = out + g;  // bin-major, as block_kernel
     for (int b = 0; b < K.nk; ++b) {
         const int km = K.km[b];
         if (km == 0) {
-            o[b] = sum;
+            o[b * nblocks] = sum;
             continue;
         }
         double2 acc = make_double2(0.0, 0.0);
         for (int q = 0; q < G.D; ++q)
             acc = cadd(acc, cmul(Samp<T>::at(x, base + q), W[(int)(((uint32_t)km * (uint32_t)q) % (uint32_t)G.N)]));
-        o[b] = acc;
+        o[b * nblocks] = acc;
     }
-    o[K.nk] = sum;
-    o[K.nk + 1] = make_double2(l1, 0.0);
+    o[K.nk * nblocks] = sum;
+    o[(K.nk + 1) * nblocks] = make_double2(l1, 0.0);
 }
 
 // dB error of a band of n bins with energy E when every bin's amplitude is off by at most d
@@ -236,7 +238,7 @@ __device__ __forceinline__ double band_db_bound64(double E, int n, double d) {
 // the Hann taps, |Y|^2 * scale, the band sums in np.sum order, 10 log10(E + 1e-12); delta and its bound
 __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, const int64_t *__restrict__ fstart,
                                                     const int64_t *__restrict__ fcs, const int64_t *__restrict__ bstart,
-                                                    const int64_t *__restrict__ bcs, int64_t nframes,
+                                                    const int64_t *__restrict__ bcs, int64_t nframes, int64_t nblocks,
                                                     const double2 *__restrict__ rot, const double2 *__restrict__ blk,
                                                     double *__restrict__ delta, double *__restrict__ ed) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -244,20 +246,22 @@ __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, 
     const int r = find_range(fcs, G.nr, f);
     const int64_t t = fstart[r] + (f - fcs[r]);
     const int64_t m0 = t * G.hop / G.D;            // first block of the frame
-    const double2 *b0 = blk + (bcs[r] + (m0 - bstart[r])) * (int64_t)(K.nk + 2);
-    const int stride = K.nk + 2;
+    // bin-major blocks: neighbouring frames read neighbouring addresses
+    const double2 *b0 = blk + (bcs[r] + (m0 - bstart[r]));
+    const int64_t stride = nblocks;
     double2 sum = make_double2(0.0, 0.0);
     double l1 = 0.0;
     for (int j = 0; j < G.R; ++j) {
-        sum = cadd(sum, b0[j * stride + K.nk]);
-        l1 += b0[j * stride + K.nk + 1].x;
+        sum = cadd(sum, b0[K.nk * stride + j]);
+        l1 += b0[(K.nk + 1) * stride + j].x;
     }
     const double2 mean = make_double2(sum.x / G.N, sum.y / G.N);
     // V[k'] of the detrended frame at needed bin b
     auto V = [&](int b) {
         const double2 *rb = rot + b * G.R;
-        double2 z = b0[b];
-        for (int j = 1; j < G.R; ++j) z = cadd(z, cmul(rb[j], b0[j * stride + b]));
+        const double2 *bb = b0 + b * stride;
+        double2 z = bb[0];
+        for (int j = 1; j < G.R; ++j) z = cadd(z, cmul(rb[j], bb[j]));
         if (b == K.dc) z = csub(z, make_double2(mean.x * G.N, mean.y * G.N));
         return z;
     };
@@ -363,7 +367,7 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
                                    static_cast<const float *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
         }
         hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, G, K, d_fstart,
-                           d_fcs, d_bstart, d_bcs, nframes, rot, blk, delta, ed);
+                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed);
         e = hipGetLastError();
     }
     // the host tables are pageable: wait for the copies (and the kernels) before they go
