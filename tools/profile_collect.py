@@ -21,11 +21,13 @@ def last_json(path):
 
 
 json.dump(last_json(f"{src}/bench.json"), open(f"{dst}/{tag}_bench.json", "w"))
-for wl, suffix in (("", ""), ("_live", "_live"), ("_c5", "_c5")):
+for wl, suffix in (("", ""), ("_live", "_live"), ("_c5", "_c5"), ("_c5x", "_c5_exact")):
+    if not os.path.exists(f"{src}/kt{wl}"):
+        continue
     shutil.copy(f"{src}/kt{wl}/kt_kernel_stats.csv", f"{dst}/{tag}_kernel_stats{suffix}.csv")
     json.dump(last_json(f"{src}/kt{wl}.log"), open(f"{dst}/{tag}_bench{suffix}_under_rocprof.json", "w"))
 for sub, name, kernel, match in ((tag, "stft", "stft1024_kernel<short, 0, true>", {"files": 1440, "nperseg": 1024}),
-                                 (f"{tag}_c5", "cstft", "cstft4096_kernel<short, 4>", None),
+                                 (f"{tag}_c5", "cstft", "cstft4096_kernel<short, 4, false>", None),
                                  (f"{tag}_c5det", None, None, None)):
     out = subprocess.run([sys.executable, os.path.join(root, "tools", "pmc_summary.py"), f"{pmc}/{sub}"],
                          capture_output=True, text=True, check=True).stdout
