@@ -188,3 +188,36 @@ def test_certification_off_is_the_old_path():
         det.close()
     assert res.certified is None and res.refined_delta_frames == 0
     assert res2.certified and [(int(a["start"]), int(a["stop"])) for a in res2.detections] == d0
+
+
+def test_sharded_certification_matches_oracle():
+    """the constructed near-tie stream time-sharded over 3 rank-threads (each its own context and
+    spectrogram of its samples): the certificate is merged over the ranks, each rank refines its
+    part of the uncertain windows (which cross the shard edges: W = 375 frames, shards ~1250), and
+    every rank ends certified with the float64 oracle's detections"""
+    from stream_np_ops import run_threads
+    i, q, placed, _ = _near_tie_stream(seed=45)
+    rdets, _, _, _, _ = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - HOP, **KW)
+    buf, _ = iq.interleave(i, q)
+    n = buf.size // 2
+
+    def body(r, comm):
+        ctx = _lib.Context(0)
+        try:
+            det = iq.IQShardDetector(ctx, n, FS, N, N - HOP, BAND, NOISE, 4.0, True, rank=r, world=3, seg_len=512,
+                                     dtype=buf.dtype, certify=True, **KW)
+            det.upload(buf[2 * det.s0: 2 * det.s1])
+            det.spectrogram_and_delta()
+            res = det.detect(comm, thresholds=False)
+            det.close()
+            return res
+        finally:
+            ctx.close()
+
+    res = run_threads(3, body)
+    bs = HOP / FS
+    want = [(x[0], x[1]) for x in rdets]
+    for r in res:
+        assert r.certified and not r.near_tie and r.uncertain_initial >= len(placed) and r.refined_delta_frames > 0
+        assert [(int(a) * bs, int(b) * bs) for a, b, _ in r.detections] == want
+    assert len({(r.refined_delta_frames, r.uncertain_initial, r.detector_passes) for r in res}) == 1
