@@ -15,7 +15,8 @@
 //      max(MFMA alone, VALU alone), and a pass moved to MFMA removes its VALU time.
 //
 // Cycles from s_memtime, per loop iteration per SIMD.  Build:
-//   hipcc --offload-arch=gfx950 -O3 coissue_xpose.hip -o coissue_xpose
+//   hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize coissue_xpose.hip -o coissue_xpose
+// (no SLP: packed v_pk_fma_f32 would issue at a different rate than the scalar FMAs compared)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <algorithm>
@@ -154,6 +155,44 @@ __global__ __launch_bounds__(1024) void k_coissue(long long *cyc, float *out, in
     if (r == 1234.5f) out[threadIdx.x] = r;
 }
 
+// control for (b): the same loop with a bf16 MFMA (v_mfma_f32_16x16x32_bf16), which the guide
+// documents as running beside VALU fillers -- shows the method sees co-issue where it exists
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+template <int NM, int NV>
+__global__ __launch_bounds__(1024) void k_coissue_bf16(long long *cyc, float *out, int iters, float a, float b) {
+    const int lane = threadIdx.x & 63;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = a * (lane + i);
+    f4 acc[4] = {};
+    bf8 ma, mb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        ma[i] = (__bf16)(a * (lane + i));
+        mb[i] = (__bf16)(b * (lane - i));
+    }
+    __syncthreads();
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ma, mb, acc[m & 3], 0, 0, 0);
+            valu_block<NV / (NM > 0 ? NM : 1)>(v, a, b);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, NV / (NM > 0 ? NM : 1), 0);
+        }
+    }
+    __syncthreads();
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    stamp(cyc, t0, t1);
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r += v[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
+    if (r == 1234.5f) out[threadIdx.x] = r;
+}
+
 static double run(void (*kern)(long long *, float *, int, float, float), long long *cyc, float *out, int cus,
                   int iters) {
     // per workgroup t1 - t0 (all workgroups run at once, one per CU), averaged; best of 3
@@ -199,6 +238,15 @@ int main() {
                NM, NV, m, v, mv, il, std::max(m, v), m + v);                                                \
     }
     CO(16, 64) CO(16, 128) CO(16, 256) CO(32, 256) CO(32, 512) CO(64, 512)
+    printf("(b') control: NM v_mfma_f32_16x16x32_bf16 + NV FMAs, interleaved\n");
+#define CB(NM, NV)                                                                                          \
+    {                                                                                                       \
+        const double m = run(k_coissue_bf16<NM, 0>, cyc, out, cus, it), v = run(k_coissue<0, NV>, cyc, out, cus, it); \
+        const double mv = run(k_coissue_bf16<NM, NV>, cyc, out, cus, it);                                  \
+        printf("NM=%3d NV=%4d  mfma alone %7.1f  valu alone %7.1f  interleaved %7.1f  (max %7.1f, sum %7.1f)\n", NM, NV, \
+               m, v, mv, std::max(m, v), m + v);                                                            \
+    }
+    CB(16, 64) CB(16, 128) CB(16, 256) CB(32, 512)
     (void)hipFree(cyc);
     (void)hipFree(out);
     return 0;
