@@ -221,3 +221,14 @@ def test_sharded_certification_matches_oracle():
         assert r.certified and not r.near_tie and r.uncertain_initial >= len(placed) and r.refined_delta_frames > 0
         assert [(int(a) * bs, int(b) * bs) for a, b, _ in r.detections] == want
     assert len({(r.refined_delta_frames, r.uncertain_initial, r.detector_passes) for r in res}) == 1
+
+
+def test_chunked_stream_certifies():
+    """proc_iq_samples streaming the spectrogram through HBM in chunks (chunk_sec): the refinement
+    re-reads each uncertain window's samples from the source in chunk-sized pieces; the result is
+    certified and the float64 oracle's"""
+    i, q, placed, _ = _near_tie_stream(seed=47)
+    rdets, _, _, _, _ = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - HOP, **KW)
+    dets, _, _, r = iq.proc_iq_samples(i, q, FS, BAND, NOISE, chunk_sec=1.5, **KW)
+    assert r.certified and r.refined_delta_frames > 0 and r.uncertain_initial >= len(placed)
+    assert [(d.t_start, d.t_stop) for d in dets] == [(x[0], x[1]) for x in rdets]
