@@ -232,3 +232,26 @@ def test_chunked_stream_certifies():
     dets, _, _, r = iq.proc_iq_samples(i, q, FS, BAND, NOISE, chunk_sec=1.5, **KW)
     assert r.certified and r.refined_delta_frames > 0 and r.uncertain_initial >= len(placed)
     assert [(d.t_start, d.t_stop) for d in dets] == [(x[0], x[1]) for x in rdets]
+
+
+@pytest.mark.parametrize("hop", [1000, 2048, 512])
+def test_float64_refinement_other_hops(hop):
+    """the refinement's block geometry at other hops: D = gcd(N, hop) = 8 (one lane per block,
+    block_small_kernel), 2048 (R = 2), 512 (R = 8); the float64 delta against the oracle's"""
+    i, q, _ = synth.synth_iq(50 + hop, FS, 3.0, 1000.0, rate_per_min=30, snr_db=(10, 30))
+    buf, code = iq.interleave(i, q)
+    n = buf.size // 2
+    det = iq.IQShardDetector(context(0), n, FS, N, N - hop, BAND, NOISE, 4.0, True, dtype=buf.dtype, certify=True,
+                             **KW)
+    try:
+        det.process_host(buf[2 * det.s0: 2 * det.s1])
+        T = det.T
+        det._refine_local([(3, 40), (T - 30, T)])
+        d = det.plan.delta()
+        ed = det.plan.ed()
+    finally:
+        det.close()
+    _, _, _, _, ref = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - hop, **KW)
+    sel = np.r_[3:40, T - 30:T]
+    err = np.abs(d[sel] - ref[sel])
+    assert np.all(err <= ed[sel]) and ed[sel].max() < 1e-7, (err.max(), ed[sel].max())
