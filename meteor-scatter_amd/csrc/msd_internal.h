@@ -191,6 +191,16 @@ struct KernelTimer {
     ~KernelTimer();
 };
 
+// a float constant held in a VGPR for the rest of the kernel: on gfx950 a VALU operand read from
+// an SGPR issues at ~4.4 cycles per wave-instruction and a 32-bit literal at 2.65, a VGPR operand
+// at 2.3 (VOP2) / 2.65 (VOP3) (tools/ubench/operand_rate.hip); the compiler hoists uniform constants
+// into SGPRs or literals, the opaque move keeps this one in a VGPR
+__device__ __forceinline__ float vgpr_f(float c) {
+    float r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(c));
+    return r;
+}
+
 // scratch buffer i of the context grown to at least `bytes`
 int ctx_scratch(msd_ctx *ctx, int slot, size_t bytes, void **out);
 

@@ -62,10 +62,10 @@ __device__ __forceinline__ void dft4(float2 &a0, float2 &a1, float2 &a2, float2 
     a3 = csub(t1, t3);
 }
 
-// second half of a forward 8-point DFT: a_j = v_j + v_{j+4}, b_j = v_j - v_{j+4} given
+// second half of a forward 8-point DFT: a_j = v_j + v_{j+4}, b_j = v_j - v_{j+4} given; s = sqrt(1/2)
+// in a VGPR (vgpr_f: as an SGPR or literal operand its multiplies issue slower)
 __device__ __forceinline__ void dft8_tail(float2 *v, float2 a0, float2 a1, float2 a2, float2 a3, float2 b0, float2 b1,
-                                          float2 b2, float2 b3) {
-    const float s = 0.70710678118654752440f;
+                                          float2 b2, float2 b3, float s) {
     b1 = make_float2((b1.x + b1.y) * s, (b1.y - b1.x) * s);
     b2 = mul_mi(b2);
     b3 = make_float2((b3.y - b3.x) * s, -(b3.x + b3.y) * s);
@@ -76,14 +76,14 @@ __device__ __forceinline__ void dft8_tail(float2 *v, float2 a0, float2 a1, float
 }
 
 // in-place forward DFT of 8 points, natural order in and out
-__device__ __forceinline__ void dft8(float2 *v) {
+__device__ __forceinline__ void dft8(float2 *v, float s) {
     dft8_tail(v, cadd(v[0], v[4]), cadd(v[1], v[5]), cadd(v[2], v[6]), cadd(v[3], v[7]), csub(v[0], v[4]),
-              csub(v[1], v[5]), csub(v[2], v[6]), csub(v[3], v[7]));
+              csub(v[1], v[5]), csub(v[2], v[6]), csub(v[3], v[7]), s);
 }
 
 // dft8 of the windowed points d_j * w_j (componentwise), the window product of v_{j+4} shared
 // by the first-stage sum and difference: 3 ops per component pair instead of 4
-__device__ __forceinline__ void dft8_windowed(float2 *v, const float2 *d, const float2 *w) {
+__device__ __forceinline__ void dft8_windowed(float2 *v, const float2 *d, const float2 *w, float s) {
     float2 a[4], b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -91,7 +91,7 @@ __device__ __forceinline__ void dft8_windowed(float2 *v, const float2 *d, const 
         a[j] = make_float2(__builtin_fmaf(d[j].x, w[j].x, px), __builtin_fmaf(d[j].y, w[j].y, py));
         b[j] = make_float2(__builtin_fmaf(d[j].x, w[j].x, -px), __builtin_fmaf(d[j].y, w[j].y, -py));
     }
-    dft8_tail(v, a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]);
+    dft8_tail(v, a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], s);
 }
 
 
@@ -318,6 +318,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     };
     FileCur prev = cur;
     bool have_prev = false;
+    const float hs = vgpr_f(0.70710678118654752440f);  // sqrt(1/2) of the DFT8s, in a VGPR
 
     for (int64_t tl = tb; tl < te; ++tl) {
         const bool has_next = tl + 1 < te;
@@ -387,8 +388,8 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 
         // ---- pass 1 (Ns = 1): out[8 l + r].  One scratch per wave: frame A's transpose is
         // read back before frame B's is written (LDS executes a wave's accesses in order)
-        dft8_windowed(v[0], v[0], wv);
-        dft8_windowed(v[1], v[1], wv);
+        dft8_windowed(v[0], v[0], wv, hs);
+        dft8_windowed(v[1], v[1], wv, hs);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
 #pragma unroll
@@ -421,8 +422,8 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 v[1][r] = cmul(v[1][r], w[r]);
             }
         }
-        dft8(v[0]);
-        dft8(v[1]);
+        dft8(v[0], hs);
+        dft8(v[1], hs);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
 #pragma unroll
@@ -448,8 +449,8 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 v[1][r] = cmul(v[1][r], w[r]);
             }
         }
-        dft8(v[0]);
-        dft8(v[1]);
+        dft8(v[0], hs);
+        dft8(v[1], hs);
         // ---- post: X' = 2X = (Z + conj Zm) + W^k (-i)(Z - conj Zm), Zm = Z[(512 - k) mod 512],
         // and from the same e, o the mirror bin X'[512 - k] = conj(e - W^k o).  Lane l owns the
         // four pairs (k = pi(l) + 64 r, 512 - k), r = 0..3: Zm sits in lane l^1, register 7-r

@@ -39,6 +39,15 @@
 #define PERM(r) "v_perm_b32 " #r ", v41, v42, v43\n"
 #define BFE(r) "v_bfe_i32 " #r ", v41, 16, 16\n"
 #define MOV(r) "v_mov_b32_e32 " #r ", v41\n"
+// operand sources other than VGPRs: an SGPR, a 32-bit literal, an inline constant
+#define FMA_SGPR(r) "v_fma_f32 " #r ", v41, s40, " #r "\n"
+#define FMA_NEGSGPR(r) "v_fma_f32 " #r ", v41, s40, -" #r "\n"
+#define MUL_LIT(r) "v_mul_f32_e32 " #r ", 0x3f3504f3, " #r "\n"
+#define FMAMK_LIT(r) "v_fmamk_f32 " #r ", v41, 0x3f3504f3, " #r "\n"
+#define MUL_SGPR(r) "v_mul_f32_e32 " #r ", s40, " #r "\n"
+#define ADD_SGPR(r) "v_add_f32_e32 " #r ", s40, " #r "\n"
+#define MUL_INL(r) "v_mul_f32_e32 " #r ", 0.5, " #r "\n"
+#define FMA_NEGV(r) "v_fma_f32 " #r ", v41, v42, -" #r "\n"
 // packed / mixed bodies on the register pairs v[8:9], v[12:13], ... (8 independent chains)
 #define G8P(OP) OP(8, 9) OP(12, 13) OP(16, 17) OP(20, 21) OP(24, 25) OP(28, 29) OP(32, 33) OP(36, 37)
 #define PKADD(a, b) "v_pk_add_f32 v[" #a ":" #b "], v[42:43], v[" #a ":" #b "]\n"
@@ -91,6 +100,14 @@ KERNEL(k_cvt, CVT)
 KERNEL(k_perm, PERM)
 KERNEL(k_bfe, BFE)
 KERNEL(k_mov, MOV)
+KERNEL(k_fma_sgpr, FMA_SGPR)
+KERNEL(k_fma_negsgpr, FMA_NEGSGPR)
+KERNEL(k_mul_lit, MUL_LIT)
+KERNEL(k_fmamk_lit, FMAMK_LIT)
+KERNEL(k_mul_sgpr, MUL_SGPR)
+KERNEL(k_add_sgpr, ADD_SGPR)
+KERNEL(k_mul_inl, MUL_INL)
+KERNEL(k_fma_negv, FMA_NEGV)
 #define G8 G8P
 KERNEL(k_pkadd, PKADD)
 KERNEL(k_pkfma, PKFMA)
@@ -133,6 +150,8 @@ int main() {
         R(k_mul_diff, 32) R(k_cnd_vcc, 32) R(k_cnd_sgpr, 32) R(k_dpp_mov, 32) R(k_dpp_add, 32)
         R(k_sdwa_cvt, 32) R(k_cvt, 32) R(k_perm, 32) R(k_bfe, 32) R(k_mov, 32) R(k_pkadd, 32) R(k_pkfma, 32)
         R(k_mix_addfma, 64)
+        R(k_fma_sgpr, 32) R(k_fma_negsgpr, 32) R(k_mul_lit, 32) R(k_fmamk_lit, 32) R(k_mul_sgpr, 32)
+        R(k_add_sgpr, 32) R(k_mul_inl, 32) R(k_fma_negv, 32)
     }
     (void)hipFree(cyc);
     return 0;
