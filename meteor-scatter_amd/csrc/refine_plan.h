@@ -52,6 +52,8 @@ inline int plan_refine(int nperseg, int64_t hop, double fs, int band_lo, int ban
     };
     if (nperseg < 4 || hop <= 0 || !(fs > 0) || nranges < 0 || (nranges && !ranges))
         return err(E_INVALID, "bad arguments");
+    // the kernels form twiddle indices k * n (k < N, n <= N) in 32 bits
+    if (nperseg > 65536) return err(E_UNSUPPORTED, "nperseg above 65536");
     const int N = nperseg;
     const int h = N / 2;
     auto ok = [&](int lo, int hi) { return hi < lo || (lo >= -h && hi <= N - h - 1); };

@@ -164,3 +164,4 @@ def test_refine_plan_under_sanitizers(harness):
     assert run(harness, "refine", 4096, 1024, 21, 22, -65, -63, 10 ** 6, 0, 10, 5, 20).startswith("err")
     assert run(harness, "refine", 4096, 1024, 21, 5000, -65, -63, 10 ** 6, 0, 10).startswith("err")
     assert run(harness, "refine", 4096, 1024, 21, 22, -65, -63, 8192, 0, 10).startswith("err")
+    assert run(harness, "refine", 131072, 1024, 21, 22, -65, -63, 10 ** 7, 0, 10).startswith("err")  # > 65536
