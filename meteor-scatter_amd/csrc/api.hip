@@ -545,6 +545,7 @@ void msd_block_plan_destroy(msd_block_plan *p) {
     hipFree(p->d_tw);
     hipFree(p->d_bins);
     hipFree(p->d_bconst);
+    hipFree(p->d_energy);
     delete p;
 }
 

@@ -210,8 +210,7 @@ template <typename T, int SPL>
 __global__ __launch_bounds__(256) void block_delta2_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len, int64_t nfiles,
     int64_t blocks_per_file, int64_t B, int L, const double *__restrict__ g_win, const double *__restrict__ bconst,
-    int nband, int nnoise, double *__restrict__ band_db, double *__restrict__ noise_db, double *__restrict__ delta,
-    int64_t ld) {
+    int nband, int nnoise, double2 *__restrict__ energy) {
     extern __shared__ double smem_d[];
     // window [16 segments][SPL + 1]: the window reads are ds_read2_b64 (two accesses of 4 x 16
     // lanes, bank = dword mod 32), so with an odd pitch segment s starts at bank 2s mod 32 and the
@@ -261,39 +260,60 @@ __global__ __launch_bounds__(256) void block_delta2_kernel(
             default: break;
         }
         __builtin_amdgcn_wave_barrier();
-        // band dB on the group's lane 0, noise dB on lane 1 (one float64 log10 issued per wave
-        // instead of two in a row); lane 0 takes lane 1's value by a shuffle of the whole wave
-        double e_db = 0.0;
-        if (sub < 2 && valid) {
-            const double e = (sub == 0 ? np_sum_small(ArrRef{pb}, 0, nband) : np_sum_small(ArrRef{pb}, nband, nnoise)) +
-                             1e-12;
-            e_db = 10.0 * log10(e);
-        }
-        const double nd_next = __shfl_down(e_db, 1, 64);
-        if (sub == 0 && valid) {
-            const double bd = e_db;
-            const double nd = nd_next;
-            const int64_t o = f * ld + b;
-            if (band_db) band_db[o] = bd;
-            if (noise_db) noise_db[o] = nd;
-            delta[o] = bd - nd;
-        }
+        // band energy on the group's lane 0, noise energy on lane 1 (numpy's pairwise order over the
+        // powers in LDS); lane 0 takes lane 1's by a shuffle of the whole wave.  The dB values and
+        // delta follow in block_db_kernel, 64 blocks per wave: two float64 log10 per block on one
+        // lane in sixteen cost a quarter of this kernel's float64 issue
+        double e = 0.0;
+        if (sub < 2 && valid)
+            e = (sub == 0 ? np_sum_small(ArrRef{pb}, 0, nband) : np_sum_small(ArrRef{pb}, nband, nnoise)) + 1e-12;
+        const double e_next = __shfl_down(e, 1, 64);
+        if (sub == 0 && valid) energy[gb] = make_double2(e, e_next);
         __builtin_amdgcn_wave_barrier();  // pbuf is rewritten by the next group
     }
+}
+
+// 10 log10 of the two energies and their difference, one thread per block (main.py:388-393)
+__global__ __launch_bounds__(256) void block_db_kernel(const double2 *__restrict__ energy,
+                                                       const int64_t *__restrict__ len, int64_t nfiles,
+                                                       int64_t blocks_per_file, int64_t B, double *__restrict__ band_db,
+                                                       double *__restrict__ noise_db, double *__restrict__ delta,
+                                                       int64_t ld) {
+    const int64_t gb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t f = gb / blocks_per_file;
+    const int64_t b = gb - f * blocks_per_file;
+    if (f >= nfiles || b >= len[f] / B) return;
+    const double2 e = energy[gb];
+    const double bd = 10.0 * log10(e.x);
+    const double nd = 10.0 * log10(e.y);
+    const int64_t o = f * ld + b;
+    if (band_db) band_db[o] = bd;
+    if (noise_db) noise_db[o] = nd;
+    delta[o] = bd - nd;
 }
 
 template <typename T, int SPL>
 int launch_bd2(msd_block_plan *p, const void *x, const int64_t *off, const int64_t *len, int64_t nfiles,
                int64_t max_blocks, double *band_db, double *noise_db, double *delta, int64_t ld) {
     const int64_t blocks = nfiles * max_blocks;
+    if ((size_t)blocks > p->energy_cap) {  // grown once per plan (the stream is drained first)
+        MSD_HIP(hipStreamSynchronize(p->ctx->stream));
+        MSD_HIP(hipFree(p->d_energy));
+        p->d_energy = nullptr;
+        p->energy_cap = 0;
+        MSD_HIP(hipMalloc(&p->d_energy, sizeof(double2) * (size_t)blocks));
+        p->energy_cap = (size_t)blocks;
+    }
     // persistent grid: a few workgroups per CU, each walking groups of 16 blocks
     const int64_t grid = std::min<int64_t>((blocks + BD2_GROUPS - 1) / BD2_GROUPS, (int64_t)p->ctx->num_cu * 8);
     const size_t lds = sizeof(double) * (16 * bd2_pitch(SPL) + BD2_GROUPS * (size_t)(p->nbins > 0 ? p->nbins : 1));
     hipLaunchKernelGGL((block_delta2_kernel<T, SPL>), dim3((unsigned)grid), dim3(256), lds, p->ctx->stream,
                        static_cast<const T *>(x), off, len, nfiles, max_blocks, p->block_size, p->L, p->d_window,
                        p->d_bconst, p->band_hi - p->band_lo + 1 > 0 ? p->band_hi - p->band_lo + 1 : 0,
-                       p->noise_hi - p->noise_lo + 1 > 0 ? p->noise_hi - p->noise_lo + 1 : 0, band_db, noise_db,
-                       delta, ld);
+                       p->noise_hi - p->noise_lo + 1 > 0 ? p->noise_hi - p->noise_lo + 1 : 0, p->d_energy);
+    MSD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(block_db_kernel, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, p->ctx->stream,
+                       p->d_energy, len, nfiles, max_blocks, p->block_size, band_db, noise_db, delta, ld);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }

@@ -82,6 +82,8 @@ struct msd_block_plan {
     // segment) the rotation exp(-i th (seg*SPL + SPL - 1)) — host-computed in float64
     double *d_bconst = nullptr;
     int spl = 0;                          // samples per lane segment of the fast path
+    double2 *d_energy = nullptr;          // fast path: per block (band, noise) energy + 1e-12, grown
+    size_t energy_cap = 0;                // blocks d_energy holds
 };
 
 struct msd_welch_plan {

@@ -11,8 +11,9 @@ for i in $(seq 1 "$N"); do
   for t in "$@"; do
     lib=$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp_$t.so
     [ "$t" = cur ] && lib=$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp.so
+    extra=""; [ "$WL" = c3 ] && extra="--no-c5"
     MSD_LIB_PATH=$lib timeout -k 10 200 python3 "$ROOT/bench.py" --workload "$WL" --steps 10 --warmup 2 \
-        --no-cpu-baseline > "$ROOT/gpurun_out/ab_${WL}_${t}_$i.log" 2>&1 || exit 1
+        --no-cpu-baseline $extra > "$ROOT/gpurun_out/ab_${WL}_${t}_$i.log" 2>&1 || exit 1
   done
 done
 for t in "$@"; do
