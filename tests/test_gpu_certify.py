@@ -255,3 +255,60 @@ def test_float64_refinement_other_hops(hop):
     sel = np.r_[3:40, T - 30:T]
     err = np.abs(d[sel] - ref[sel])
     assert np.all(err <= ed[sel]) and ed[sel].max() < 1e-7, (err.max(), ed[sel].max())
+
+
+def _global_near_tie_stream(seed=61, seconds=12.0, eps=3e-7):
+    """float32 I/Q whose global-threshold decisions (main.py:404-412: delta > mean + k std of the
+    whole stream) at a few frames sit eps dB above or below thr0: a tone in the newest hop block of
+    frame fi (frames fi..fi+3 see it), its amplitude bisected with thr0 recomputed over the whole
+    delta each time; every placement moves thr0, so the placements are repeated until they hold
+    together"""
+    i32, q32 = _iq_f32(seed, seconds, rate=4.0)
+    z = i32.astype(np.float64) + 1j * q32.astype(np.float64)
+    tone = np.exp(2j * np.pi * (21 * FS / N) * np.arange(HOP) / FS)
+    T = (len(z) - N) // HOP + 1
+    _, _, _, _, D = Q.proc_iq_ref(z.real, z.imag, FS, BAND, NOISE, N, N - HOP, flag_adaptive_threshold=False)
+    thr = np.mean(D) + 4.0 * np.std(D)
+    placed = [fi for fi in range(200, T - 8, 700) if D[fi] < thr - 0.5]
+    orig = {fi: z[fi * HOP + 3 * HOP: fi * HOP + 4 * HOP].copy() for fi in placed}
+    for _sweep in range(5):
+        for k, fi in enumerate(placed):
+            _, _, _, _, D = Q.proc_iq_ref(z.real, z.imag, FS, BAND, NOISE, N, N - HOP, flag_adaptive_threshold=False)
+            sign = 1 if k % 2 == 0 else -1
+            blk = slice(fi * HOP + 3 * HOP, fi * HOP + 4 * HOP)
+
+            def gap(alpha):
+                v = orig[fi] + alpha * tone
+                z[blk] = v.real.astype(np.float32) + 1j * v.imag.astype(np.float32)
+                D2 = D.copy()
+                for j in range(fi, min(fi + 4, T)):
+                    D2[j] = _frame_delta(z, j)
+                return D2[fi] - (np.mean(D2) + 4.0 * np.std(D2)) - sign * eps
+
+            lo, hi = 0.0, 50.0
+            while gap(hi) < 0:
+                hi *= 2
+            for _ in range(80):
+                mid = 0.5 * (lo + hi)
+                if gap(mid) < 0:
+                    lo = mid
+                else:
+                    hi = mid
+            gap(min((lo, hi), key=lambda a: abs(gap(a))))  # leaves z with the chosen amplitude
+    i_, q_ = z.real.astype(np.float32), z.imag.astype(np.float32)
+    _, thr0, _, _, delta = Q.proc_iq_ref(i_, q_, FS, BAND, NOISE, N, N - HOP, flag_adaptive_threshold=False)
+    return i_, q_, placed, np.abs(delta[placed] - thr0)
+
+
+def test_global_threshold_near_ties_decide_as_the_oracle():
+    """the global detector (flag_adaptive_threshold=False): thr0's error bound comes from the whole
+    stream's ed sums; decisions placed within 3e-7 dB of thr0 are listed, and the refinement (the
+    whole stream: thr0 reads every frame) gives the oracle's detections"""
+    i, q, placed, margins = _global_near_tie_stream()
+    assert len(placed) >= 2 and margins.max() < 5e-6, (placed, margins)
+    rdets, _, _, _, _ = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - HOP, flag_adaptive_threshold=False)
+    _, _, _, r0 = iq.proc_iq_samples(i, q, FS, BAND, NOISE, flag_adaptive_threshold=False, exact_decisions=False)
+    assert r0.certified is False and r0.uncertain >= 1
+    dets, _, _, r = iq.proc_iq_samples(i, q, FS, BAND, NOISE, flag_adaptive_threshold=False)
+    assert r.certified and r.refined_delta_frames > 0
+    assert [(d.t_start, d.t_stop) for d in dets] == [(x[0], x[1]) for x in rdets]
