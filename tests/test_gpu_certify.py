@@ -312,3 +312,29 @@ def test_global_threshold_near_ties_decide_as_the_oracle():
     dets, _, _, r = iq.proc_iq_samples(i, q, FS, BAND, NOISE, flag_adaptive_threshold=False)
     assert r.certified and r.refined_delta_frames > 0
     assert [(d.t_start, d.t_stop) for d in dets] == [(x[0], x[1]) for x in rdets]
+
+
+def test_certification_over_rccl_single_rank():
+    """the certified detector through the exchange protocol over RCCL (stream.RcclComm at world
+    size 1 on the one-GPU box: halos and ed halos, the ed sums, the merged certificate go through
+    ncclAllGather) on the near-tie stream: certified, the oracle's detections"""
+    from meteorgpu import stream
+    from meteorgpu.batch import Communicator
+    i, q, placed, _ = _near_tie_stream(seed=49)
+    rdets, _, _, _, _ = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - HOP, **KW)
+    buf, _ = iq.interleave(i, q)
+    n = buf.size // 2
+    ctx = _lib.Context(0)
+    comm = Communicator(ctx, 1, Communicator.unique_id(), 0)
+    try:
+        det = iq.IQShardDetector(ctx, n, FS, N, N - HOP, BAND, NOISE, 4.0, True, dtype=buf.dtype, certify=True, **KW)
+        det.upload(buf[2 * det.s0: 2 * det.s1])
+        det.spectrogram_and_delta()
+        res = det.detect(stream.RcclComm(comm, 0, 1), thresholds=False)
+        det.close()
+    finally:
+        comm.close()
+        ctx.close()
+    bs = HOP / FS
+    assert res.certified and res.refined_delta_frames > 0 and res.uncertain_initial >= len(placed)
+    assert [(int(a) * bs, int(b) * bs) for a, b, _ in res.detections] == [(x[0], x[1]) for x in rdets]
