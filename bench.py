@@ -229,6 +229,12 @@ def main_live(a, world, rank, local, job_of):
                      "algorithmic_flops_per_launch": flops},
         "kernel_ms_per_step": {"welch": round(avg_s * 1e3, 4), "live_detect": round(l_ms / max(l_n, 1), 4)},
     }
+    # the near-tie guard of every recording (margin.py, live part; outside the timed region): a
+    # decision within the proven over-noise error bound of its threshold would be flagged
+    lb.check_near_ties(warn=False)
+    out["near_tie"] = {"files_flagged": int(lb.near_tie.sum()), "files": F,
+                       "max_decision_bound_db": float(np.max(lb.decision_bounds)),
+                       "min_margin_db": float(np.min(lb.min_margins))}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
         secs = 1800
         v, dt = cpu_baseline_live(pool, secs)
