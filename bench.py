@@ -567,6 +567,7 @@ def main():
     if "roofline" in r:
         out["roofline"] = r["roofline"]
     out["kernel_ms_per_step"] = r["kernel_ms"]
+    out["near_tie"] = r["near_tie"]  # margin.py's guard over this rank's files (C3 decisions vs numpy)
     if not a.shard_day:
         # BASELINE configs[3] (C4): the SAME 1440-file day sharded over the N ranks (strong scaling),
         # measured after the weak-scaling line so that the driver's 1/2/4/8 runs carry both curves
@@ -653,8 +654,14 @@ def run_c3(a, ctx, job, rank, world, pool, lo, hi, one_day, detail):
     sync_all()
     # correctness guard on the benchmarked data: every file's detector finished cleanly and
     # the (all-reduced) hour histogram holds every detection of every rank
-    _, counts, status, _ = bp.detections()
+    import warnings
+    with warnings.catch_warnings():  # the near-tie guard's verdict is reported in the line instead
+        warnings.simplefilter("ignore")
+        _, counts, status, margins = bp.detections()
     assert (status == 0).all(), "detector status"
+    near = {"files_flagged": int(bp.near_tie.sum()), "files": F,
+            "max_decision_bound_db": float(np.max(bp.decision_bounds)) if F else 0.0,
+            "min_margin_db": float(np.min(margins)) if F else float("inf")}
     # events only around the roofline kernel in the timed region; the breakdown of the other
     # kernels (kernel_ms_per_step) comes from one more step with every kernel timed, after it
     for c in bp.contexts:
@@ -675,7 +682,8 @@ def run_c3(a, ctx, job, rank, world, pool, lo, hi, one_day, detail):
     hist = bp.hour_counts()
     assert int(hist.sum()) == total_dets, "hour histogram != detections"
     stft_ms, stft_launches = ctx.timing_get(_lib.K_STFT)
-    res = {"elapsed": elapsed, "detections": total_dets, "hour_total": int(hist.sum()), "T": bp.T, "K": bp.K}
+    res = {"elapsed": elapsed, "detections": total_dets, "hour_total": int(hist.sum()), "T": bp.T, "K": bp.K,
+           "near_tie": near}
     if not a.no_spectrogram and stft_launches:
         avg_s = stft_ms / stft_launches / 1e3
         alg_bytes = F * (n * 2 + bp.K * bp.T * 4)  # samples read once + spectrogram written once
