@@ -344,7 +344,8 @@ int msd_stream_certificate(msd_stream_plan *plan, int64_t *uncertain, double *mi
  * 10*log10(E + 1e-12)) by a direct DFT of the band bins (blocks of gcd(nperseg, hop) samples, the
  * Hann window as three bin taps) -- into delta[t] and its error bound against the reference into
  * ed[t] (device float64).  x: device interleaved I/Q (MSD_CI16 or MSD_CF32), n_samples complex
- * samples.  Synchronous. */
+ * samples.  Asynchronous on the context's stream (the ranges are copied before the call
+ * returns; nperseg <= 65536). */
 int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg, int64_t hop,
                        double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo, int32_t noise_hi,
                        const int64_t *ranges, int64_t nranges, double *delta, double *ed);

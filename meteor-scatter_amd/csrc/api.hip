@@ -178,6 +178,9 @@ void msd_destroy(msd_ctx *ctx) {
     for (auto e : ctx->pool) hipEventDestroy(e);
     for (void *p : ctx->scratch)
         if (p) hipFree(p);
+    if (ctx->rf_w) hipFree(ctx->rf_w);
+    if (ctx->rf_ev) hipEventSynchronize(ctx->rf_ev), hipEventDestroy(ctx->rf_ev);
+    if (ctx->rf_pin) hipHostFree(ctx->rf_pin);
     if (ctx->copy_stream) {
         hipStreamSynchronize(ctx->copy_stream);
         hipStreamDestroy(ctx->copy_stream);

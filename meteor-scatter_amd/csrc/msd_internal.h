@@ -53,6 +53,13 @@ struct msd_ctx {
     // (slot 4: msd_iq_delta64_dev's block table, rotations and ranges)
     void *scratch[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t scratch_bytes[5] = {0, 0, 0, 0, 0};
+    // msd_iq_delta64_dev's twiddle table W^m (m < rf_w_n), built once per frame length
+    double2 *rf_w = nullptr;
+    int rf_w_n = 0;
+    // its per-call tables staged in pinned memory (no stream sync), reusable once rf_ev has passed
+    void *rf_pin = nullptr;
+    size_t rf_pin_bytes = 0;
+    hipEvent_t rf_ev = nullptr;
 };
 
 struct msd_stft_plan {

@@ -20,7 +20,9 @@
 // Goertzel chains and the combination; the reference's: pocketfft's 4 log2 N + 8 and the detrend /
 // window roundings), against sum |v_n w_n| <= sum |z_n| + N |mean|: ~1e-12 dB, so a decision that
 // stays uncertain after refinement is a genuine float64 near tie.
+#include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <numeric>
 #include <type_traits>
 #include <vector>
@@ -306,26 +308,42 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     RefineGeom &G = P.G;
     const std::vector<int64_t> &fstart = P.fstart, &fcs = P.fcs, &bstart = P.bstart, &bcs = P.bcs;
     const int64_t nblocks = P.nblocks, nframes = P.nframes;
-    // host tables: W^m (m < N), then the per-bin block rotations rot[b][j] = W^{k_b j D} (j < R)
-    const int R = G.R;
-    std::vector<double2> tab((size_t)N + (size_t)K.nk * R);
-    for (int m = 0; m < N; ++m) {
-        const double a = -2.0 * M_PI * (double)m / (double)N;
-        tab[m] = make_double2(std::cos(a), std::sin(a));
-    }
-    for (int b = 0; b < K.nk; ++b)
-        for (int j = 0; j < R; ++j) tab[(size_t)N + (size_t)b * R + j] = tab[(size_t)G.D * (((int64_t)K.km[b] * j) % R)];
     DeviceGuard g(ctx->device);
     hipStream_t st = ctx->stream;
+    // W^m (m < N): built and uploaded once per frame length (N sin / cos on the host cost
+    // ~0.2 ms, more than the refinement's other host work), kept on the context
+    if (ctx->rf_w_n != N) {
+        std::vector<double2> W(N);
+        for (int m = 0; m < N; ++m) {
+            const double a = -2.0 * M_PI * (double)m / (double)N;
+            W[m] = make_double2(std::cos(a), std::sin(a));
+        }
+        MSD_HIP(hipStreamSynchronize(st));
+        if (ctx->rf_w) MSD_HIP(hipFree(ctx->rf_w));
+        ctx->rf_w = nullptr;
+        ctx->rf_w_n = 0;
+        MSD_HIP(hipMalloc(&ctx->rf_w, sizeof(double2) * N));
+        MSD_HIP(hipMemcpy(ctx->rf_w, W.data(), sizeof(double2) * N, hipMemcpyHostToDevice));
+        ctx->rf_w_n = N;
+    }
+    const double2 *Wd = ctx->rf_w;
+    // per call: the per-bin block rotations rot[b][j] = W^{k_b j D} (j < R), and the ranges
+    const int R = G.R;
+    std::vector<double2> rt((size_t)K.nk * R);
+    for (int b = 0; b < K.nk; ++b)
+        for (int j = 0; j < R; ++j) {
+            const int64_t m = (int64_t)G.D * (((int64_t)K.km[b] * j) % R);
+            const double a = -2.0 * M_PI * (double)m / (double)N;
+            rt[(size_t)b * R + j] = make_double2(std::cos(a), std::sin(a));
+        }
     const size_t nb_blk = (sizeof(double2) * (size_t)nblocks * (K.nk + 2) + 255) / 256 * 256;
-    const size_t nb_tab = (sizeof(double2) * tab.size() + 255) / 256 * 256;
+    const size_t nb_rot = (sizeof(double2) * rt.size() + 255) / 256 * 256;
     const size_t nb_meta = sizeof(int64_t) * (4 * (size_t)nranges + 2);
     void *d = nullptr;
-    if (int rc = ctx_scratch(ctx, 4, nb_blk + nb_tab + nb_meta, &d)) return rc;  // grown once, kept
+    if (int rc = ctx_scratch(ctx, 4, nb_blk + nb_rot + nb_meta, &d)) return rc;  // grown once, kept
     auto *blk = static_cast<double2 *>(d);
-    auto *Wd = reinterpret_cast<double2 *>(static_cast<char *>(d) + nb_blk);
-    const double2 *rot = Wd + N;
-    auto *meta = reinterpret_cast<int64_t *>(static_cast<char *>(d) + nb_blk + nb_tab);
+    auto *rot = reinterpret_cast<double2 *>(static_cast<char *>(d) + nb_blk);
+    auto *meta = reinterpret_cast<int64_t *>(static_cast<char *>(d) + nb_blk + nb_rot);
     std::vector<int64_t> hm;
     hm.insert(hm.end(), fstart.begin(), fstart.end());
     hm.insert(hm.end(), fcs.begin(), fcs.end());
@@ -333,8 +351,25 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     hm.insert(hm.end(), bcs.begin(), bcs.end());
     const int64_t *d_fstart = meta, *d_fcs = meta + nranges, *d_bstart = meta + 2 * nranges + 1,
                   *d_bcs = meta + 3 * nranges + 1;
-    hipError_t e = hipMemcpyAsync(Wd, tab.data(), sizeof(double2) * tab.size(), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(meta, hm.data(), sizeof(int64_t) * hm.size(), hipMemcpyHostToDevice, st);
+    // both tables through a pinned staging block (the copies are truly async, so the call returns
+    // while the kernels run); the previous call's copies have left it once its event has passed
+    const size_t b_rt = sizeof(double2) * rt.size(), b_hm = sizeof(int64_t) * hm.size();
+    if (!ctx->rf_ev) MSD_HIP(hipEventCreateWithFlags(&ctx->rf_ev, hipEventDisableTiming));
+    else MSD_HIP(hipEventSynchronize(ctx->rf_ev));
+    if (ctx->rf_pin_bytes < b_rt + b_hm) {
+        if (ctx->rf_pin) MSD_HIP(hipHostFree(ctx->rf_pin));
+        ctx->rf_pin = nullptr;
+        ctx->rf_pin_bytes = 0;
+        const size_t want = std::max<size_t>(b_rt + b_hm, 4096);
+        MSD_HIP(hipHostMalloc(&ctx->rf_pin, want, hipHostMallocDefault));
+        ctx->rf_pin_bytes = want;
+    }
+    char *pin = static_cast<char *>(ctx->rf_pin);
+    std::memcpy(pin, rt.data(), b_rt);
+    std::memcpy(pin + b_rt, hm.data(), b_hm);
+    hipError_t e = hipMemcpyAsync(rot, pin, b_rt, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(meta, pin + b_rt, b_hm, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(ctx->rf_ev, st);
     if (e == hipSuccess) {
         KernelTimer timer(ctx, K_REFINE);
         if (G.D >= 64) {  // rows of 16 lanes, S = D/16 (a multiple of 4) samples per lane
@@ -370,8 +405,6 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
                            d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed);
         e = hipGetLastError();
     }
-    // the host tables are pageable: wait for the copies (and the kernels) before they go
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "msd_iq_delta64_dev");
     return MSD_OK;
 }
