@@ -77,7 +77,7 @@ def parse():
                     help="c3: the headline day batch (default); live: the phase-2 live detector "
                          "(Welch band powers + state machine) over a day of 4 kHz audio; c5: 192 kHz I/Q, "
                          "4096-point two-sided spectrogram, 75 %% overlap, 3 h of the 24 h stream per GPU; files: "
-                         "end to end from WAV files on disk (native reader, pinned double-buffered uploads)")
+                         "end to end from WAV files on disk (native reader, pinned triple-buffered uploads)")
     return ap.parse_args()
 
 
@@ -419,7 +419,7 @@ def run_c5(a, ctx, job, rank, world):
 def main_files(a, world, rank, local, job_of):
     """End to end from disk: `--files` one-minute 48 kHz WAVs written to a temp dir, then
     meteorgpu.ingest.WavDay (native reader threads → pinned memory → copy stream → the C3
-    pipeline, double-buffered batches of 120).  The page cache is warm (files just written):
+    pipeline, triple-buffered batches of 120).  The page cache is warm (files just written):
     this measures decode + PCIe + compute, not the disk."""
     import shutil
     import tempfile
@@ -456,7 +456,7 @@ def main_files(a, world, rank, local, job_of):
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic: {F} one-minute 48 kHz int16 WAV files per GPU (page cache warm)",
             "config": {"workload": "files -> native WAV reader (8 threads) -> pinned host -> copy stream -> STFT + "
-                                   "block delta + adaptive detector, batches of 120, double-buffered",
+                                   "block delta + adaptive detector, batches of 120, triple-buffered",
                        "files_per_gpu": F, "read_s": round(info["read_s"], 3),
                        "detections": int(sum(len(x) for x in dets)), "hour_total": int(hist.sum())},
         }

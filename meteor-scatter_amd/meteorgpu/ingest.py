@@ -3,9 +3,10 @@
 ``read(path)`` is the native counterpart of ``scipy.io.wavfile.read`` (dsp/src/main.py:249):
 libmsdsp parses the RIFF chunks and preads the samples.  ``WavDay`` runs a list of
 equal-format recordings (a day of one-minute files) through ``BatchPipeline`` in batches,
-double-buffered: while the GPU processes batch i, reader threads decode batch i+1 straight
-into page-locked host memory (the C calls release the GIL), the upload runs on the context's
-copy stream, and a stream fence orders the next compute after it.  File start times come from
+triple-buffered: while the GPU uploads and processes batch i, reader threads decode the next
+batches straight into page-locked host memory (the C calls release the GIL), the uploads run
+back to back on the context's copy stream, and a stream fence orders each batch's compute
+after its own upload.  File start times come from
 the reference's file-name conventions (``wav.start_datetime_from_name``) or are given.
 """
 from __future__ import annotations
@@ -71,9 +72,15 @@ class PinnedBuffer:
 
 
 class WavDay:
-    """Detections for many equal-format WAV files, batched and double-buffered (see module doc).
+    """Detections for many equal-format WAV files, batched and triple-buffered (see module doc).
 
-    ``run()`` returns (per-file detections [start, stop, db] rows, hour histogram, timings)."""
+    ``run()`` returns (per-file detections [start, stop, db] rows, hour histogram, timings).
+    The pipeline keeps the copy engine busy: a background thread decodes batch b + 1 (and b + 2)
+    into free page-locked slots while batch b uploads and computes, and the upload of b + 1 is
+    enqueued before the host waits for b's detections, so consecutive uploads run back to back
+    and the whole run is bound by PCIe."""
+
+    SLOTS = 3  # pinned host + device batch buffers: one uploading, one decoding, one computing
 
     def __init__(self, ctx: _lib.Context, paths, batch_files: int = 120, start_times=None, base_time=None,
                  readers: int = 8, **pipeline_kwargs):
@@ -94,15 +101,22 @@ class WavDay:
         self.bp = BatchPipeline(ctx, self.B, self.n, self.fs, dtype=self.dtype, **pipeline_kwargs)
         es = self.dtype.itemsize
         self.slot_bytes = self.B * self.bp.n_pad * es
-        self.d_x = [self.bp.d_x, ctx.alloc(self.slot_bytes)]
-        self.d_st = [self.bp.d_start_us, ctx.alloc(self.B * 8)]
-        self.h_x = [PinnedBuffer(ctx, self.slot_bytes) for _ in range(2)]
-        self.h_st = [PinnedBuffer(ctx, self.B * 8) for _ in range(2)]
+        nbatch = (len(self.paths) + self.B - 1) // self.B
+        self.S = min(self.SLOTS, max(1, nbatch))
+        self.d_x = [self.bp.d_x] + [ctx.alloc(self.slot_bytes) for _ in range(self.S - 1)]
+        self.d_st = [self.bp.d_start_us] + [ctx.alloc(self.B * 8) for _ in range(self.S - 1)]
+        self.h_x = [PinnedBuffer(ctx, self.slot_bytes) for _ in range(self.S)]
+        self.h_st = [PinnedBuffer(ctx, self.B * 8) for _ in range(self.S)]
         self.pool = ThreadPoolExecutor(max_workers=max(1, int(readers)))
+        self.decoder = ThreadPoolExecutor(max_workers=1)  # one batch at a time, its files on `pool`
         self.bp.hist.base_us = int(self.base_us)
+        self._short = False  # d_len / d_nb hold a short last batch's lengths
 
-    def _read_batch(self, b: int, slot: int) -> int:
-        """Decode batch b's files into pinned slot `slot`; returns the number of files."""
+    def _read_batch(self, b: int, slot: int):
+        """Decode batch b's files into pinned slot `slot` (no HIP calls: runs on the decoder
+        thread); returns (number of files, seconds)."""
+        import time
+        r0 = time.perf_counter()
         lo = b * self.B
         paths = self.paths[lo:lo + self.B]
         es = self.dtype.itemsize
@@ -120,41 +134,56 @@ class WavDay:
         st = self.h_st[slot].view(np.int64, self.B)
         st[:] = 0
         st[: len(paths)] = self.start_us[lo:lo + len(paths)]
-        return len(paths)
+        return len(paths), time.perf_counter() - r0
 
     def _upload(self, slot: int):
-        # the slot's previous batch (b - 2) has finished: run() downloaded its results before
-        # enqueuing the next batch, so the copy needs no fence behind the compute stream
+        # the slot's previous batch (b - S) has finished: run() downloaded its results before
+        # its slot was decoded into again, so the copy needs no fence behind the compute stream
         lib, h = self.ctx.lib, self.ctx.h
         _lib.check(lib.msd_memcpy_h2d_async(h, self.d_x[slot].ptr, self.h_x[slot].ptr, C.c_size_t(self.slot_bytes)))
         _lib.check(lib.msd_memcpy_h2d_async(h, self.d_st[slot].ptr, self.h_st[slot].ptr, C.c_size_t(self.B * 8)))
-        _lib.check(lib.msd_fence(h, 0))  # compute enqueued next waits for the upload
+        # compute enqueued from now on waits for this upload; compute already enqueued (batch
+        # b - 1) does not, so uploading b never delays b - 1
+        _lib.check(lib.msd_fence(h, 0))
+
+    def _set_lengths(self, nfiles: int):
+        if nfiles == self.B and not self._short:
+            return
+        lens = np.full(self.B, self.n, np.int64)
+        lens[nfiles:] = 0  # a short last batch: the slot's tail files get no samples
+        self.bp.d_len.upload(lens)
+        self.bp.d_nb.upload(np.where(lens > 0, self.bp.nb, 0).astype(np.int64))
+        self._short = nfiles < self.B
 
     def run(self):
         import time
         nbatch = (len(self.paths) + self.B - 1) // self.B
+        S = self.S
         t0 = time.perf_counter()
-        r0 = time.perf_counter()
-        nfiles = self._read_batch(0, 0)
-        t_read = time.perf_counter() - r0
+        # decode ahead: batch b into slot b % S as soon as that slot's batch b - S has computed
+        reads, sub = {}, [0]
+
+        def feed(last):  # submit the decodes of batches up to `last`
+            while sub[0] <= last and sub[0] < nbatch:
+                reads[sub[0]] = self.decoder.submit(self._read_batch, sub[0], sub[0] % S)
+                sub[0] += 1
+
+        feed(max(0, S - 2))
+        t_read = 0.0
+        nfiles, dt = reads.pop(0).result()
+        t_read += dt
         self._upload(0)
         out = []
         for b in range(nbatch):
-            slot = b % 2
-            if nfiles < self.B:  # a short last batch: the slot's tail files get no samples
-                lens = np.full(self.B, self.n, np.int64)
-                lens[nfiles:] = 0
-                nbs = np.where(lens > 0, self.bp.nb, 0).astype(np.int64)
-                self.bp.d_len.upload(lens)
-                self.bp.d_nb.upload(nbs)
+            slot = b % S
+            feed(b + S - 1)  # batch b + S - 1's slot held b - 1, whose detections were downloaded
+            self._set_lengths(nfiles)
             self.bp.run(x=self.d_x[slot], start_us=self.d_st[slot], clear_hist=(b == 0))
             nxt = 0
-            if b + 1 < nbatch:
-                _lib.check(self.ctx.lib.msd_copy_synchronize(self.ctx.h))  # the other pinned slot is free
-                r0 = time.perf_counter()
-                nxt = self._read_batch(b + 1, 1 - slot)  # overlaps batch b on the GPU
-                t_read += time.perf_counter() - r0
-                self._upload(1 - slot)
+            if b + 1 < nbatch:  # enqueue the next upload now: it runs right behind this one
+                nxt, dt = reads.pop(b + 1).result()
+                t_read += dt
+                self._upload((b + 1) % S)
             dets, counts, status, _ = self.bp.detections()  # waits for batch b
             out.extend(dets[:nfiles])
             nfiles = nxt

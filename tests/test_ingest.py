@@ -96,16 +96,24 @@ def test_wav_day_matches_single_file_drop_in(tmp_path):
         wav.write(p, 6000, x)
         paths.append(p)
         xs.append(x)
-    wd = ingest.WavDay(context(0), paths, batch_files=3, freq_band=(993, 1013), noise_band=(690, 710), n_fft=512)
-    dets, hist, info = wd.run()
-    assert len(dets) == 7 and info["files"] == 7
-    total = 0
-    for p, x, d in zip(paths, xs, dets):
+    refs = []
+    for x in xs:
         res = dsp.process_samples(x, 6000, 0.2, (993, 1013), (690, 710), 512, 4.0)
-        ref = [(round(r.t_start / 0.2), round(r.t_stop / 0.2), r.dB) for r in res.detections]
-        assert [(int(a["start"]), int(a["stop"]), float(a["db"])) for a in d] == ref
-        total += len(ref)
-    assert total > 0 and int(hist.sum()) == total
+        refs.append([(round(r.t_start / 0.2), round(r.t_stop / 0.2), r.dB) for r in res.detections])
+    total = sum(len(r) for r in refs)
+    assert total > 0
+    # batches of 3 (three slots: two full batches and a short one), 4 (two slots, short second)
+    # and 7 (one batch); each day run twice (the short batch's lengths must not leak into the
+    # next run's first batch)
+    for bf in (3, 4, 7):
+        wd = ingest.WavDay(context(0), paths, batch_files=bf, freq_band=(993, 1013), noise_band=(690, 710),
+                           n_fft=512)
+        for _ in range(2):
+            dets, hist, info = wd.run()
+            assert len(dets) == 7 and info["files"] == 7
+            for ref, d in zip(refs, dets):
+                assert [(int(a["start"]), int(a["stop"]), float(a["db"])) for a in d] == ref
+            assert int(hist.sum()) == total
 
 
 def test_iq_wav_file_rejects_mono(tmp_path):
