@@ -175,11 +175,10 @@ class BatchPipeline:
         self.d_band.download(band)
         self.d_noise.download(noise)
         win = hanning_sym(self.block_size)[: self.L]
-        self.decision_bounds = np.array([
-            M.decision_bound(M.delta_error_bound(band[i, : self.nb], noise[i, : self.nb], nfft=self.nfft, L=self.L,
-                                                 window=win, xmax=self.xmax[i], band=self.band_bins,
-                                                 noise=self.noise_bins), self.k_std)
-            for i in range(self.nfiles)])
+        err = M.delta_error_bounds(band[:, : self.nb], noise[:, : self.nb], nfft=self.nfft, L=self.L, window=win,
+                                   xmax=np.asarray(self.xmax, np.float64)[: self.nfiles], band=self.band_bins,
+                                   noise=self.noise_bins)
+        self.decision_bounds = M.decision_bounds(err, self.k_std)
         self.near_tie = np.isfinite(margin) & (margin <= self.decision_bounds)
         if self.near_tie.any():
             idx = np.nonzero(self.near_tie)[0]

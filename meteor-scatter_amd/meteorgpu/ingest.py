@@ -110,6 +110,11 @@ class WavDay:
         self.pool = ThreadPoolExecutor(max_workers=max(1, int(readers)))
         self.decoder = ThreadPoolExecutor(max_workers=1)  # one batch at a time, its files on `pool`
         self.bp.hist.base_us = int(self.base_us)
+        # max |x| per file for the near-tie bound (margin.py): the format's full scale for integer
+        # samples (a conservative bound, no pass over the samples), measured per file for float
+        self.full_scale = ({np.uint8: 255.0, np.int16: 32768.0, np.int32: 2.0 ** 31}.get(self.dtype.type)
+                           if self.dtype.kind in "iu" else None)
+        self.xmax = [np.full(self.B, self.full_scale or 0.0) for _ in range(self.S)]
         self._short = False  # d_len / d_nb hold a short last batch's lengths
 
     def _read_batch(self, b: int, slot: int):
@@ -129,6 +134,9 @@ class WavDay:
             _lib.check(lib.msd_wav_read(paths[i].encode(), 0, 0, self.n, dst, self.n * es, C.byref(info)))
             if info.frames != self.n or info.rate != self.fs or info.dtype != self.info.dtype:
                 raise ValueError(f"{paths[i]}: format differs from the batch's first file")
+            if self.full_scale is None:
+                x = self.h_x[slot].view(self.dtype, self.n, i * self.bp.n_pad * es)
+                self.xmax[slot][i] = float(np.max(np.abs(x))) if self.n else 0.0
 
         list(self.pool.map(one, range(len(paths))))
         st = self.h_st[slot].view(np.int64, self.B)
@@ -184,6 +192,7 @@ class WavDay:
                 nxt, dt = reads.pop(b + 1).result()
                 t_read += dt
                 self._upload((b + 1) % S)
+            self.bp.xmax[:] = self.xmax[slot]
             dets, counts, status, _ = self.bp.detections()  # waits for batch b
             out.extend(dets[:nfiles])
             nfiles = nxt

@@ -103,6 +103,26 @@ def delta_error_bound(band_db: np.ndarray, noise_db: np.ndarray, *, nfft: int, L
     return band_db_error(band_db, nb, dx) + band_db_error(noise_db, nn, dx)
 
 
+def delta_error_bounds(band_db: np.ndarray, noise_db: np.ndarray, *, nfft: int, L: int, window: np.ndarray,
+                       xmax: np.ndarray, band: tuple[int, int], noise: tuple[int, int]) -> np.ndarray:
+    """delta_error_bound for many files at once: band_db / noise_db [files, blocks], xmax [files]
+    (one vectorised pass instead of a Python loop over the files of a batch)."""
+    wsum = float(np.abs(np.asarray(window, dtype=np.float64)[:L]).sum())
+    nb = max(0, band[1] - band[0] + 1)
+    nn = max(0, noise[1] - noise[0] + 1)
+    bins = np.concatenate([np.arange(band[0], band[1] + 1), np.arange(noise[0], noise[1] + 1)])
+    s = np.asarray(xmax, dtype=np.float64).reshape(-1, 1) * wsum
+    dx = _chain(nfft, L, bins) * U * s
+    return band_db_error(band_db, nb, dx) + band_db_error(noise_db, nn, dx)
+
+
+def decision_bounds(delta_err: np.ndarray, k_std: float) -> np.ndarray:
+    """decision_bound of each row of delta_err [files, blocks]."""
+    e = np.asarray(delta_err, dtype=np.float64)
+    m = e.max(axis=1) if e.shape[1] else np.zeros(e.shape[0])
+    return (2.0 + abs(float(k_std))) * m * (1.0 + 1e-6)
+
+
 def decision_bound(delta_err: np.ndarray, k_std: float) -> float:
     """|delta - thr| at or below this can flip a decision (module docstring)."""
     m = float(np.max(delta_err)) if np.size(delta_err) else 0.0

@@ -114,6 +114,8 @@ def test_wav_day_matches_single_file_drop_in(tmp_path):
             for ref, d in zip(refs, dets):
                 assert [(int(a["start"]), int(a["stop"]), float(a["db"])) for a in d] == ref
             assert int(hist.sum()) == total
+            # the near-tie guard bounds with the int16 full scale (no pass over the samples)
+            assert (wd.bp.decision_bounds > 0).all() and not wd.bp.near_tie.any()
 
 
 def test_iq_wav_file_rejects_mono(tmp_path):

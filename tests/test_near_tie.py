@@ -169,3 +169,22 @@ def test_live_flag_on_constructed_near_tie():
     with pytest.warns(M.NearTieWarning):
         _, thr3, over3 = L.live_detect_ref(r2, 4000, 800, rcfg)
         LV.near_tie_check(r2, thr3, over3, span, 4000, cfg)
+
+
+def test_batched_bounds_equal_per_file_loop():
+    """delta_error_bounds / decision_bounds (BatchPipeline's one vectorised pass over a batch) equal
+    delta_error_bound / decision_bound file by file, empty bands and zero-amplitude files included"""
+    rng = np.random.default_rng(11)
+    F, nb, L = 6, 40, 1024
+    win = np.hanning(9600)[:L]
+    band = rng.uniform(-40.0, 60.0, (F, nb))
+    noise = rng.uniform(-40.0, 60.0, (F, nb))
+    band[2, 5] = -120.0  # E = 1e-12
+    xmax = np.array([4000.0, 32768.0, 1.0, 0.0, 123.0, 32767.0])
+    for bb, nn in (((170, 172), (118, 121)), ((170, 172), (0, -1)), ((0, -1), (0, -1))):
+        err = M.delta_error_bounds(band, noise, nfft=1024, L=L, window=win, xmax=xmax, band=bb, noise=nn)
+        got = M.decision_bounds(err, 4.0)
+        for i in range(F):
+            e1 = M.delta_error_bound(band[i], noise[i], nfft=1024, L=L, window=win, xmax=xmax[i], band=bb, noise=nn)
+            np.testing.assert_array_equal(err[i], e1)
+            assert got[i] == M.decision_bound(e1, 4.0)
