@@ -29,7 +29,12 @@ pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="g++ needed 
 
 @pytest.fixture(scope="module")
 def harness():
-    subprocess.run(["make", "-s", "-C", CSRC, "sanitize"], check=True, capture_output=True)
+    # one build at a time: pytest-xdist workers would otherwise exec a half-linked binary
+    import fcntl
+    os.makedirs(os.path.join(CSRC, "build"), exist_ok=True)
+    with open(os.path.join(CSRC, "build", ".sanitize.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", CSRC, "sanitize"], check=True, capture_output=True)
     return EXE
 
 
