@@ -138,7 +138,11 @@ class WavDay:
                 x = self.h_x[slot].view(self.dtype, self.n, i * self.bp.n_pad * es)
                 self.xmax[slot][i] = float(np.max(np.abs(x))) if self.n else 0.0
 
-        list(self.pool.map(one, range(len(paths))))
+        futs = [self.pool.submit(one, i) for i in range(len(paths))]
+        errs = [f.exception() for f in futs]  # every reader has stopped writing into the slot
+        err = next((e for e in errs if e is not None), None)
+        if err is not None:
+            raise err
         st = self.h_st[slot].view(np.int64, self.B)
         st[:] = 0
         st[: len(paths)] = self.start_us[lo:lo + len(paths)]
@@ -176,26 +180,40 @@ class WavDay:
                 reads[sub[0]] = self.decoder.submit(self._read_batch, sub[0], sub[0] % S)
                 sub[0] += 1
 
-        feed(max(0, S - 2))
         t_read = 0.0
-        nfiles, dt = reads.pop(0).result()
-        t_read += dt
-        self._upload(0)
         out = []
-        for b in range(nbatch):
-            slot = b % S
-            feed(b + S - 1)  # batch b + S - 1's slot held b - 1, whose detections were downloaded
-            self._set_lengths(nfiles)
-            self.bp.run(x=self.d_x[slot], start_us=self.d_st[slot], clear_hist=(b == 0))
-            nxt = 0
-            if b + 1 < nbatch:  # enqueue the next upload now: it runs right behind this one
-                nxt, dt = reads.pop(b + 1).result()
-                t_read += dt
-                self._upload((b + 1) % S)
-            self.bp.xmax[:] = self.xmax[slot]
-            dets, counts, status, _ = self.bp.detections()  # waits for batch b
-            out.extend(dets[:nfiles])
-            nfiles = nxt
+        try:
+            feed(max(0, S - 2))
+            nfiles, dt = reads.pop(0).result()
+            t_read += dt
+            self._upload(0)
+            for b in range(nbatch):
+                slot = b % S
+                feed(b + S - 1)  # batch b + S - 1's slot held b - 1, whose detections were downloaded
+                self._set_lengths(nfiles)
+                self.bp.run(x=self.d_x[slot], start_us=self.d_st[slot], clear_hist=(b == 0))
+                nxt = 0
+                if b + 1 < nbatch:  # enqueue the next upload now: it runs right behind this one
+                    nxt, dt = reads.pop(b + 1).result()
+                    t_read += dt
+                    self._upload((b + 1) % S)
+                self.bp.xmax[:] = self.xmax[slot]
+                dets, counts, status, _ = self.bp.detections()  # waits for batch b
+                out.extend(dets[:nfiles])
+                nfiles = nxt
+        except BaseException:
+            # a failed file (or an interrupt) leaves decodes in flight that write into the pinned
+            # slots: let them finish before the error propagates and the slots can be freed
+            for f in reads.values():
+                f.cancel()
+            for f in reads.values():
+                if not f.cancelled():
+                    try:
+                        f.result()
+                    except BaseException:
+                        pass
+            self.ctx.synchronize()
+            raise
         hist = self.bp.hour_counts()
         wall = time.perf_counter() - t0
         return out, hist, {"wall_s": wall, "read_s": t_read, "files": len(self.paths)}

@@ -118,6 +118,30 @@ def test_wav_day_matches_single_file_drop_in(tmp_path):
             assert (wd.bp.decision_bounds > 0).all() and not wd.bp.near_tie.any()
 
 
+@pytest.mark.gpu
+def test_wav_day_bad_file_raises_after_readers_stop(tmp_path):
+    """a file whose format differs from the first one fails the run with the file named; the
+    decodes still in flight finish before the error leaves run(), and the day runs again once the
+    file is fixed"""
+    from meteorgpu import ingest, wav
+    from meteorgpu.dsp import context
+    day = datetime.datetime(2025, 6, 1, 3, 0)
+    rng = np.random.default_rng(5)
+    paths = []
+    for i in range(7):
+        t = day + datetime.timedelta(minutes=i)
+        p = tmp_path / f"SDR_gqrx_{t:%Y%m%d}_{t:%H%M%S}_49969000.wav"
+        wav.write(p, 6000, rng.integers(-3000, 3000, 6000 * 20, dtype=np.int16))
+        paths.append(p)
+    good = paths[5].read_bytes()
+    wav.write(paths[5], 8000, rng.integers(-3000, 3000, 6000 * 20, dtype=np.int16))  # batch 2 of 3
+    wd = ingest.WavDay(context(0), paths, batch_files=2, freq_band=(993, 1013), noise_band=(690, 710), n_fft=512)
+    with pytest.raises(ValueError, match="format differs"):
+        wd.run()
+    paths[5].write_bytes(good)
+    dets, hist, info = wd.run()
+    assert len(dets) == 7 and info["files"] == 7
+
 def test_iq_wav_file_rejects_mono(tmp_path):
     """the I/Q entry point asserts a 2-channel file before touching the GPU"""
     import pytest as _pt
