@@ -50,9 +50,11 @@ for sub, name, kernel, match in ((tag, "stft", "stft1024_kernel<short, 0, true>"
 # per-dispatch durations of each workload's roofline kernel from the kernel trace: the stats
 # average includes the cold first (warm-up) dispatch; the timed steps' average is the figure
 # the bench line's live HIP-event timing reports under the profiler
+kt0 = last_json(f"{src}/kt.log")
+KW, KS = kt0.get("warmup", 1), kt0.get("steps", 5)
 lines = ["roofline kernel, per-dispatch durations (ms) from rocprofv3 --kernel-trace; the run is "
-         "bench.py --steps 5 --warmup 1: dispatch 1 is the warm-up, 2-6 the timed steps, 7 the step after "
-         "the timed region that times every kernel for the breakdown"]
+         f"bench.py --steps {KS} --warmup {KW}: dispatches 1-{KW} are the warm-up, {KW + 1}-{KW + KS} the timed "
+         f"steps, {KW + KS + 1} the step after the timed region that times every kernel for the breakdown"]
 for wl, key in (("", "stft1024_kernel"), ("_live", "welch_bands_kernel"), ("_c5", "cstft4096_kernel")):
     import csv
     rows = list(csv.DictReader(open(f"{src}/kt{wl}/kt_kernel_trace.csv")))
@@ -60,7 +62,7 @@ for wl, key in (("", "stft1024_kernel"), ("_live", "welch_bands_kernel"), ("_c5"
     b = last_json(f"{src}/kt{wl}.log")
     live = b["roofline"].get("kernel_ms")
     lines.append(f"{key} ({wl[1:] or 'c3'}): " + " ".join(f"{x:.3f}" for x in d) +
-                 f" | all {sum(d) / len(d):.3f} | timed steps {sum(d[1:6]) / max(1, len(d[1:6])):.3f}"
+                 f" | all {sum(d) / len(d):.3f} | timed steps {sum(d[KW:KW + KS]) / max(1, len(d[KW:KW + KS])):.3f}"
                  f" | bench live HIP events {live}")
 open(f"{dst}/{tag}_dispatches.txt", "w").write("\n".join(lines) + "\n")
 print("profiles updated for", tag)
