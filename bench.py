@@ -473,7 +473,17 @@ def dry_run(rank, world, files):
     rendezvous file, each publishes the digest it saw, and rank 0 checks they all agree."""
     import hashlib
     from meteorgpu import launch
+    if os.environ.get("MSD_DRYRUN_PID_DIR"):  # test hook: where the ranks' PIDs go (liveness checks)
+        with open(os.path.join(os.environ["MSD_DRYRUN_PID_DIR"], f"rank{rank}.pid"), "w") as fh:
+            fh.write(str(os.getpid()))
     uid = launch.share_bytes(rank, lambda: os.urandom(128))
+    if os.environ.get("MSD_DRYRUN_FAIL_RANK") == str(rank):
+        # test hook: this rank dies after the id rendezvous (where a real rank has its RCCL
+        # communicator up) while the others block waiting for it -- once every rank is up
+        pid_dir, t_end = os.environ.get("MSD_DRYRUN_PID_DIR"), time.monotonic() + 30
+        while pid_dir and len(os.listdir(pid_dir)) < world and time.monotonic() < t_end:
+            time.sleep(0.01)
+        sys.exit(7)
     launch.share_bytes(0, lambda: hashlib.sha1(uid).digest(), tag=f"seen{rank}")
     if rank != 0:
         return

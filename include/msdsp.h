@@ -330,7 +330,11 @@ int msd_stream_detect_local(msd_stream_plan *plan, int32_t exact_thresholds, msd
  * msd_stream_certificate returns their count, the smallest slack, the largest error zone (ed +
  * threshold bound) of any decision and up to cap of them as
  * (global frame, frame whose window gave the threshold, -1 = thr0).  Zero uncertain decisions:
- * the detections are the reference's. */
+ * the detections are the reference's.  msd_stream_certificate fails (MSD_ERR_INVALID) unless the
+ * plan's last full scan ran with certification on: msd_stream_set_certify invalidates the
+ * certificate until the next msd_stream_scan with reset 1 or 2 (or msd_stream_detect_local).
+ * msd_iq_delta64_dev: blocks of D = gcd(nperseg, hop) samples run as 16-lane Goertzel rows when D
+ * is a multiple of 64, else one lane per block (any D). */
 int msd_stream_set_certify(msd_stream_plan *plan, int32_t on);
 int msd_stream_error_buffers(msd_stream_plan *plan, double **ed, double **tail, double **head);
 int msd_stream_ed_sums(msd_stream_plan *plan, double *sum_ed, double *sum_ed2);

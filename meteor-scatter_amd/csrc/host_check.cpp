@@ -145,6 +145,12 @@ bool check_plan(const msd::RefinePlan &P, const std::vector<int64_t> &ranges, in
         why = "block geometry";
         return false;
     }
+    // block_kernel's assumptions (refine.hip): 16 lanes x D/16 samples loaded as aligned quads, so
+    // the row path needs D % 64 == 0; any other D must take the one-lane path
+    if (G.rows != (G.D % 64 == 0 ? 1 : 0) || (G.rows && (G.L * 16 != G.D || G.L % 4)) || (!G.rows && G.L != G.D)) {
+        why = "kernel path";
+        return false;
+    }
     if (K.nk < 0 || K.nk > msd::RF_MAXK || K.nb > msd::RF_MAXK / 2 || K.nn > msd::RF_MAXK / 2) {
         why = "bin counts";
         return false;
@@ -213,7 +219,7 @@ int cmd_refine(int argc, char **argv) {
         std::printf("bad %s\n", why.c_str());
         return 1;
     }
-    std::printf("ok %d %d %d %" PRId64 " %" PRId64 "\n", P.K.nk, P.G.D, P.G.R, P.nblocks, P.nframes);
+    std::printf("ok %d %d %d %" PRId64 " %" PRId64 " %d\n", P.K.nk, P.G.D, P.G.R, P.nblocks, P.nframes, P.G.rows);
     return 0;
 }
 

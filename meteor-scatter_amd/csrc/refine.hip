@@ -114,7 +114,7 @@ struct Quad<float> {
     }
 };
 
-// D >= 64: sixteen lanes per block (a row of the wave), lane L the D/16 consecutive samples from
+// D % 64 == 0 (RefineGeom::rows): sixteen lanes per block (a row of the wave), lane L the D/16 consecutive samples from
 // L D/16; one pass over the samples runs the Goertzel recurrence of NK bins (the nk needed ones,
 // padded with copies of bin 0 whose results are dropped: no per-bin branch in the loop), each
 // segment's DFT is rotated to the block origin with two table twiddles, and the row sums the 16
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void block_kernel(const T *__restrict__ x, Ref
     }
 }
 
-// D < 64: one lane per block (a direct DFT over its D samples)
+// D not a multiple of 64: one lane per block (a direct DFT over its D samples)
 template <typename T>
 __global__ __launch_bounds__(256) void block_small_kernel(const T *__restrict__ x, RefineGeom G, RefineBins K,
                                                           const int64_t *__restrict__ bstart,
@@ -372,7 +372,7 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     if (e == hipSuccess) e = hipEventRecord(ctx->rf_ev, st);
     if (e == hipSuccess) {
         KernelTimer timer(ctx, K_REFINE);
-        if (G.D >= 64) {  // rows of 16 lanes, S = D/16 (a multiple of 4) samples per lane
+        if (G.rows) {  // rows of 16 lanes, S = D/16 (a multiple of 4) samples per lane
             const unsigned grid = (unsigned)((nblocks + 15) / 16);
             auto go = [&](auto nkc, const auto *xp) {
                 constexpr int NKC = decltype(nkc)::value;

@@ -28,6 +28,8 @@ struct RefineBins {
 
 struct RefineGeom {
     int N, D, R, L;           // frame, block, blocks per frame, samples per Goertzel segment
+    int rows;                 // 1: block_kernel (D % 64 == 0: 16 lanes x D/16 samples, 16-B aligned quads);
+                              // 0: block_small_kernel (one lane per block, any D)
     int64_t hop;
     double scale;             // density: 1 / (fs sum w^2)
     double chain;             // our float64 rounding chain + the reference's, in units of u
@@ -103,7 +105,11 @@ inline int plan_refine(int nperseg, int64_t hop, double fs, int band_lo, int ban
     G.hop = hop;
     G.D = (int)std::gcd((int64_t)N, hop);
     G.R = N / G.D;
-    G.L = G.D >= 64 ? G.D / 16 : G.D;  // samples per Goertzel segment
+    // block_kernel runs 16 lanes of D/16 samples each and loads them four at a time (16-B quads at
+    // m D + n0): D must be a multiple of 64; any other D (e.g. N 1000, hop 500: D 500) takes the
+    // one-lane-per-block direct DFT
+    G.rows = G.D % 64 == 0 ? 1 : 0;
+    G.L = G.rows ? G.D / 16 : G.D;  // samples per Goertzel segment (direct products)
     // periodic Hann: sum w^2 = 3N/8 exactly; scipy's scale 1/(fs * sum(w^2)) from its float64 window
     {
         double sw = 0.0;
@@ -124,8 +130,8 @@ inline int plan_refine(int nperseg, int64_t hop, double fs, int band_lo, int ban
         const double sn = std::fabs(std::sin(2.0 * M_PI * km / N));
         gmax = std::max(gmax, std::min(sn > 0 ? 1.0 / sn : 1e300, (double)G.L));
     }
-    // the D < 64 path sums D direct products (D + 4); the Goertzel path 3 L Gmax + 8 and the 16-lane sum
-    const double own = G.D >= 64 ? 3.0 * G.L * gmax + 8.0 + 4.0 : (double)G.D + 4.0;
+    // the one-lane path sums D direct products (D + 4); the Goertzel path 3 L Gmax + 8 and the 16-lane sum
+    const double own = G.rows ? 3.0 * G.L * gmax + 8.0 + 4.0 : (double)G.D + 4.0;
     G.chain = own + (G.R + 4.0) + 8.0 + 4.0 * std::log2((double)N) + 11.0;
     if (nranges > (1 << 20)) return err(E_UNSUPPORTED, "too many ranges");
     // frame ranges -> block ranges, compact prefix counts

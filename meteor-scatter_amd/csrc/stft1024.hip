@@ -30,30 +30,10 @@
 namespace msd {
 namespace {
 
-#ifndef STFT_WO
-#define STFT_WO 4  // measured fastest: rows 0-255 after the first transposes, 256-512 after the second
-#endif
-// Where the previous tile's write-out (row groups j = 0..4, rows 128 j + tid / 8) is issued in the
-// loop: positions 0 before pass 1, 1 between the two frames' first transposes, 2 after them, 3
-// between the second transposes, 4 after them, 5 after pass 3.  Each row lists the split point
-// after which positions' groups start: group j goes to the first position p with j < cut[p].
-constexpr int k_wo_cut[][6] = {
-    {0, 0, 5, 5, 5, 5},  // 0: all after the first transposes (rounds 1-3)
-    {0, 0, 0, 0, 5, 5},  // 1: all after the second transposes
-    {0, 0, 3, 3, 5, 5},  // 2: 0-2 after the first, 3-4 after the second transposes
-    {5, 5, 5, 5, 5, 5},  // 3: all before pass 1
-    {0, 0, 2, 2, 5, 5},  // 4: 0-1 / 2-4
-    {0, 1, 2, 3, 5, 5},  // 5: one group at each of positions 1-3, the rest after the second transposes
-    {0, 0, 2, 2, 4, 5},  // 6: 0-1 / 2-3 / 4 after pass 3
-    {0, 2, 2, 4, 5, 5},  // 7: 0-1 between the first transposes, 2-3 between the second, 4 after
-    {0, 0, 3, 3, 3, 5},  // 8: 0-2 after the first transposes, 3-4 after pass 3
-    {1, 1, 2, 2, 5, 5},  // 9: 0 before pass 1, 1 after the first transposes, 2-4 after the second
-    {0, 0, 0, 0, 0, 5},  // 10: all after pass 3
-    {0, 0, 1, 1, 5, 5},  // 11: 0 / 1-4
-    {1, 1, 1, 1, 5, 5},  // 12: 0 before pass 1, 1-4 after the second transposes
-};
-constexpr int wo_lo(int p) { return p == 0 ? 0 : k_wo_cut[STFT_WO][p - 1]; }
-constexpr int wo_hi(int p) { return k_wo_cut[STFT_WO][p]; }
+// The previous tile's write-out (row groups j = 0..4, rows 128 j + tid / 8) leaves in two bursts:
+// groups [0, F_WO_SPLIT) after the first transposes, [F_WO_SPLIT, 5) after the second ones (the
+// placement measured fastest among 13; the A/B variants live in tools/)
+constexpr int F_WO_SPLIT = 2;
 constexpr int F_NW = 16;                  // waves per workgroup (4 per SIMD)
 constexpr int F_TT = 32;                  // frames per tile
 constexpr int F_K = 513;                  // one-sided bins
@@ -344,12 +324,6 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     };
     FileCur prev = cur;
     bool have_prev = false;
-    // the previous tile's write-out, row groups [wo_lo, wo_hi) at loop position P
-#define WO_AT(P)                                                                                            \
-    do {                                                                                                    \
-        if constexpr (wo_hi(P) > wo_lo(P))                                                                   \
-            if (have_prev) write_out(prev, std::integral_constant<int, wo_lo(P)>{}, std::integral_constant<int, wo_hi(P)>{}); \
-    } while (0)
     const float hs = vgpr_f(0.70710678118654752440f);  // sqrt(1/2) of the DFT8s, in a VGPR
 
     for (int64_t tl = tb; tl < te; ++tl) {
@@ -418,7 +392,6 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             b_ok = nxt.ti * F_TT + wcol + 1 < nxt.nfr;
         }
 
-        WO_AT(0);  // before pass 1
         // ---- pass 1 (Ns = 1): out[8 l + r].  One scratch per wave: frame A's transpose is
         // read back before frame B's is written (LDS executes a wave's accesses in order)
         dft8_windowed(v[0], v[0], wv, hs);
@@ -433,13 +406,12 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[q][r] = scr[phys(l + 64 * r)];
             wave_sync();
-            if (q == 0) WO_AT(1);
         }
         // the previous tile's write-out, split between here (after the first transposes) and after
         // the second ones: its LDS reads and stores overlap the other waves' arithmetic in two
         // smaller bursts instead of one (A/B: all at the loop top +2 %, all here 0, half here and
         // half after the second transposes -3.4 %)
-        WO_AT(2);
+        if (have_prev) write_out(prev, std::integral_constant<int, 0>{}, std::integral_constant<int, F_WO_SPLIT>{});
         // ---- pass 2 (Ns = 8): out[64 (l>>3) + (l&7) + 8 r]
         const int o2 = 64 * (l >> 3) + (l & 7);
         float2 tw3_1;  // the first pass-3 twiddle shares the pass-2 table's last ds_read_b128
@@ -468,9 +440,8 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[q][r] = scr[phys(pi + 64 * r)];
             wave_sync();
-            if (q == 0) WO_AT(3);
         }
-        WO_AT(4);
+        if (have_prev) write_out(prev, std::integral_constant<int, F_WO_SPLIT>{}, std::integral_constant<int, 5>{});
         // ---- pass 3 (Ns = 64): butterfly pi(l) → lane holds Z[pi(l) + 64 r]
         {
             float2 w[8];  // pass-3 twiddles r = 1..7 at 19..25
@@ -489,7 +460,6 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         }
         dft8(v[0], hs);
         dft8(v[1], hs);
-        WO_AT(5);
         // ---- post: X' = 2X = (Z + conj Zm) + W^k (-i)(Z - conj Zm), Zm = Z[(512 - k) mod 512],
         // and from the same e, o the mirror bin X'[512 - k] = conj(e - W^k o).  Lane l owns the
         // four pairs (k = pi(l) + 64 r, 512 - k), r = 0..3: Zm sits in lane l^1, register 7-r

@@ -85,6 +85,11 @@ struct msd_stream_plan {
     int nleaf = 0;
     double thr0 = 0;
     bool scanned = false;
+    // every segment's certificate entries (d_ucnt, d_slack) come from a scan that ran with
+    // certification on: set by a scan over all segments with certify on, cleared by
+    // msd_stream_set_certify and by any scan with it off (a stale or never-written certificate
+    // must not read as "certified")
+    bool cert_valid = false;
     bool want_exact = true;  // msd_stream_set_exact_thresholds
     int32_t listed = -1;     // decisions only: frames listed by the last msd_stream_scan (host copy)
     // pinned host block for the small per-step readbacks (counters, exit state, margins, chunk
@@ -1441,6 +1446,7 @@ int msd_stream_fresh(msd_stream_plan *p) {
 int msd_stream_set_certify(msd_stream_plan *p, int32_t on) {
     if (!p) return fail(MSD_ERR_INVALID, "msd_stream_set_certify: null plan");
     p->certify = on != 0;
+    p->cert_valid = false;  // the next full scan writes the certificate
     return MSD_OK;
 }
 
@@ -1499,7 +1505,8 @@ int msd_stream_certificate(msd_stream_plan *p, int64_t *uncertain, double *min_s
     *max_zone = 0.0;
     if (!p->certify) return fail(MSD_ERR_INVALID, "msd_stream_certificate: certification is off");
     if (p->nseg == 0) return MSD_OK;
-    if (!p->scanned) return fail(MSD_ERR_INVALID, "msd_stream_certificate: call msd_stream_scan first");
+    if (!p->scanned || !p->cert_valid)
+        return fail(MSD_ERR_INVALID, "msd_stream_certificate: call msd_stream_scan with certification on first");
     DeviceGuard g(p->ctx->device);
     hipStream_t st = p->ctx->stream;
     // pinned staging (grown once): counts and slacks in one round trip, the lists in a second one
@@ -1583,6 +1590,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
     DeviceGuard g(p->ctx->device);
     hipStream_t st = p->ctx->stream;
     int32_t nround = 0;
+    const int32_t scan_mode = !p->scanned ? 1 : (reset == 1 || reset == 2 ? reset : 0);
     if (p->nseg == 0) {
         if (exit_state) *exit_state = *entry;
         if (rounds) *rounds = 0;
@@ -1591,9 +1599,8 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
     {  // entry states and active flags set on the device (kernel arguments: no host staging, no sync)
         SState e0;
         std::memcpy(&e0, entry, sizeof(SState));
-        const int32_t mode = !p->scanned ? 1 : (reset == 1 || reset == 2 ? reset : 0);
         hipLaunchKernelGGL(scan_entry_kernel, dim3((unsigned)((p->nseg + 2 + 255) / 256)), dim3(256), 0, st, st_in(p),
-                           p->d_active, p->nseg, e0, thr0, p->terr0, mode);
+                           p->d_active, p->nseg, e0, thr0, p->terr0, scan_mode);
         MSD_HIP(hipGetLastError());
     }
     p->thr0 = thr0;
@@ -1662,6 +1669,10 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
         MSD_HIP(hipMemsetAsync(p->d_active, 0, sizeof(int32_t) * p->nseg, st));
     }
     p->scanned = true;
+    // mode 1 / 2 scanned every segment: with certification on, every segment's entries are current;
+    // mode 0 re-scans some and keeps the others' (valid only if they were)
+    if (!p->certify) p->cert_valid = false;
+    else if (scan_mode != 0) p->cert_valid = true;
     if (exit_state) std::memcpy(exit_state, &ex, sizeof(SState));
     if (rounds) *rounds = nround;
     return MSD_OK;

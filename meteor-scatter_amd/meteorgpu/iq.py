@@ -154,21 +154,24 @@ class IQShardDetector:
     """One rank's time shard of an I/Q stream on the GPU: spectrogram (frame-major, kept in HBM) →
     per-frame band delta written straight into the stream plan → detector over the whole stream.
 
-    Certification (``certify``; off by default here, on in proc_iq_samples / proc_iq_wav_file): the
-    spectrogram kernel also writes each frame's energy,
+    Certification (``certify``, on by default, as in proc_iq_samples / proc_iq_wav_file; the
+    uncertified fast path is ``certify=False``): the spectrogram kernel also writes each frame's energy,
     the band delta kernel a bound on |delta - delta_ref| against the float64 reference (scipy's
     spectrogram of complex128 input), and every decision of the detector is checked against its
     bounds (include/msdsp.h, msd_stream_set_certify).  ``detect(exact_decisions=True)`` then
     recomputes in float64 (msd_iq_delta64_dev, from the samples) the delta of every frame an
     uncertain decision depends on -- the frame itself and the window its threshold comes from -- and
     runs the detector again, until no decision is uncertain (or only float64-level near ties are
-    left, flagged as ``near_tie``).  The detections are then the float64 reference's."""
+    left, flagged as ``near_tie``).  The detections are then the float64 reference's.  Last, the
+    frames of every detection are made float64 too (the same refinement) and the dB means
+    (main.py:501-502, np.mean over delta[start:stop]) recomputed over them, so the CSV's dB column
+    is the float64 reference's within the refinement's ~1e-12 dB bound, not the fp32 path's."""
 
     def __init__(self, ctx: _lib.Context, n_samples_total: int, fs, nperseg, noverlap, freq_band, noise_band,
                  threshold_std_factor=4.0, flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                  threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                  threshold_fixed_init_duration_sec=10, rank: int = 0, world: int = 1, dtype=np.int16,
-                 seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = False):
+                 seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = True):
         """chunk_frames: keep only that many frames of spectrogram in HBM and stream the shard through
         it (``process_host``); the detector still sees the whole shard's delta.  A 24 h 192 kHz
         stream (66 GB of int16 I/Q, 265 GB of spectrogram) then runs on one GPU."""
@@ -253,20 +256,33 @@ class IQShardDetector:
                                    self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T,
                                    etot=etot, ed=ed)
 
-    MAX_REFINE = 8
+    MAX_REFINE = 8  # refinement rounds before giving up (refine_budget_exhausted)
 
     def detect(self, comm=None, thresholds: bool = True, exact_decisions: bool = True) -> _stream.StreamResult:
         """The detector over the whole stream (every rank gets the same result).  Certifying, each
-        decision is checked against its error bounds; exact_decisions refines the uncertain ones
-        (class docstring)."""
+        decision is checked against its error bounds; exact_decisions refines the uncertain ones,
+        then the detections' own frames (class docstring)."""
         comm = comm or _stream.LocalComm()
-        refined, first, passes = 0, None, 0
-        for _ in range(self.MAX_REFINE + 1):
-            res = _stream.StreamDetector(self.ops, comm, self.adaptive, self.k, self.W, self.F0).run(thresholds)
+        refined, first, passes, exhausted, db_frames = 0, None, 0, False, 0
+        while True:
+            res = self._detector(comm).run(thresholds)
             passes += 1
             if first is None:
                 first = res.uncertain
-            if not self.certify or not exact_decisions or res.certified:
+            if not self.certify or not exact_decisions:
+                break
+            if res.certified:
+                # the detections' own frames in float64 (the CSV's dB column); with the thresholds
+                # output one more pass, so that the thresholds, the delta and the dB means agree
+                n = self._refine_detections(res)
+                db_frames += n
+                if n and thresholds and passes <= self.MAX_REFINE:
+                    continue
+                if n:
+                    res.detections["db"] = self._detector(comm).db_means(res.detections, refresh_halos=True)
+                break
+            if passes > self.MAX_REFINE:  # refined MAX_REFINE times, still uncertain: reported, not a tie
+                exhausted = True
                 break
             need = self._dependencies(res.uncertain_frames)
             if not need:  # every uncertain decision already reads float64 values: a float64 near tie
@@ -274,11 +290,35 @@ class IQShardDetector:
             self._refined = _merge(self._refined + need)
             refined += sum(b - a for a, b in need)
         if self.certify:
-            res.refined_delta_frames = refined
-            res.near_tie = not res.certified
+            if exact_decisions and not res.certified:  # a near tie / exhausted budget: the dB still float64
+                n = self._refine_detections(res)
+                if n:
+                    db_frames += n
+                    res.detections["db"] = self._detector(comm).db_means(res.detections, refresh_halos=True)
+            res.refined_delta_frames = refined + db_frames
+            res.db_refined_frames = db_frames
+            res.near_tie = not res.certified and not exhausted
+            res.refine_budget_exhausted = exhausted
             res.uncertain_initial = first
             res.detector_passes = passes
         return res
+
+    def _detector(self, comm) -> _stream.StreamDetector:
+        return _stream.StreamDetector(self.ops, comm, self.adaptive, self.k, self.W, self.F0)
+
+    def _refine_detections(self, res) -> int:
+        """float64 delta for every frame of every detection not refined yet (main.py:501-502 takes
+        np.mean(delta_power[start:stop]) over them); returns the frames refined.  Every rank holds
+        the same detections and refined ranges and refines its own part."""
+        dets = res.detections
+        if dets is None or len(dets) == 0:
+            return 0
+        need = _subtract(_merge(zip(dets["start"], dets["stop"])), self._refined)
+        if not need:
+            return 0
+        self._refine_local(need)
+        self._refined = _merge(self._refined + need)
+        return sum(b - a for a, b in need)
 
     def _dependencies(self, uncertain) -> list:
         """global frame ranges the uncertain decisions (frame, threshold source) depend on, and

@@ -156,11 +156,15 @@ def spawn(argv: list[str], nprocs: int, env: dict | None = None, poll_s: float =
             if p.poll() is None:
                 p.kill()
                 p.wait()
-        for tag in ("rccl",):
-            try:
-                os.unlink(os.path.join(_rdzv_dir(), f"msd_rdzv_{base['MSD_RDZV_KEY']}_{tag}.bin"))
-            except FileNotFoundError:
-                pass
+        # every rendezvous file of this launch (the RCCL id and any other tag, or a rank's
+        # half-written temporary): a failed job leaves none behind
+        prefix = f"msd_rdzv_{base['MSD_RDZV_KEY']}_"
+        for name in os.listdir(_rdzv_dir()):
+            if name.startswith(prefix):
+                try:
+                    os.unlink(os.path.join(_rdzv_dir(), name))
+                except FileNotFoundError:
+                    pass
     return rc
 
 

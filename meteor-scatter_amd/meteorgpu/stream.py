@@ -151,6 +151,8 @@ class StreamResult:
     near_tie: bool = False          # uncertain decisions left after refinement (float64 near ties)
     uncertain_initial: int = 0      # uncertain decisions of the first pass (before any refinement)
     detector_passes: int = 1        # detector runs (1 + refinement rounds)
+    db_refined_frames: int = 0      # detection frames made float64 for the dB means (exact decisions)
+    refine_budget_exhausted: bool = False  # uncertain decisions left after MAX_REFINE refinements
 
 
 class StreamDetector:
@@ -265,6 +267,24 @@ class StreamDetector:
                 entry = exits[r - 1]
                 exit_, _ = ops.scan(thr0, entry, 0)
 
+    def db_means(self, dets: np.ndarray, refresh_halos: bool = False) -> np.ndarray:
+        """np.mean dB of every detection (main.py:422-423, :501-502), computed by the rank whose
+        shard holds the run's start (its head halo covers a run into the next shards) and
+        allgathered.  refresh_halos: the delta of other ranks' frames changed since the halo
+        exchange (float64 refinement): exchange them again first."""
+        ops, comm = self.ops, self.comm
+        if refresh_halos and comm.world > 1:
+            self.exchange_halos()
+        lo, hi = ops.frame0, ops.frame0 + ops.n_local
+        mine = (dets["start"] >= lo) & (dets["start"] < hi)
+        db_local = ops.db(dets[mine])["db"] if mine.any() else np.zeros(0)
+        db_all = np.full(len(dets), np.nan)
+        for g in comm.allgather(np.concatenate([np.flatnonzero(mine).astype(np.int64),
+                                                np.asarray(db_local, np.float64).view(np.int64)])):
+            m = g.size // 2  # the owner's detection indices, then their dB bits
+            db_all[g[:m]] = g[m:].view(np.float64)
+        return db_all
+
     def run(self, thresholds: bool = True) -> StreamResult:
         ops, comm = self.ops, self.comm
         if ops.n_total == 0:
@@ -310,16 +330,7 @@ class StreamDetector:
             dets["stop"][-1] = ops.n_total - 1  # burst_stops gets len-1 (main.py:414-415)
             if dets["stop"][-1] - dets["start"][-1] <= 0:
                 raise AssertionError("Detection duration must be greater than 0")  # main.py:437
-        # dB means: the rank whose shard holds the run's start
-        lo, hi = ops.frame0, ops.frame0 + ops.n_local
-        mine = (dets["start"] >= lo) & (dets["start"] < hi)
-        db_local = ops.db(dets[mine])["db"] if mine.any() else np.zeros(0)
-        db_all = np.full(len(dets), np.nan)
-        for g in comm.allgather(np.concatenate([np.flatnonzero(mine).astype(np.int64),
-                                                np.asarray(db_local, np.float64).view(np.int64)])):
-            m = g.size // 2  # the owner's detection indices, then their dB bits
-            db_all[g[:m]] = g[m:].view(np.float64)
-        dets["db"] = db_all
+        dets["db"] = self.db_means(dets)
         thr = None if not thresholds else (ops.thresholds() if self.adaptive else np.array([thr0]))
         return self._certified(StreamResult(dets, thr0, thr, margin, rounds, refined))
 

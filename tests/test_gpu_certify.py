@@ -163,8 +163,8 @@ def test_constructed_near_ties_decide_as_the_oracle():
     dets, _, _, r = iq.proc_iq_samples(i, q, FS, BAND, NOISE, **KW)
     assert r.certified and not r.near_tie and r.refined_delta_frames > 0 and r.detector_passes >= 2
     assert [(d.t_start, d.t_stop) for d in dets] == [(x[0], x[1]) for x in rdets]
-    for d, x in zip(dets, rdets):
-        assert abs(d.dB - x[3]) < 1e-4
+    for d, x in zip(dets, rdets):  # the detections' frames refined: the float64 bar
+        assert abs(d.dB - x[3]) < 1e-9, (d.dB, x[3])
 
 
 def test_ordinary_stream_certifies_and_matches():
@@ -173,6 +173,8 @@ def test_ordinary_stream_certifies_and_matches():
     rdets, _, _, _, _ = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - HOP, **KW)
     assert r.certified and [(d.t_start, d.t_stop) for d in dets] == [(x[0], x[1]) for x in rdets]
     assert 0 < r.decision_bound < 0.1 and r.min_slack > 0
+    assert r.db_refined_frames > 0 and not r.refine_budget_exhausted
+    assert max(abs(d.dB - x[3]) for d, x in zip(dets, rdets)) < 1e-9
 
 
 def test_certification_off_is_the_old_path():
@@ -204,8 +206,9 @@ def test_sharded_certification_matches_oracle():
     def body(r, comm):
         ctx = _lib.Context(0)
         try:
+            # the default constructor certifies (the N-GPU worker of INTEGRATION.md §3)
             det = iq.IQShardDetector(ctx, n, FS, N, N - HOP, BAND, NOISE, 4.0, True, rank=r, world=3, seg_len=512,
-                                     dtype=buf.dtype, certify=True, **KW)
+                                     dtype=buf.dtype, **KW)
             det.upload(buf[2 * det.s0: 2 * det.s1])
             det.spectrogram_and_delta()
             res = det.detect(comm, thresholds=False)
@@ -220,6 +223,8 @@ def test_sharded_certification_matches_oracle():
     for r in res:
         assert r.certified and not r.near_tie and r.uncertain_initial >= len(placed) and r.refined_delta_frames > 0
         assert [(int(a) * bs, int(b) * bs) for a, b, _ in r.detections] == want
+        # dB over float64 frames refined by the ranks holding them, through refreshed halos
+        assert np.max(np.abs(r.detections["db"] - np.array([x[3] for x in rdets]))) < 1e-9
     assert len({(r.refined_delta_frames, r.uncertain_initial, r.detector_passes) for r in res}) == 1
 
 

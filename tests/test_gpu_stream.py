@@ -4,8 +4,10 @@ against the oracle of dsp/src/main.py:396-522 over the whole stream.
 Bars: run bounds, dB means, every threshold and the global threshold bit-exact on identical delta
 (float64, numpy's pairwise order); the I/Q band delta within DELTA_TOL dB of the float64 scipy
 spectrogram (the spectrogram is float32 on the device: <= 1e-5 relative per bin); end to end on
-I/Q the same detections as the oracle (the test asserts the oracle's margin to its thresholds
-exceeds the delta tolerance, so identical decisions are required, not lucky)."""
+I/Q (proc_iq_samples: every decision certified against the float64 reference, tests/
+test_gpu_certify.py) the same detections as the oracle, and the CSV's dB column within DB_TOL of
+the oracle's (the detections' frames are recomputed in float64 before the means), the t / UTC
+columns string-equal."""
 import numpy as np
 import pytest
 
@@ -15,7 +17,8 @@ from test_stream_protocol import make_delta, oracle
 
 pytestmark = pytest.mark.gpu
 
-DELTA_TOL = 1e-4  # dB
+DELTA_TOL = 1e-4  # dB, the fp32 spectrogram path's delta against scipy's float64 one
+DB_TOL = 1e-9     # dB, the CSV's dB column (float64 detection frames) against the oracle's
 
 
 def _ctx():
@@ -158,10 +161,13 @@ def test_iq_end_to_end(seed, adaptive):
     rdets, rthr, _, _, rdelta = Q.proc_iq_ref(i, q, 192000, (950, 1050), (-3050, -2950), **kw)
     assert delta.shape == rdelta.shape
     assert np.max(np.abs(delta - rdelta)) < DELTA_TOL
-    rt = np.asarray(rthr) if adaptive else rthr
-    assert np.nanmin(np.abs(rdelta - rt)) > 10 * DELTA_TOL  # decisions are not near-ties
+    assert res.certified and not res.near_tie  # every decision proven to be the float64 reference's
     assert [(d.t_start, d.t_stop) for d in dets] == [(r[0], r[1]) for r in rdets]
-    assert np.allclose([d.dB for d in dets], [r[3] for r in rdets], rtol=0, atol=DELTA_TOL)
+    assert np.max(np.abs(np.array([d.dB for d in dets]) - [r[3] for r in rdets])) < DB_TOL
+    inside = np.zeros(delta.size, bool)
+    for r in rdets:  # the detections' frames are float64: within the refinement's bound of the oracle
+        inside[int(round(r[0] * 192000 / 1024)): int(round(r[1] * 192000 / 1024))] = True
+    assert res.db_refined_frames > 0 and np.max(np.abs(delta - rdelta)[inside]) < DB_TOL
     # on the device's own delta the detector is bit-exact with the oracle's
     bs = 1024 / 192000
     from oracle import dsp_oracle as O
@@ -231,7 +237,7 @@ def test_iq_half_hour_sharded_matches_whole():
             ctx = _lib.Context(0)
             try:
                 det = iq.IQShardDetector(ctx, n, fs, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
-                                         rank=r, world=world)
+                                         rank=r, world=world, certify=False)
                 det.upload(buf[2 * det.s0: 2 * det.s1])
                 det.spectrogram_and_delta()
                 res = det.detect(comm, thresholds=thresholds)
@@ -283,7 +289,7 @@ def test_iq_day_eight_shards_chunked_matches_whole():
             ctx = _lib.Context(0)
             try:
                 det = iq.IQShardDetector(ctx, n, fs, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
-                                         rank=r, world=world, chunk_frames=1 << 19)
+                                         rank=r, world=world, chunk_frames=1 << 19, certify=False)
                 assert det.W == 22500
                 det.process_source(lambda a, b: stream(det.s0 + a, det.s0 + b))
                 res = det.detect(comm, thresholds=False)
@@ -344,8 +350,10 @@ def test_iq_dc_band_float32_global():
 
 
 def test_iq_csv_matches_oracle(tmp_path):
-    """proc_iq_samples writes the reference's detection CSV (main.py:640-658) byte for byte as the
-    oracle does from its own detections, UTC columns included"""
+    """proc_iq_samples writes the reference's detection CSV (main.py:640-658): against the CSV the
+    oracle writes from its OWN detections and dB values, the header and the t_start / t_stop /
+    dur_s / utc columns are string-equal row for row and the dB column is within DB_TOL"""
+    import csv
     import datetime
     from meteorgpu import iq, synth
     from oracle import dsp_oracle as O
@@ -358,10 +366,15 @@ def test_iq_csv_matches_oracle(tmp_path):
     dets, *_ = iq.proc_iq_samples(i, q, 192000, (950, 1050), (-3050, -2950), out_csv_file=str(out), **kw)
     rdets, *_ = Q.proc_iq_ref(i, q, 192000, (950, 1050), (-3050, -2950), **kw)
     ref = tmp_path / "ref.csv"
-    # the dB column is compared within DELTA_TOL elsewhere; here the device's dB values stand in
-    O.write_csv_ref([(r[0], r[1], r[2], d.dB, r[4], r[5]) for r, d in zip(rdets, dets)], str(ref))
+    O.write_csv_ref(rdets, str(ref))
     assert len(dets) == len(rdets) > 0
-    assert out.read_bytes() == ref.read_bytes()
+    got, want = out.read_bytes().split(b"\r\n"), ref.read_bytes().split(b"\r\n")
+    assert len(got) == len(want) and got[0] == want[0]  # rows and header
+    rows = list(csv.DictReader(open(out, newline=""))), list(csv.DictReader(open(ref, newline="")))
+    for g, w in zip(*rows):
+        for col in ("t_start", "t_stop", "dur_s", "utc_start", "utc_stop"):
+            assert g[col] == w[col], (col, g, w)
+        assert abs(float(g["dB"]) - float(w["dB"])) < DB_TOL, (g["dB"], w["dB"])
 
 
 def test_capacity_and_halo_errors_are_loud():

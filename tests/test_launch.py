@@ -21,8 +21,9 @@ def _run(cmd, env=None, timeout=120):
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e, cwd=ROOT)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_bench_spawns_n_ranks(n, tmp_path):
+    """N = 8 is the driver's full-node SCALE run: eight interpreters, one rendezvous"""
     r = _run([sys.executable, BENCH, "--gpus", str(n), "--dry-run"], env={"MSD_RDZV_DIR": str(tmp_path)})
     assert r.returncode == 0, r.stderr
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -106,3 +107,27 @@ def test_rdzv_key_restart_and_single_node(monkeypatch):
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
     with pytest.raises(RuntimeError, match="single-node"):
         launch.rdzv_key()
+
+
+def test_rank_dying_after_init_fails_the_job(tmp_path):
+    """a rank that exits after the communicator rendezvous (the others blocked waiting for it, as
+    in a collective) makes bench.py's parent exit with its code well within the rendezvous
+    timeout, and every sibling rank is terminated and reaped (spawn starts children; nothing
+    re-execs)"""
+    import time
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    t0 = time.monotonic()
+    r = _run([sys.executable, BENCH, "--gpus", "4", "--dry-run"],
+             env={"MSD_RDZV_DIR": str(tmp_path), "MSD_DRYRUN_FAIL_RANK": "2", "MSD_DRYRUN_PID_DIR": str(pids)},
+             timeout=100)
+    assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
+    assert time.monotonic() - t0 < 60  # not the 120 s rendezvous timeout of the blocked ranks
+    got = sorted(pids.iterdir())
+    assert len(got) == 4
+    for f in got:
+        pid = int(f.read_text())
+        assert pid != os.getpid()
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)  # gone (spawn waited for it: no zombie left either)
+    assert not [p for p in tmp_path.iterdir() if p.name.startswith("msd_rdzv_")]  # rendezvous cleaned up

@@ -165,6 +165,12 @@ def test_refine_plan_under_sanitizers(harness):
     assert run(harness, "refine", 4096, 1024, 21, 22, -65, -63, 10 ** 6, 0, 10, 40, 90).split()[1:4] == ["9", "1024", "4"]
     # a hop that is not a power of two (blocks of gcd(4096, 1000) = 8 samples)
     assert run(harness, "refine", 4096, 1000, 21, 22, -65, -63, 10 ** 6, 3, 9).split()[2:4] == ["8", "512"]
+    # the 16-lane Goertzel rows only for D % 64 == 0: D = 1024 rows, D = 500 (N 1000,
+    # hop 500) and D = 96 (N 192, hop 96) the one-lane direct path
+    assert run(harness, "refine", 4096, 1024, 21, 22, -65, -63, 10 ** 6, 0, 10).split()[6] == "1"
+    for n, hop, d in ((1000, 500, "500"), (192, 96, "96"), (4096, 2560, "512")):
+        out = run(harness, "refine", n, hop, 3, 4, -9, -7, 10 ** 5, 0, 10).split()
+        assert out[0] == "ok" and out[2] == d and out[6] == ("1" if int(d) % 64 == 0 else "0"), out
     # refused, not crashed: overlapping ranges, a band outside the spectrum, frames past the samples
     assert run(harness, "refine", 4096, 1024, 21, 22, -65, -63, 10 ** 6, 0, 10, 5, 20).startswith("err")
     assert run(harness, "refine", 4096, 1024, 21, 5000, -65, -63, 10 ** 6, 0, 10).startswith("err")
