@@ -40,6 +40,9 @@ NOISE = (2950.0, 3050.0)  # far from the ping: the 48 kHz crop leaks into near b
 NPERSEG, NOVERLAP = 1024, 512
 C5_FS, C5_N, C5_HOP, C5_SECONDS = 192000, 4096, 1024, 3 * 3600
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+# C5 decision modes: (certify, delta source, exact decisions) -- meteorgpu.iq.IQShardDetector
+C5_MODES = {"exact": (True, "auto", True), "off": (False, "fp32", False), "flag": (True, "fp32", False),
+            "refine": (True, "fp32", True)}
 POOL = 16              # distinct synthetic recordings, replicated over the batch
 
 
@@ -64,11 +67,13 @@ def parse():
                     "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 run appended to the line (key \"c5\")")
-    ap.add_argument("--c5-mode", choices=("all", "off", "flag", "exact"), default="all",
-                    help="C5 decisions: off = the streaming detector's default (no certification: the reference's "
-                         "work); flag = every decision certified against the float64 reference, uncertain ones "
-                         "reported; exact = the uncertain ones recomputed in float64 (proc_iq_samples' default); "
-                         "all = the line on 'off', plus timed 'flag' and 'exact' passes under \"certification\"")
+    ap.add_argument("--c5-mode", choices=("all",) + tuple(C5_MODES), default="all",
+                    help="C5 decisions: exact = the drop-in default (proc_iq_samples): every frame's delta in "
+                         "float64 from the samples (exact integer DFT on the matrix cores), every decision "
+                         "certified against the float64 reference; off = fp32 spectrogram band sums, uncertified; "
+                         "flag = the same certified, uncertain decisions reported; refine = flag + the uncertain "
+                         "ones and every detection's frames recomputed in float64 (round 3's certified path); "
+                         "all = the line on 'exact', plus the other modes timed under \"modes\"")
     ap.add_argument("--shard-day", action="store_true",
                     help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
                          "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "
@@ -272,10 +277,11 @@ def run_c5(a, ctx, job, rank, world):
     from meteorgpu import _lib, iq, stream, synth
     shard = int(C5_FS * a.c5_seconds)
     n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
-    head_mode = "off" if a.c5_mode == "all" else a.c5_mode
+    head_mode = "exact" if a.c5_mode == "all" else a.c5_mode
+    cert_on, delta_src, _ = C5_MODES[head_mode]
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
                              rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")),
-                             certify=head_mode != "off")
+                             certify=cert_on, delta=delta_src)
     chunk = C5_FS * 60
     pool = []
     for j in range(4):  # seeded 1-minute chunks: noise + meteor pings at +1 kHz, int16 I/Q interleaved
@@ -297,7 +303,7 @@ def run_c5(a, ctx, job, rank, world):
 
     def step():
         det.spectrogram_and_delta()
-        return det.detect(comm, thresholds=False, exact_decisions=mode[0] == "exact")
+        return det.detect(comm, thresholds=False, exact_decisions=C5_MODES[mode[0]][2])
 
     def sync_all():
         ctx.synchronize()
@@ -328,26 +334,31 @@ def run_c5(a, ctx, job, rank, world):
     sync_all()
     kms = {}
     for name, kid in (("cstft", _lib.K_CSTFT), ("band_delta", _lib.K_IQDELTA), ("fresh_thresholds", _lib.K_FRESH),
-                      ("scan", _lib.K_SSCAN), ("refine_delta64", _lib.K_REFINE)):
+                      ("scan", _lib.K_SSCAN), ("delta64", _lib.K_REFINE)):
         ms, cnt = ctx.timing_get(kid)
         kms[name] = round(ms, 4)
     kms["cstft"] = round(k_ms / max(k_n, 1), 4)  # the timed region's average
 
     def cert_info(r, m):
-        return {"mode": m, "certified": bool(r.certified), "near_tie": bool(r.near_tie),
-                "uncertain_before_refinement": int(r.uncertain_initial),
-                "refined_delta_frames": int(r.refined_delta_frames), "detector_passes": int(r.detector_passes),
-                "decision_bound_db": round(float(r.decision_bound), 6), "min_slack_db": round(float(r.min_slack), 6)}
+        if r.certified is None:
+            return {"mode": m, "certified": None, "delta": "fp32"}
+        return {"mode": m, "delta": "exact" if det.exact_delta else "fp32", "certified": bool(r.certified),
+                "near_tie": bool(r.near_tie), "uncertain_before_refinement": int(r.uncertain_initial),
+                "refined_delta_frames": int(r.refined_delta_frames), "db_refined_frames": int(r.db_refined_frames),
+                "detector_passes": int(r.detector_passes), "refine_budget_exhausted": bool(r.refine_budget_exhausted),
+                "decision_bound_db": float("%.6g" % r.decision_bound), "min_slack_db": float("%.6g" % r.min_slack)}
 
-    cert = {}
-    if head_mode != "off":
-        cert[head_mode] = cert_info(res, head_mode)
+    cert = cert_info(res, head_mode)
+    head_exact_delta = det.exact_delta
+    others = {}
     if a.c5_mode == "all":
-        # the certified modes, each timed on its own after the headline (fewer steps): flag = every
-        # decision checked against its error bounds, exact = the uncertain ones recomputed in float64
-        det.set_certify(True)
-        for m in ("flag", "exact"):
+        # the other decision modes, each timed on its own after the headline (fewer steps): off = the
+        # fp32 band sums uncertified, flag = certified with uncertain decisions reported, refine =
+        # the uncertain ones and the detections' frames recomputed in float64 (round 3's path)
+        for m in ("off", "flag", "refine"):
             mode[0] = m
+            det.set_certify(C5_MODES[m][0])
+            det.set_delta(C5_MODES[m][1])
             for _ in range(min(a.warmup, 3)):
                 r = step()
             sync_all()
@@ -359,11 +370,11 @@ def run_c5(a, ctx, job, rank, world):
             el = time.perf_counter() - t1
             if job is not None:
                 el = job.max_f64(el)
-            cert[m] = cert_info(r, m)
-            cert[m].update(steps=ns, ms_per_step=round(el / ns * 1e3, 4),
-                           value=round(world * int(C5_FS * a.c5_seconds) * ns / el / 1e6, 1),
-                           same_detections=bool(np.array_equal(r.detections[["start", "stop"]],
-                                                               res.detections[["start", "stop"]])))
+            others[m] = cert_info(r, m)
+            others[m].update(steps=ns, ms_per_step=round(el / ns * 1e3, 4),
+                             value=round(world * int(C5_FS * a.c5_seconds) * ns / el / 1e6, 1),
+                             same_detections=bool(np.array_equal(r.detections[["start", "stop"]],
+                                                                 res.detections[["start", "stop"]])))
     avg_s = k_ms / max(k_n, 1) / 1e3
     T = det.f1 - det.f0
     samples = shard  # per rank: its 3 h (the 3072-sample frame tail is read, not counted)
@@ -387,9 +398,8 @@ def run_c5(a, ctx, job, rank, world):
         "detections_per_step": int(len(res.detections)),
         "state_rounds": int(res.rounds),
         "exact_threshold_frames": int(res.refined),
-        # the headline's decision mode: off = the reference's arithmetic path uncertified; flag = every
-        # decision checked against its float64 error bounds; exact = the uncertain ones recomputed in
-        # float64 (meteorgpu.iq.IQShardDetector.detect).  "certification" times flag and exact.
+        # the headline's decision mode (C5_MODES): exact = the drop-in default, every frame's delta
+        # float64 from the samples and every decision certified; "modes" times the others
         "decisions": head_mode,
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
@@ -397,8 +407,19 @@ def run_c5(a, ctx, job, rank, world):
                      "kernel": "cstft4096_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
         "kernel_ms_per_step": kms,
-        "certification": cert or None,
+        "certification": cert,
+        "modes": others or None,
     }
+    if head_exact_delta:
+        # the exact delta's block step (refine_i8.hip + refine.hip frame_kernel): it re-reads every
+        # sample (4 B per complex sample) and writes / reads the 11-row block table (176 B per block)
+        # and delta, ed (16 B per frame)
+        nblk = (det.s1 - det.s0) // C5_HOP
+        xb = (det.s1 - det.s0) * 4 + nblk * 176 * 2 + T * 16
+        dms = kms["delta64"]
+        out["exact_delta"] = {"kernel": "block_i8_kernel<7> + frame_kernel", "ms": dms, "bytes": xb,
+                              "achieved_gbs": round(xb / (dms * 1e-3) / 1e9, 1) if dms > 0 else None,
+                              "frac_of_hbm": round(xb / (dms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dms > 0 else None}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
         from oracle import iq_oracle as Q
         m = C5_FS * 60  # one minute of the stream
@@ -616,7 +637,7 @@ def main():
             out["c5"] = {k: c5[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "scaling",
                                             "dtype", "roofline", "kernel_ms_per_step", "detections_per_step",
                                             "state_rounds", "exact_threshold_frames", "config", "cpu_baseline",
-                                            "certification") if k in c5}
+                                            "decisions", "certification", "modes", "exact_delta") if k in c5}
         except Exception as e:  # noqa: BLE001 -- one rank: the C3 line stands; several: fail as one job
             if world > 1:
                 raise

@@ -72,9 +72,12 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
  * specialised one exists (A/B testing of the kernels; results must agree).
  * MSD_OPT_FRESH_ALL = 1 → the C5 stream detector computes every adaptive threshold exactly up
  * front instead of only where a scan reads it (A/B of that scheme; results must agree; also
- * set by MSD_FRESH_ALL=1 in the environment). */
+ * set by MSD_FRESH_ALL=1 in the environment).
+ * MSD_OPT_REFINE_GOERTZEL = 1 → msd_iq_delta64_dev computes int16 blocks with the float64
+ * Goertzel kernel instead of the exact int8-MFMA one (A/B; both within their bounds). */
 #define MSD_OPT_GENERIC_STFT 1
 #define MSD_OPT_FRESH_ALL 2
+#define MSD_OPT_REFINE_GOERTZEL 3
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.
@@ -353,6 +356,18 @@ int msd_stream_certificate(msd_stream_plan *plan, int64_t *uncertain, double *mi
 int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg, int64_t hop,
                        double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo, int32_t noise_hi,
                        const int64_t *ranges, int64_t nranges, double *delta, double *ed);
+/* Which block step msd_iq_delta64_dev takes for a geometry (host only, no GPU): int16 input with
+ * blocks of D = gcd(nperseg, hop) = 1024 samples, no band touching bin 0 and at most 10 needed
+ * bins (band and noise bins +- 1) runs the EXACT integer DFT on the matrix cores (int16 samples as
+ * two int8 digits, the twiddles as six balanced base-256 digits, v_mfma_i32_16x16x64_i8, float64
+ * combination; bound ~120 u instead of the Goertzel's ~3 L / |sin theta| u) unless
+ * MSD_OPT_REFINE_GOERTZEL is set; other D % 64 == 0 the float64 Goertzel rows; any other D one
+ * lane per block.  Returns the path (> 0) or an error code. */
+#define MSD_REFINE_DIRECT 1
+#define MSD_REFINE_GOERTZEL_ROWS 2
+#define MSD_REFINE_INT8_MFMA 3
+int msd_iq_delta64_path(int32_t nperseg, int64_t hop, double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
+                        int32_t noise_hi, int32_t dtype);
 
 /* ------------------------------------------- a10: legacy spectrogram noise floor
  * prime_detection.py:65-91: band_power = np.sum(Pxx[noise_band]) sums the spectrogram over

@@ -181,6 +181,7 @@ void msd_destroy(msd_ctx *ctx) {
     if (ctx->rf_w) hipFree(ctx->rf_w);
     if (ctx->rf_ev) hipEventSynchronize(ctx->rf_ev), hipEventDestroy(ctx->rf_ev);
     if (ctx->rf_pin) hipHostFree(ctx->rf_pin);
+    if (ctx->i8_tab) hipFree(ctx->i8_tab);
     if (ctx->copy_stream) {
         hipStreamSynchronize(ctx->copy_stream);
         hipStreamDestroy(ctx->copy_stream);
@@ -246,6 +247,7 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
     switch (option) {
         case MSD_OPT_GENERIC_STFT: ctx->force_generic = value != 0; return MSD_OK;
         case MSD_OPT_FRESH_ALL: ctx->fresh_all = value != 0; return MSD_OK;
+        case MSD_OPT_REFINE_GOERTZEL: ctx->refine_goertzel = value != 0; return MSD_OK;
         default: return fail(MSD_ERR_INVALID, "msd_set_option: unknown option");
     }
 }

@@ -60,6 +60,11 @@ struct msd_ctx {
     void *rf_pin = nullptr;
     size_t rf_pin_bytes = 0;
     hipEvent_t rf_ev = nullptr;
+    // the int8-MFMA block step's tables (refine_i8.hip): B fragments, column starts, lane twiddles,
+    // built once per (frame length, bins)
+    void *i8_tab = nullptr;
+    uint64_t i8_key = 0;
+    bool refine_goertzel = false;  // MSD_OPT_REFINE_GOERTZEL: int16 refinement on the float64 Goertzel
 };
 
 struct msd_stft_plan {

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "msd_internal.h"
+#include "refine_i8.h"
 #include "refine_plan.h"
 
 namespace msd {
@@ -291,6 +292,17 @@ using namespace msd;
 
 extern "C" {
 
+int msd_iq_delta64_path(int32_t nperseg, int64_t hop, double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
+                        int32_t noise_hi, int32_t dtype) {
+    if (dtype != MSD_CI16 && dtype != MSD_CF32) return fail(MSD_ERR_UNSUPPORTED, "msd_iq_delta64_path: CI16 or CF32");
+    RefinePlan P;
+    std::string msg;
+    if (int rc = plan_refine(nperseg, hop, fs, band_lo, band_hi, noise_lo, noise_hi, nullptr, 0, 0, P, msg))
+        return fail(rc, "msd_iq_delta64_path: " + msg);
+    if (dtype == MSD_CI16 && i8_supported(P.G, P.K)) return MSD_REFINE_INT8_MFMA;
+    return P.G.rows ? MSD_REFINE_GOERTZEL_ROWS : MSD_REFINE_DIRECT;
+}
+
 int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg, int64_t hop,
                        double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo, int32_t noise_hi,
                        const int64_t *ranges, int64_t nranges, double *delta, double *ed) {
@@ -370,7 +382,19 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     hipError_t e = hipMemcpyAsync(rot, pin, b_rt, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(meta, pin + b_rt, b_hm, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipEventRecord(ctx->rf_ev, st);
-    if (e == hipSuccess) {
+    // int16 blocks of 1024 samples: the exact integer DFT on the matrix cores (refine_i8.hip), its
+    // own (smaller) rounding chain in the bound
+    RefineGeom GF = G;
+    const bool i8 = dtype == MSD_CI16 && !ctx->refine_goertzel && i8_supported(G, K);
+    if (i8) GF.chain = i8_chain_own() + G.chain_tail;
+    if (e == hipSuccess && i8) {
+        KernelTimer timer(ctx, K_REFINE);
+        if (int rc = launch_refine_i8(ctx, static_cast<const int16_t *>(x), G, K, d_bstart, d_bcs, nblocks, blk))
+            return rc;
+        hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, GF, K, d_fstart,
+                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed);
+        e = hipGetLastError();
+    } else if (e == hipSuccess) {
         KernelTimer timer(ctx, K_REFINE);
         if (G.rows) {  // rows of 16 lanes, S = D/16 (a multiple of 4) samples per lane
             const unsigned grid = (unsigned)((nblocks + 15) / 16);

@@ -33,6 +33,8 @@ struct RefineGeom {
     int64_t hop;
     double scale;             // density: 1 / (fs sum w^2)
     double chain;             // our float64 rounding chain + the reference's, in units of u
+    double chain_tail;        // the part of `chain` after the block values (frame combination, taps,
+                              // |Y|^2, the reference's chain): chain = own block step + chain_tail
     int nr;                   // frame ranges
 };
 
@@ -132,7 +134,8 @@ inline int plan_refine(int nperseg, int64_t hop, double fs, int band_lo, int ban
     }
     // the one-lane path sums D direct products (D + 4); the Goertzel path 3 L Gmax + 8 and the 16-lane sum
     const double own = G.rows ? 3.0 * G.L * gmax + 8.0 + 4.0 : (double)G.D + 4.0;
-    G.chain = own + (G.R + 4.0) + 8.0 + 4.0 * std::log2((double)N) + 11.0;
+    G.chain_tail = (G.R + 4.0) + 8.0 + 4.0 * std::log2((double)N) + 11.0;
+    G.chain = own + G.chain_tail;
     if (nranges > (1 << 20)) return err(E_UNSUPPORTED, "too many ranges");
     // frame ranges -> block ranges, compact prefix counts
     std::vector<int64_t> &fstart = P.fstart, &fcs = P.fcs, &bstart = P.bstart, &bcs = P.bcs;

@@ -38,6 +38,7 @@ K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE, K_CSTFT = 0, 1, 2, 3, 4, 5, 
 K_IQDELTA, K_FRESH, K_SSCAN, K_REFINE = 7, 8, 9, 10
 OPT_GENERIC_STFT = 1
 OPT_FRESH_ALL = 2
+OPT_REFINE_GOERTZEL = 3
 COMM_ID_BYTES = 128
 
 
@@ -219,6 +220,8 @@ _SIGS = [
     ("msd_iq_delta64_dev", C.c_int,
      [_P, _P, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_double, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
       _P, C.c_int64, _P, _P]),
+    ("msd_iq_delta64_path", C.c_int,
+     [C.c_int32, C.c_int64, C.c_double, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     ("msd_stream_plan_create", C.c_int,
      [_P, C.POINTER(MsdDetCfg), C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.POINTER(_P)]),
     ("msd_stream_plan_destroy", None, [_P]),
@@ -829,6 +832,18 @@ def iq_band_delta_dev(ctx: Context, spec: DeviceBuffer, nstreams: int, max_frame
     check(ctx.lib.msd_iq_band_delta_bound_dev(ctx.h, spec.ptr, _dp(etot), int(nstreams), int(max_frames), frames.ptr,
                                               int(nperseg), int(band[0]), int(band[1]), int(noise[0]), int(noise[1]),
                                               _dp(band_db), _dp(noise_db), _dp(delta), _dp(ed), int(ld)))
+
+
+REFINE_DIRECT, REFINE_GOERTZEL_ROWS, REFINE_INT8_MFMA = 1, 2, 3
+
+
+def iq_delta64_path(nperseg: int, hop: int, fs: float, band: tuple[int, int], noise: tuple[int, int],
+                    dtype_code_iq: int) -> int:
+    """the block step msd_iq_delta64_dev takes (REFINE_*; host only)"""
+    rc = load().msd_iq_delta64_path(int(nperseg), int(hop), float(fs), int(band[0]), int(band[1]), int(noise[0]),
+                                    int(noise[1]), int(dtype_code_iq))
+    check(min(rc, 0))
+    return rc
 
 
 def iq_delta64_dev(ctx: Context, x, dtype_code_iq: int, n_samples: int, nperseg: int, hop: int, fs: float,

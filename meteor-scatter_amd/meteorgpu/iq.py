@@ -155,7 +155,12 @@ class IQShardDetector:
     per-frame band delta written straight into the stream plan → detector over the whole stream.
 
     Certification (``certify``, on by default, as in proc_iq_samples / proc_iq_wav_file; the
-    uncertified fast path is ``certify=False``): the spectrogram kernel also writes each frame's energy,
+    uncertified fast path is ``certify=False``).  For int16 input at C5's geometry the detector's
+    delta is then float64-grade for EVERY frame (``delta="auto"`` -> exact: msd_iq_delta64_dev's
+    exact integer DFT of each 1024-sample block on the matrix cores, ~1e-13 dB bound), so one
+    certified pass settles every decision and the dB means are float64 as they stand.  Otherwise
+    (``delta="fp32"``, float32 input, other geometries) the delta comes from the fp32 spectrogram:
+    the spectrogram kernel also writes each frame's energy,
     the band delta kernel a bound on |delta - delta_ref| against the float64 reference (scipy's
     spectrogram of complex128 input), and every decision of the detector is checked against its
     bounds (include/msdsp.h, msd_stream_set_certify).  ``detect(exact_decisions=True)`` then
@@ -171,10 +176,18 @@ class IQShardDetector:
                  threshold_std_factor=4.0, flag_adaptive_threshold=True, threshold_estimation_window_sec=120,
                  threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                  threshold_fixed_init_duration_sec=10, rank: int = 0, world: int = 1, dtype=np.int16,
-                 seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = True):
+                 seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = True,
+                 delta: str = "auto"):
         """chunk_frames: keep only that many frames of spectrogram in HBM and stream the shard through
         it (``process_host``); the detector still sees the whole shard's delta.  A 24 h 192 kHz
-        stream (66 GB of int16 I/Q, 265 GB of spectrogram) then runs on one GPU."""
+        stream (66 GB of int16 I/Q, 265 GB of spectrogram) then runs on one GPU.
+        delta: where the detector's per-frame delta comes from -- "fp32": the band sums of the fp32
+        spectrogram (iq_band_delta); "exact": every frame in float64 from the samples
+        (msd_iq_delta64_dev), the spectrogram then only the product output; "auto": exact when
+        certifying int16 input whose geometry the exact integer DFT on the matrix cores covers
+        (REFINE_INT8_MFMA: blocks of 1024 samples, <= 10 bins, no band at 0 Hz -- C5), else fp32.
+        With the exact delta every frame's error bound is ~1e-13 dB, so certification settles every
+        decision in one pass (no energy partials, no refinement, no second detector pass)."""
         self.ctx, self.fs, self.N = ctx, fs, int(nperseg)
         self.hop = self.N - int(noverlap)
         self.block_sec = self.hop / fs
@@ -192,6 +205,16 @@ class IQShardDetector:
         self.chunk = int(chunk_frames) if chunk_frames and 0 < int(chunk_frames) < nloc else None
         nb = (self.chunk - 1) * self.hop + self.N if self.chunk else max(self.s1 - self.s0, 1)
         self.batch = IQBatch(ctx, 1, nb, fs, self.N, noverlap, dtype)
+        if delta not in ("auto", "fp32", "exact"):
+            raise ValueError(f"delta must be 'auto', 'fp32' or 'exact', not {delta!r}")
+        try:
+            self.delta_path = _lib.iq_delta64_path(self.N, self.hop, fs, self.band, self.noise, self.batch.code)
+        except _lib.MsdError:  # a geometry the float64 refinement does not cover (nperseg > 65536)
+            self.delta_path = 0
+        if delta == "exact" and not self.delta_path:
+            raise ValueError("delta='exact': msd_iq_delta64_dev does not cover this geometry")
+        self._delta_mode = delta
+        self.exact_delta = False
         self.d_frames = ctx.alloc(8)
         self.d_frames.upload(np.array([self.batch.T if self.s1 > self.s0 else 0], np.int64))
         cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
@@ -204,12 +227,24 @@ class IQShardDetector:
         self._read = None      # the shard's sample source when chunked (refinement re-reads samples)
         self._refined = []     # global frame ranges whose delta is float64 already
 
+    def set_delta(self, mode: str):
+        """the delta source ("auto", "fp32", "exact"; class docstring), from the next
+        spectrogram_and_delta on"""
+        if mode not in ("auto", "fp32", "exact"):
+            raise ValueError(f"delta must be 'auto', 'fp32' or 'exact', not {mode!r}")
+        if mode == "exact" and not self.delta_path:
+            raise ValueError("delta='exact': msd_iq_delta64_dev does not cover this geometry")
+        self._delta_mode = mode
+        self.exact_delta = mode == "exact" or (mode == "auto" and self.certify and
+                                               self.delta_path == _lib.REFINE_INT8_MFMA)
+        if self.certify and not self.exact_delta and self.d_etot is None:
+            self.d_etot = self.ctx.alloc(16 * 4 * self.ctx.lib.msd_cstft_energy_stride(1, max(self.batch.T, 1)))
+
     def set_certify(self, on: bool):
         """certification on / off (takes effect at the next spectrogram_and_delta)"""
-        if on and self.d_etot is None:
-            self.d_etot = self.ctx.alloc(16 * 4 * self.ctx.lib.msd_cstft_energy_stride(1, max(self.batch.T, 1)))
         self.certify = bool(on)
         self.plan.set_certify(self.certify)
+        self.set_delta(self._delta_mode)  # "auto" follows certification
 
     def upload(self, iq: np.ndarray, sample_offset: int = 0):
         """interleaved I/Q of this shard's samples, starting at shard sample `sample_offset`"""
@@ -219,11 +254,25 @@ class IQShardDetector:
         """async: spectrogram of the shard and its per-frame band delta (into the stream plan)"""
         self._refined = []
         if self.f1 > self.f0:
-            etot = self.d_etot if self.certify else None
-            self.batch.run(etot)
-            _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
-                                   self.noise, self.plan.d_delta, self.batch.T, etot=etot,
-                                   ed=self.plan.d_ed if self.certify else None)
+            if self.exact_delta:
+                self.batch.run()
+                self._delta_exact(self.batch.n, self.f1 - self.f0, 0)
+            else:
+                etot = self.d_etot if self.certify else None
+                self.batch.run(etot)
+                _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
+                                       self.noise, self.plan.d_delta, self.batch.T, etot=etot,
+                                       ed=self.plan.d_ed if self.certify else None)
+        if self.exact_delta:
+            self._refined = [[0, self.T]]  # every rank's frames are float64 (the ranks agree on this list)
+
+    def _delta_exact(self, n_samples: int, nframes: int, c0: int):
+        """float64 delta and bound of the local frames [c0, c0 + nframes), whose samples start at the
+        batch buffer's first sample (frame c0 + j at sample j * hop)"""
+        _lib.iq_delta64_dev(self.ctx, self.batch.d_x, self.batch.code, n_samples, self.N, self.hop, self.fs_,
+                            self.band, self.noise, np.array([[0, nframes]], np.int64),
+                            _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0),
+                            _lib.C.c_void_p(self.plan.d_ed.value + 8 * c0))
 
     def process_host(self, iq_shard: np.ndarray):
         """interleaved I/Q of the shard's samples [s0, s1) on the host → the shard's delta in the
@@ -248,6 +297,10 @@ class IQShardDetector:
             a = c0 * self.hop
             b = a + (nf - 1) * self.hop + self.N
             self.batch.upload(0, np.ascontiguousarray(read(a, b)))
+            if self.exact_delta:
+                self.batch.run()  # frames past nf read stale samples; the spectrogram is the product
+                self._delta_exact(b - a, nf, c0)
+                continue
             self.d_frames.upload(np.array([nf], np.int64))
             etot = self.d_etot if self.certify else None
             self.batch.run(etot)  # frames past nf read stale samples; their powers are not used
@@ -255,6 +308,8 @@ class IQShardDetector:
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                    self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T,
                                    etot=etot, ed=ed)
+        if self.exact_delta:
+            self._refined = [[0, self.T]]
 
     MAX_REFINE = 8  # refinement rounds before giving up (refine_budget_exhausted)
 
@@ -370,13 +425,15 @@ def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072
                     threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                     threshold_fixed_init_duration_sec=10, wav_start_date_time=None, out_csv_file=None,
                     device: int = 0, chunk_sec: float | None = None, exact_decisions: bool = True,
-                    certify: bool = True):
+                    certify: bool = True, delta: str = "auto"):
     """The batch detector of dsp/src/main.py (:380-527, :640-658) over an I/Q recording with the STFT
     frame as the block.  Returns (detections [OutputDetection], thresholds, delta, result).
     chunk_sec: stream the spectrogram through HBM in chunks of that many seconds (long recordings).
     certify / exact_decisions: every detector decision certified against the float64 reference, the
     uncertain ones recomputed in float64 (IQShardDetector); result.certified / near_tie /
-    decision_bound / refined_delta_frames report it.  certify=False is the uncertified fast path."""
+    decision_bound / refined_delta_frames report it.  certify=False is the uncertified fast path.
+    delta: IQShardDetector's delta source ("auto": the exact float64 delta of every frame for int16
+    C5-like geometries, else the fp32 spectrogram's band sums with certification and refinement)."""
     buf, code = interleave(i, q)
     n = buf.size // 2
     det = IQShardDetector(context(device), n, fs, nperseg, noverlap, freq_band, noise_band, threshold_std_factor,
@@ -384,7 +441,7 @@ def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072
                           threshold_freeze_before_detection_sec, threshold_freeze_after_detection_sec,
                           threshold_fixed_init_duration_sec, dtype=buf.dtype,
                           chunk_frames=int(chunk_sec * fs / (nperseg - noverlap)) if chunk_sec else None,
-                          certify=certify)
+                          certify=certify, delta=delta)
     try:
         det.process_host(buf[2 * det.s0: 2 * det.s1])
         res = det.detect(exact_decisions=exact_decisions)

@@ -343,3 +343,65 @@ def test_certification_over_rccl_single_rank():
     bs = HOP / FS
     assert res.certified and res.refined_delta_frames > 0 and res.uncertain_initial >= len(placed)
     assert [(int(a) * bs, int(b) * bs) for a, b, _ in res.detections] == [(x[0], x[1]) for x in rdets]
+
+
+def _refined_all(i, q, band=BAND, noise=NOISE, goertzel=False, hop=HOP):
+    """delta and ed of every frame from msd_iq_delta64_dev (int16: the int8-MFMA exact block step,
+    or with MSD_OPT_REFINE_GOERTZEL the float64 Goertzel one)"""
+    buf, _ = iq.interleave(i, q)
+    n = buf.size // 2
+    ctx = _lib.Context(0)
+    try:
+        ctx.set_option(_lib.OPT_REFINE_GOERTZEL, 1 if goertzel else 0)
+        det = iq.IQShardDetector(ctx, n, FS, N, N - hop, band, noise, 4.0, True, dtype=buf.dtype, **KW)
+        try:
+            det.process_host(buf[2 * det.s0: 2 * det.s1])
+            det._refine_local([(0, det.T)])
+            return det.plan.delta(), det.plan.ed()
+        finally:
+            det.close()
+    finally:
+        ctx.close()
+
+
+def test_int8_exact_blocks_match_oracle_and_goertzel():
+    """the int8-MFMA block step (exact integer DFT of int16 blocks, six-digit twiddles): every
+    frame's delta within its bound of the float64 oracle, the bound far below the float64
+    Goertzel's, and both paths within their joint bound of each other"""
+    i, q, _ = synth.synth_iq(71, FS, 4.0, 1000.0, rate_per_min=30, snr_db=(10, 30))
+    d8, e8 = _refined_all(i, q)
+    dg, eg = _refined_all(i, q, goertzel=True)
+    _, _, _, _, ref = Q.proc_iq_ref(i, q, FS, BAND, NOISE, N, N - HOP, **KW)
+    assert np.all(np.abs(d8 - ref) <= e8), np.max(np.abs(d8 - ref) / e8)
+    assert np.all(np.abs(dg - ref) <= eg)
+    assert np.all(np.abs(d8 - dg) <= e8 + eg)
+    assert e8.max() < 1e-10 and np.median(e8) < 0.1 * np.median(eg), (e8.max(), np.median(e8), np.median(eg))
+
+
+@pytest.mark.parametrize("case", ["full_scale", "tiny", "wide_bands"])
+def test_int8_exact_blocks_edge_cases(case):
+    """digit edge cases of the int8 step: samples at -32768 / 32767 and random full-scale values
+    (the high digit at its extremes), a near-silent stream (|x| <= 3: the bound scales with the
+    signal), and bands of 8 and 10 bins (6 and 8 column tiles)"""
+    rng = np.random.default_rng({"full_scale": 1, "tiny": 2, "wide_bands": 3}[case])
+    n = int(FS * 1.5)
+    band, noise = BAND, NOISE
+    if case == "full_scale":
+        i = rng.choice([-32768, 32767, -1, 0], n).astype(np.int16)
+        q = rng.integers(-32768, 32768, n).astype(np.int16)
+        i[: n // 3] = rng.integers(-32768, 32768, n // 3)
+    elif case == "tiny":
+        i = rng.integers(-3, 4, n).astype(np.int16)
+        q = rng.integers(-3, 4, n).astype(np.int16)
+    else:
+        i, q, _ = synth.synth_iq(72, FS, 1.5, 1000.0, rate_per_min=60, snr_db=(10, 30))
+    bands = [(band, noise)] if case != "wide_bands" else [((950.0, 1050.0), (-3050.0, -3000.0)),
+                                                       ((950.0, 1100.0), (-3050.0, -2950.0))]
+    for band, noise in bands:
+        nk = len({(b % N) for lo, hi in (iq.iq_band_bins(N, FS, band), iq.iq_band_bins(N, FS, noise))
+                  for k in range(lo, hi + 1) for b in (k - 1, k, k + 1)})
+        d8, e8 = _refined_all(i, q, band, noise)
+        _, _, _, _, ref = Q.proc_iq_ref(i, q, FS, band, noise, N, N - HOP, **KW)
+        ok = np.isfinite(ref)
+        assert np.all(np.abs(d8[ok] - ref[ok]) <= e8[ok]), (case, nk, np.max(np.abs(d8 - ref)[ok] / e8[ok]))
+        assert nk == {"wide_bands": nk if nk in (8, 10) else -1}.get(case, 9)

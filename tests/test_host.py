@@ -154,3 +154,20 @@ def test_proc_wav_file_asserts_before_gpu(tmp_path):
         dsp.proc_wav_file(str(p), 0.2, (993, 1013), (690, 710), 512, 4, wav_end_sec=2.0,
                           disable_show_and_write=True)
 
+
+
+def test_refinement_path_query():
+    """msd_iq_delta64_path (host only): which block step the float64 refinement takes -- the exact
+    int8-MFMA DFT for int16 at C5's geometry, the float64 Goertzel rows for float32 input, other
+    block sizes and bands at 0 Hz, one lane per block when D is not a multiple of 64"""
+    from meteorgpu import _lib
+    c5 = ((21, 22), (-65, -63))
+    assert _lib.iq_delta64_path(4096, 1024, 192000, *c5, _lib.MSD_CI16) == _lib.REFINE_INT8_MFMA
+    assert _lib.iq_delta64_path(4096, 1024, 192000, *c5, _lib.MSD_CF32) == _lib.REFINE_GOERTZEL_ROWS
+    assert _lib.iq_delta64_path(4096, 2048, 192000, *c5, _lib.MSD_CI16) == _lib.REFINE_GOERTZEL_ROWS  # D 2048
+    assert _lib.iq_delta64_path(4096, 1000, 192000, *c5, _lib.MSD_CI16) == _lib.REFINE_DIRECT        # D 8
+    assert _lib.iq_delta64_path(4096, 1024, 192000, (-2, 2), (40, 42), _lib.MSD_CI16) == _lib.REFINE_GOERTZEL_ROWS
+    assert _lib.iq_delta64_path(4096, 1024, 192000, (20, 27), (-66, -60), _lib.MSD_CI16) == _lib.REFINE_GOERTZEL_ROWS
+    import pytest
+    with pytest.raises(_lib.MsdError):
+        _lib.iq_delta64_path(131072, 1024, 192000, *c5, _lib.MSD_CI16)
