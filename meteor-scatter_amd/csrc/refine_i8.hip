@@ -167,6 +167,15 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
             ym = __builtin_fma(q, tw[0][r].y, ym);
         }
         double yx[NX > 0 ? NX : 1];
+        // tile 6's columns 6 and 7 (no digit there) carry the sub-block sums of I and Q (B = 1 on
+        // the I / Q values): the block's exact sample sum, for the detrend term of the bound
+        int32_t bsum = 0;
+        if constexpr (NX > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bsum += (acc_h[6][r] << 8) + acc_l[6][r];
+            bsum += __shfl_xor(bsum, 16, 64);
+            bsum += __shfl_xor(bsum, 32, 64);
+        }
 #pragma unroll
         for (int e = 0; e < NX; ++e) {
             yx[e] = 0.0;
@@ -198,10 +207,16 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
 #pragma unroll
             for (int e = 0; e < NX; ++e)
                 if ((c & 7) == 0) o[2 * ((int64_t)(8 + e) * nblocks + g) + (c >> 3)] = yx[e];
-            if (l == 0) {
+            // sum (|I| + |Q|) <= 256 (sum |h| + values): x = 256 h + (x & 255).  frame_kernel bounds the
+            // detrended frame's sum |v| by it plus N |mean|, the mean from the block sums (NX > 0:
+            // exact; else unknown, the sum row 0 and the bound doubled instead, N |mean| <= sum |x|)
+            const double l1 = 256.0 * ((double)hsum + 2.0 * D);
+            if constexpr (NX > 0) {
+                if (c == 6 || c == 7) o[2 * ((int64_t)nk * nblocks + g) + (c - 6)] = (double)bsum;
+                if (l == 0) out[(int64_t)(nk + 1) * nblocks + g] = make_double2(l1, 0.0);
+            } else if (l == 0) {
                 out[(int64_t)nk * nblocks + g] = make_double2(0.0, 0.0);
-                // sum (|I| + |Q|) <= 256 (sum |h| + values): x = 256 h + (x & 255); doubled for the mean term
-                out[(int64_t)(nk + 1) * nblocks + g] = make_double2(2.0 * 256.0 * ((double)hsum + 2.0 * D), 0.0);
+                out[(int64_t)(nk + 1) * nblocks + g] = make_double2(2.0 * l1, 0.0);
             }
         }
     }
@@ -245,11 +260,18 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
             bin = 8 + (t - 6), part = cc >> 3, dig = cc & 7;
             return bin < nk && dig < I8_ND;
         };
+        // tile 6, columns 6 / 7: ones on the I / Q values (the sub-block sums, block_i8_kernel)
+        auto sumcol = [&](int t, int cc) { return t == 6 && (cc == 6 || cc == 7); };
         // B[t][v][c] for v = 0..127: value v of a sub-block row = sample v >> 1, I (v even) or Q
         std::vector<int8_t> Bm((size_t)NT * 128 * 16, 0);
         std::vector<int> init((size_t)NT * 16, 0);
         for (int t = 0; t < NT; ++t)
             for (int cc = 0; cc < 16; ++cc) {
+                if (sumcol(t, cc)) {
+                    for (int v = 0; v < 128; ++v) Bm[((size_t)t * 128 + v) * 16 + cc] = (v & 1) == cc - 6 ? 1 : 0;
+                    init[t * 16 + cc] = 128 * 64;
+                    continue;
+                }
                 int bin, part, dig;
                 if (!colmap(t, cc, bin, part, dig)) continue;
                 const int64_t km = K.km[bin];

@@ -375,7 +375,8 @@ def test_int8_exact_blocks_match_oracle_and_goertzel():
     assert np.all(np.abs(d8 - ref) <= e8), np.max(np.abs(d8 - ref) / e8)
     assert np.all(np.abs(dg - ref) <= eg)
     assert np.all(np.abs(d8 - dg) <= e8 + eg)
-    assert e8.max() < 1e-10 and np.median(e8) < 0.1 * np.median(eg), (e8.max(), np.median(e8), np.median(eg))
+    # the bound itself: below the CSV's 1e-9 dB everywhere, ~25x tighter than the Goertzel's
+    assert e8.max() < 1e-9 and np.median(e8) < 0.1 * np.median(eg), (e8.max(), np.median(e8), np.median(eg))
 
 
 @pytest.mark.parametrize("case", ["full_scale", "tiny", "wide_bands"])
