@@ -60,13 +60,6 @@ __device__ __forceinline__ double dpp64(double x) {
     const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), CTRL, 0xf, 0xf, true);
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
-__device__ __forceinline__ double xor_lanes(double x, int m) {
-    const long long v = __builtin_bit_cast(long long, x);
-    const int lo = __shfl_xor((int)(v & 0xffffffffll), m, 64);
-    const int hi = __shfl_xor((int)(v >> 32), m, 64);
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 struct Raw {
     v4u a, b, c, d;  // the lane's 64 bytes: int16 values 32 q .. 32 q + 31 of its row
@@ -92,9 +85,43 @@ __device__ __forceinline__ void digits(const uint32_t *w, v4i &hi, v4i &lo, uint
     }
 }
 
+// f64 sums of lane l and lane l ^ 16 / l ^ 32 (v_permlane16/32_swap: VALU, no LDS round trip)
+__device__ __forceinline__ double add_xor16(double x) {
+    const long long v = __builtin_bit_cast(long long, x);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)(v & 0xffffffffll), (unsigned)(v & 0xffffffffll), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
+    const double a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+    const double b = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+    return a + b;
+}
+__device__ __forceinline__ double add_xor32(double x) {
+    const long long v = __builtin_bit_cast(long long, x);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)(v & 0xffffffffll), (unsigned)(v & 0xffffffffll), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
+    const double a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+    const double b = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+    return a + b;
+}
+__device__ __forceinline__ int add_xor16_i(int v) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)(r[0] + r[1]);
+}
+__device__ __forceinline__ int add_xor32_i(int v) {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)(r[0] + r[1]);
+}
+
+template <int NT>
+struct Acc {
+    v4i h[NT], l[NT];
+};
+
 // out (bin-major, refine.hip's block table): out[b * nblocks + g] = B_g[k_b] for b < nk, then the
-// block's sample sum (b = nk: written 0, the plan has no bin 0) and an upper bound of sum (|re| +
-// |im|) (b = nk + 1, .x; doubled: frame_kernel bounds sum |v| by it plus N |mean| with the mean 0)
+// block's sample sum (b = nk) and an upper bound of sum (|re| + |im|) (b = nk + 1, .x)
+//
+// Software-pipelined: while the VALU reduces block g from one accumulator set, the matrix cores
+// run block g + 1's 28 MFMAs into the other (the two sets, 112 VGPRs, are why the B fragments
+// live in LDS: 14 ds_read_b128 per block); the next block's samples are loaded one block ahead.
 template <int NT>
 __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restrict__ x, int64_t D,
                                                           const int64_t *__restrict__ bstart,
@@ -103,110 +130,101 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
                                                           const int *__restrict__ colinit,
                                                           const double2 *__restrict__ ltw, double2 *__restrict__ out) {
     constexpr int NX = NT - 6;  // extra bins (8 + e), two components each, in tiles 6 ..
+    __shared__ v4i sB[NT * 2 * 64];
+    for (int i = threadIdx.x; i < NT * 2 * 64; i += 256) sB[i] = bfrag[i];
+    __syncthreads();
     const int l = threadIdx.x & 63;
     const int c = l & 15;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t g0 = wave * per_wave;
     const int64_t g1 = g0 + per_wave < nblocks ? g0 + per_wave : nblocks;
     if (g0 >= g1) return;
-    // the B fragments (every tile, both K steps) and each column's accumulator start 128 sum_k B
-    v4i B[NT][2];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) B[t][ks] = bfrag[(t * 2 + ks) * 64 + l];
     int cinit[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) cinit[t] = colinit[t * 16 + c];
     // this lane's sub-block twiddles W^{64 k s} (s = 4 (l >> 4) + r) for its component's bin, the
-    // imaginary part signed by the component (re: -, im: +), and the same for its extra bins
+    // imaginary part signed by the component (re: +, im: -), and the same for its extra bins
     double2 tw[1 + NX][4];
 #pragma unroll
     for (int e = 0; e <= NX; ++e)
 #pragma unroll
         for (int r = 0; r < 4; ++r) tw[e][r] = ltw[(e * 4 + r) * 64 + l];
     const int ncomp = 2 * (nk < 8 ? nk : 8);
+    const int dg = c & 7;  // extra tiles: this lane's digit (6, 7: the sum columns / zero)
+    const double xscale = dg < 6 ? __builtin_ldexp(1.0, -6 - 8 * dg) : 0.0;
     auto block_at = [&](int64_t g) {
         const int r = find_range_i8(bcs, nr, g);
         return bstart[r] + (g - bcs[r]);
     };
-    Raw raw = load_raw(x + 2 * block_at(g0) * D, l);
-    for (int64_t g = g0; g < g1; ++g) {
+    // the MFMAs of one block from its raw samples (sum |h| into habs)
+    auto matmul = [&](const Raw &raw, Acc<NT> &A, uint32_t &habs) __attribute__((always_inline)) {
         uint32_t w[16];
         __builtin_memcpy(w, &raw, 64);
-        if (g + 1 < g1) raw = load_raw(x + 2 * block_at(g + 1) * D, l);  // prefetch
         v4i ah[2], al[2];
-        uint32_t habs = 0;
+        habs = 0;
         digits(w, ah[0], al[0], habs);
         digits(w + 8, ah[1], al[1], habs);
-        v4i acc_h[NT], acc_l[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            acc_h[t] = v4i{0, 0, 0, 0};
-            acc_l[t] = v4i{cinit[t], cinit[t], cinit[t], cinit[t]};
+            A.h[t] = v4i{0, 0, 0, 0};
+            A.l[t] = v4i{cinit[t], cinit[t], cinit[t], cinit[t]};
         }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                acc_h[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[ks], B[t][ks], acc_h[t], 0, 0, 0);
-                acc_l[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], B[t][ks], acc_l[t], 0, 0, 0);
+                const v4i b = sB[(t * 2 + ks) * 64 + l];
+                A.h[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[ks], b, A.h[t], 0, 0, 0);
+                A.l[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], b, A.l[t], 0, 0, 0);
             }
-        // this lane's component: P_s = 2^-6 sum_d 2^-8d (256 acc_h + acc_l), Horner from the lowest
-        // digit (the first steps are exact in float64), then the twiddled sum over its 4 rows
+    };
+    // the float64 reduction of one block and its stores
+    auto reduce = [&](const Acc<NT> &A, uint32_t habs, int64_t g) __attribute__((always_inline)) {
+        // this lane's component: P_s = 2^-6 sum_d 2^-8d (256 h_d + l_d) by Horner from the lowest digit
+        // (its first steps exact), then the twiddled sum over the lane's 4 rows with the partner
+        // component (lane ^ 1; the sign rides in tw.y)
         double ym = 0.0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            double p = (double)((acc_h[5][r] << 8) + acc_l[5][r]);
+            double p = (double)((A.h[5][r] << 8) + A.l[5][r]);
 #pragma unroll
-            for (int d = 4; d >= 0; --d) p = __builtin_fma(p, 0x1p-8, (double)((acc_h[d][r] << 8) + acc_l[d][r]));
+            for (int d = 4; d >= 0; --d) p = __builtin_fma(p, 0x1p-8, (double)((A.h[d][r] << 8) + A.l[d][r]));
             p *= 0x1p-6;
-            // the partner component (lane ^ 1): re with im; the sign rides in tw.y
             const double q = dpp64<0xB1>(p);
             ym = __builtin_fma(p, tw[0][r].x, ym);
             ym = __builtin_fma(q, tw[0][r].y, ym);
         }
+        ym = add_xor32(add_xor16(ym));  // the four lane groups (rows 0-3, 4-7, 8-11, 12-15)
+        // extra bins: each lane one digit of one component; twiddle its rows (partner: lane ^ 8,
+        // same digit), scale, then sum the 6 digit lanes of the half-row and the lane groups
         double yx[NX > 0 ? NX : 1];
-        // tile 6's columns 6 and 7 (no digit there) carry the sub-block sums of I and Q (B = 1 on
-        // the I / Q values): the block's exact sample sum, for the detrend term of the bound
         int32_t bsum = 0;
-        if constexpr (NX > 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bsum += (acc_h[6][r] << 8) + acc_l[6][r];
-            bsum += __shfl_xor(bsum, 16, 64);
-            bsum += __shfl_xor(bsum, 32, 64);
-        }
 #pragma unroll
         for (int e = 0; e < NX; ++e) {
-            yx[e] = 0.0;
-            const int dg = c & 7;
+            double acc = 0.0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int32_t tv = (acc_h[6 + e][r] << 8) + acc_l[6 + e][r];
-                double p = dg < 6 ? (double)tv * __builtin_ldexp(1.0, -6 - 8 * dg) : 0.0;
-                p += dpp64<0xB1>(p);   // the 8 digit lanes of this half-row: xor 1, xor 2, mirror
-                p += dpp64<0x4E>(p);
-                p += dpp64<0x141>(p);
-                const double q = dpp64<0x128>(p);  // row_ror:8 -- the other component of the bin
-                yx[e] = __builtin_fma(p, tw[1 + e][r].x, yx[e]);
-                yx[e] = __builtin_fma(q, tw[1 + e][r].y, yx[e]);
+                const int32_t tv = (A.h[6 + e][r] << 8) + A.l[6 + e][r];
+                if (e == 0) bsum += tv;  // columns 6 / 7 of tile 6: the sub-block sums of I / Q
+                const double v = (double)tv;
+                const double u = dpp64<0x128>(v);  // row_ror:8 -- the other component, same digit
+                acc = __builtin_fma(v, tw[1 + e][r].x, acc);
+                acc = __builtin_fma(u, tw[1 + e][r].y, acc);
             }
+            acc *= xscale;  // 0 on the lanes without a digit
+            acc += dpp64<0xB1>(acc);  // the 8 lanes of the half-row: xor 1, xor 2, mirror
+            acc += dpp64<0x4E>(acc);
+            acc += dpp64<0x141>(acc);
+            yx[e] = add_xor32(add_xor16(acc));
         }
-        // the four lane groups (rows 0-3, 4-7, 8-11, 12-15 of the tile)
-        ym += xor_lanes(ym, 16);
-        ym += xor_lanes(ym, 32);
-#pragma unroll
-        for (int e = 0; e < NX; ++e) {
-            yx[e] += xor_lanes(yx[e], 16);
-            yx[e] += xor_lanes(yx[e], 32);
-        }
+        if constexpr (NX > 0) bsum = add_xor32_i(add_xor16_i(bsum));
         const int hsum = wave_sum_i((int)habs);
         if (l < 16) {
             double *o = reinterpret_cast<double *>(out);
             if (c < ncomp) o[2 * ((int64_t)(c >> 1) * nblocks + g) + (c & 1)] = ym;
 #pragma unroll
             for (int e = 0; e < NX; ++e)
-                if ((c & 7) == 0) o[2 * ((int64_t)(8 + e) * nblocks + g) + (c >> 3)] = yx[e];
+                if (dg == 0) o[2 * ((int64_t)(8 + e) * nblocks + g) + (c >> 3)] = yx[e];
             // sum (|I| + |Q|) <= 256 (sum |h| + values): x = 256 h + (x & 255).  frame_kernel bounds the
             // detrended frame's sum |v| by it plus N |mean|, the mean from the block sums (NX > 0:
             // exact; else unknown, the sum row 0 and the bound doubled instead, N |mean| <= sum |x|)
@@ -219,6 +237,25 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
                 out[(int64_t)(nk + 1) * nblocks + g] = make_double2(2.0 * l1, 0.0);
             }
         }
+    };
+    Acc<NT> A0, A1;
+    uint32_t h0 = 0, h1 = 0;
+    Raw raw = load_raw(x + 2 * block_at(g0) * D, l);
+    matmul(raw, A0, h0);
+    if (g0 + 1 < g1) raw = load_raw(x + 2 * block_at(g0 + 1) * D, l);
+    for (int64_t g = g0; g < g1; g += 2) {
+        // block g in A0: block g + 1's MFMAs into A1 (its samples loaded), g + 2's samples requested
+        if (g + 1 < g1) {
+            matmul(raw, A1, h1);
+            if (g + 2 < g1) raw = load_raw(x + 2 * block_at(g + 2) * D, l);
+        }
+        reduce(A0, h0, g);
+        if (g + 1 >= g1) break;
+        if (g + 2 < g1) {
+            matmul(raw, A0, h0);
+            if (g + 3 < g1) raw = load_raw(x + 2 * block_at(g + 3) * D, l);
+        }
+        reduce(A1, h1, g + 1);
     }
 }
 

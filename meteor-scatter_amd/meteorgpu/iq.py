@@ -121,33 +121,42 @@ def frame_shard(n_samples: int, nperseg: int, hop: int, rank: int, world: int):
     return T, f0, f1, f0 * hop, ((f1 - 1) * hop + nperseg) if f1 > f0 else f0 * hop
 
 
-def _merge(iv):
-    """sorted, merged [a, b) intervals"""
-    out = []
-    for a, b in sorted((int(a), int(b)) for a, b in iv if b > a):
-        if out and a <= out[-1][1]:
-            out[-1][1] = max(out[-1][1], b)
-        else:
-            out.append([a, b])
-    return out
+def _as_iv(iv) -> np.ndarray:
+    a = np.asarray(list(iv) if not isinstance(iv, np.ndarray) else iv, dtype=np.int64)
+    return a.reshape(-1, 2)
 
 
-def _subtract(iv, done):
-    """intervals iv minus the (merged) intervals done"""
-    out = []
-    for a, b in iv:
-        cur = a
-        for c, d in done:
-            if d <= cur or c >= b:
-                continue
-            if c > cur:
-                out.append([cur, c])
-            cur = max(cur, d)
-            if cur >= b:
-                break
-        if cur < b:
-            out.append([cur, b])
-    return out
+def _merge(iv) -> list:
+    """sorted, merged [a, b) intervals (touching ones joined), as a list of [a, b]"""
+    a = _as_iv(iv)
+    a = a[a[:, 1] > a[:, 0]]
+    if a.size == 0:
+        return []
+    a = a[np.argsort(a[:, 0], kind="stable")]
+    ends = np.maximum.accumulate(a[:, 1])
+    new = np.ones(len(a), bool)
+    new[1:] = a[1:, 0] > ends[:-1]  # a start past every earlier end opens a new interval
+    heads = np.flatnonzero(new)
+    tails = np.r_[heads[1:] - 1, len(a) - 1]
+    return np.stack([a[heads, 0], ends[tails]], 1).tolist()
+
+
+def _subtract(iv, done) -> list:
+    """the (merged) intervals iv minus the (merged) intervals done: the elementary segments between
+    all their boundaries that iv covers and done does not, merged"""
+    a, d = _as_iv(iv), _as_iv(done)
+    if a.size == 0:
+        return []
+    if d.size == 0:
+        return a.tolist()
+    pts = np.unique(np.concatenate([a.reshape(-1), d.reshape(-1)]))
+    lo, hi = pts[:-1], pts[1:]
+
+    def covered(x, seg):  # x inside one of the sorted disjoint [start, end)
+        return np.searchsorted(seg[:, 0], x, "right") > np.searchsorted(seg[:, 1], x, "right")
+
+    keep = covered(lo, a) & ~covered(lo, d)
+    return _merge(np.stack([lo[keep], hi[keep]], 1))
 
 
 class IQShardDetector:
@@ -391,12 +400,10 @@ class IQShardDetector:
 
     def _refine_local(self, ranges):
         """float64 delta (and its bound) of this rank's frames in the global ranges, from the samples"""
-        loc = []
-        for a, b in ranges:
-            a, b = max(a, self.f0), min(b, self.f1)
-            if b > a:
-                loc.append((a - self.f0, b - self.f0))
-        if not loc:
+        r = _as_iv(ranges)
+        r = np.stack([np.maximum(r[:, 0], self.f0), np.minimum(r[:, 1], self.f1)], 1) - self.f0
+        loc = r[r[:, 1] > r[:, 0]]
+        if not len(loc):
             return
         if not self.chunk:  # the shard's samples are resident: frame j at sample j * hop
             _lib.iq_delta64_dev(self.ctx, self.batch.d_x, self.batch.code, self.batch.n, self.N, self.hop, self.fs_,

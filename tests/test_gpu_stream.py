@@ -167,7 +167,9 @@ def test_iq_end_to_end(seed, adaptive):
     inside = np.zeros(delta.size, bool)
     for r in rdets:  # the detections' frames are float64: within the refinement's bound of the oracle
         inside[int(round(r[0] * 192000 / 1024)): int(round(r[1] * 192000 / 1024))] = True
-    assert res.db_refined_frames > 0 and np.max(np.abs(delta - rdelta)[inside]) < DB_TOL
+    assert np.max(np.abs(delta - rdelta)[inside]) < DB_TOL
+    # int16 at C5's geometry: every frame's delta is the exact one already (none left to refine)
+    assert res.refined_delta_frames == 0 and np.max(np.abs(delta - rdelta)) < DB_TOL
     # on the device's own delta the detector is bit-exact with the oracle's
     bs = 1024 / 192000
     from oracle import dsp_oracle as O

@@ -171,3 +171,26 @@ def test_refinement_path_query():
     import pytest
     with pytest.raises(_lib.MsdError):
         _lib.iq_delta64_path(131072, 1024, 192000, *c5, _lib.MSD_CI16)
+
+
+def test_interval_helpers_match_sets():
+    """meteorgpu.iq's refinement bookkeeping (_merge, _subtract: vectorised) against plain sets of
+    frames on random interval lists, touching and nested ones included"""
+    import numpy as np
+    from meteorgpu.iq import _merge, _subtract
+    rng = np.random.default_rng(5)
+
+    def frames(iv):
+        return set().union(*[set(range(a, b)) for a, b in iv]) if iv else set()
+
+    for _ in range(300):
+        n, m = int(rng.integers(0, 12)), int(rng.integers(0, 6))
+        iv = [(int(a), int(a + w)) for a, w in zip(rng.integers(0, 200, n), rng.integers(-3, 40, n))]
+        dn = _merge([(int(a), int(a + w)) for a, w in zip(rng.integers(0, 200, m), rng.integers(0, 60, m))])
+        mg = _merge(iv)
+        assert frames(mg) == frames([(a, b) for a, b in iv if b > a])
+        assert all(b > a for a, b in mg) and all(mg[i][1] < mg[i + 1][0] for i in range(len(mg) - 1))
+        sub = _subtract(mg, dn)
+        assert frames(sub) == frames(mg) - frames(dn)
+        assert all(b > a for a, b in sub) and all(sub[i][1] < sub[i + 1][0] for i in range(len(sub) - 1))
+    assert _subtract([[0, 10]], []) == [[0, 10]] and _subtract([], [[0, 5]]) == [] and _merge([]) == []
