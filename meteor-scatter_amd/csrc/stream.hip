@@ -90,6 +90,7 @@ struct msd_stream_plan {
     // msd_stream_set_certify and by any scan with it off (a stale or never-written certificate
     // must not read as "certified")
     bool cert_valid = false;
+    bool cert_staged = false;  // the certificate's counts / slacks already in h_cert (detect_local)
     bool want_exact = true;  // msd_stream_set_exact_thresholds
     int32_t listed = -1;     // decisions only: frames listed by the last msd_stream_scan (host copy)
     // pinned host block for the small per-step readbacks (counters, exit state, margins, chunk
@@ -1447,6 +1448,7 @@ int msd_stream_set_certify(msd_stream_plan *p, int32_t on) {
     if (!p) return fail(MSD_ERR_INVALID, "msd_stream_set_certify: null plan");
     p->certify = on != 0;
     p->cert_valid = false;  // the next full scan writes the certificate
+    p->cert_staged = false;
     return MSD_OK;
 }
 
@@ -1495,6 +1497,35 @@ int msd_stream_set_terr0(msd_stream_plan *p, double s1, double s2) {
     return MSD_OK;
 }
 
+// pinned staging of the certificate (grown once): per-segment slacks, counts, then the lists
+static int cert_staging(msd_stream_plan *p, double2 **sl, int32_t **cnt, longlong2 **u) {
+    const size_t need =
+        sizeof(double2) * p->nseg + sizeof(int32_t) * (p->nseg + 1) + sizeof(longlong2) * p->nseg * UCAP;
+    if (p->h_cert_bytes < need) {
+        if (p->h_cert) (void)hipHostFree(p->h_cert);
+        p->h_cert = nullptr;
+        p->h_cert_bytes = 0;
+        MSD_HIP(hipHostMalloc(&p->h_cert, need, hipHostMallocDefault));
+        p->h_cert_bytes = need;
+    }
+    *sl = static_cast<double2 *>(p->h_cert);
+    *cnt = reinterpret_cast<int32_t *>(*sl + p->nseg);
+    *u = reinterpret_cast<longlong2 *>(*cnt + p->nseg + (p->nseg & 1));
+    return MSD_OK;
+}
+
+// the counts and slacks into the staging block (async, on the context stream)
+static int cert_enqueue(msd_stream_plan *p) {
+    double2 *sl;
+    int32_t *cnt;
+    longlong2 *u;
+    if (int rc = cert_staging(p, &sl, &cnt, &u)) return rc;
+    hipStream_t st = p->ctx->stream;
+    MSD_HIP(hipMemcpyAsync(sl, p->d_slack, sizeof(double2) * p->nseg, hipMemcpyDeviceToHost, st));
+    MSD_HIP(hipMemcpyAsync(cnt, p->d_ucnt, sizeof(int32_t) * p->nseg, hipMemcpyDeviceToHost, st));
+    return MSD_OK;
+}
+
 int msd_stream_certificate(msd_stream_plan *p, int64_t *uncertain, double *min_slack, double *max_zone,
                            int64_t *frames, int64_t *srcs, int64_t cap, int64_t *listed) {
     if (!p || !uncertain || !min_slack || !max_zone || !listed)
@@ -1509,23 +1540,16 @@ int msd_stream_certificate(msd_stream_plan *p, int64_t *uncertain, double *min_s
         return fail(MSD_ERR_INVALID, "msd_stream_certificate: call msd_stream_scan with certification on first");
     DeviceGuard g(p->ctx->device);
     hipStream_t st = p->ctx->stream;
-    // pinned staging (grown once): counts and slacks in one round trip, the lists in a second one
-    // only when something is uncertain
-    const size_t need =
-        sizeof(double2) * p->nseg + sizeof(int32_t) * (p->nseg + 1) + sizeof(longlong2) * p->nseg * UCAP;
-    if (p->h_cert_bytes < need) {
-        if (p->h_cert) (void)hipHostFree(p->h_cert);
-        p->h_cert = nullptr;
-        p->h_cert_bytes = 0;
-        MSD_HIP(hipHostMalloc(&p->h_cert, need, hipHostMallocDefault));
-        p->h_cert_bytes = need;
+    // counts and slacks in one round trip (already staged by msd_stream_detect_local's last sync),
+    // the lists in a second one only when something is uncertain
+    double2 *sl;
+    int32_t *cnt;
+    longlong2 *u;
+    if (int rc = cert_staging(p, &sl, &cnt, &u)) return rc;
+    if (!p->cert_staged) {
+        if (int rc = cert_enqueue(p)) return rc;
+        MSD_HIP(hipStreamSynchronize(st));
     }
-    auto *sl = static_cast<double2 *>(p->h_cert);
-    auto *cnt = reinterpret_cast<int32_t *>(sl + p->nseg);
-    auto *u = reinterpret_cast<longlong2 *>(cnt + p->nseg + (p->nseg & 1));
-    MSD_HIP(hipMemcpyAsync(sl, p->d_slack, sizeof(double2) * p->nseg, hipMemcpyDeviceToHost, st));
-    MSD_HIP(hipMemcpyAsync(cnt, p->d_ucnt, sizeof(int32_t) * p->nseg, hipMemcpyDeviceToHost, st));
-    MSD_HIP(hipStreamSynchronize(st));
     int64_t tot = 0;
     for (int64_t q = 0; q < p->nseg; ++q) {
         tot += cnt[q];
@@ -1591,6 +1615,7 @@ int msd_stream_scan(msd_stream_plan *p, double thr0, const msd_stream_state *ent
     hipStream_t st = p->ctx->stream;
     int32_t nround = 0;
     const int32_t scan_mode = !p->scanned ? 1 : (reset == 1 || reset == 2 ? reset : 0);
+    p->cert_staged = false;
     if (p->nseg == 0) {
         if (exit_state) *exit_state = *entry;
         if (rounds) *rounds = 0;
@@ -1819,7 +1844,12 @@ int msd_stream_detect_local(msd_stream_plan *p, int32_t exact_thresholds, msd_de
                        nr);
     MSD_HIP(hipGetLastError());
     MSD_HIP(hipMemcpyAsync(out, p->d_out, sizeof(msd_det) * nr, hipMemcpyDeviceToHost, st));
+    // certifying: the certificate's counts and slacks ride on the same sync
+    if (p->certify && p->cert_valid) {
+        if (int rc2 = cert_enqueue(p)) return rc2;
+    }
     MSD_HIP(hipStreamSynchronize(st));
+    p->cert_staged = p->certify && p->cert_valid;
     return MSD_OK;
 }
 
