@@ -74,6 +74,10 @@ def parse():
                          "flag = the same certified, uncertain decisions reported; refine = flag + the uncertain "
                          "ones and every detection's frames recomputed in float64 (round 3's certified path); "
                          "all = the line on 'exact', plus the other modes timed under \"modes\"")
+    ap.add_argument("--c5-overlap", type=int, default=0,
+                    help="C5: run the stream detector on a second HIP stream beside the spectrogram, which leaves "
+                         "this many workgroup slots free (exact delta only: the detector does not read the "
+                         "spectrogram); 0 = one stream")
     ap.add_argument("--shard-day", action="store_true",
                     help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
                          "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "
@@ -281,7 +285,7 @@ def run_c5(a, ctx, job, rank, world):
     cert_on, delta_src, _ = C5_MODES[head_mode]
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
                              rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")),
-                             certify=cert_on, delta=delta_src)
+                             certify=cert_on, delta=delta_src, overlap=a.c5_overlap)
     chunk = C5_FS * 60
     pool = []
     for j in range(4):  # seeded 1-minute chunks: noise + meteor pings at +1 kHz, int16 I/Q interleaved
@@ -306,7 +310,7 @@ def run_c5(a, ctx, job, rank, world):
         return det.detect(comm, thresholds=False, exact_decisions=C5_MODES[mode[0]][2])
 
     def sync_all():
-        ctx.synchronize()
+        det.synchronize()
         if job is not None:
             job.barrier()
 
@@ -330,13 +334,21 @@ def run_c5(a, ctx, job, rank, world):
     k_ms, k_n = ctx.timing_get(_lib.K_CSTFT)
     ctx.timing_select(None)
     ctx.timing_reset()
+    dctx = det.dctx if det.dctx is not ctx else None
+    if dctx is not None:  # the detector's own context (overlap)
+        dctx.timing(True)
+        dctx.timing_reset()
     step()
     sync_all()
     kms = {}
     for name, kid in (("cstft", _lib.K_CSTFT), ("band_delta", _lib.K_IQDELTA), ("fresh_thresholds", _lib.K_FRESH),
                       ("scan", _lib.K_SSCAN), ("delta64", _lib.K_REFINE)):
         ms, cnt = ctx.timing_get(kid)
+        if dctx is not None:
+            ms += dctx.timing_get(kid)[0]
         kms[name] = round(ms, 4)
+    if dctx is not None:
+        dctx.timing(False)
     kms["cstft"] = round(k_ms / max(k_n, 1), 4)  # the timed region's average
 
     def cert_info(r, m):
@@ -401,6 +413,7 @@ def run_c5(a, ctx, job, rank, world):
         # the headline's decision mode (C5_MODES): exact = the drop-in default, every frame's delta
         # float64 from the samples and every decision certified; "modes" times the others
         "decisions": head_mode,
+        "detector_overlap": a.c5_overlap,
         "roofline": {"bound": "hbm", "achieved": round(alg_bytes / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": c5_traffic[0], "traffic_source": c5_traffic[1],

@@ -74,10 +74,14 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
  * front instead of only where a scan reads it (A/B of that scheme; results must agree; also
  * set by MSD_FRESH_ALL=1 in the environment).
  * MSD_OPT_REFINE_GOERTZEL = 1 → msd_iq_delta64_dev computes int16 blocks with the float64
- * Goertzel kernel instead of the exact int8-MFMA one (A/B; both within their bounds). */
+ * Goertzel kernel instead of the exact int8-MFMA one (A/B; both within their bounds).
+ * MSD_OPT_CSTFT_RESERVE = n → the persistent C5 spectrogram kernel (msd_cstft_psd_dev) leaves n
+ * of its resident workgroup slots free, so that small kernels on another context's stream (the
+ * stream detector, when its delta does not come from the spectrogram) run beside it. */
 #define MSD_OPT_GENERIC_STFT 1
 #define MSD_OPT_FRESH_ALL 2
 #define MSD_OPT_REFINE_GOERTZEL 3
+#define MSD_OPT_CSTFT_RESERVE 4
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.

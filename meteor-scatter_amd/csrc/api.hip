@@ -248,6 +248,10 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
         case MSD_OPT_GENERIC_STFT: ctx->force_generic = value != 0; return MSD_OK;
         case MSD_OPT_FRESH_ALL: ctx->fresh_all = value != 0; return MSD_OK;
         case MSD_OPT_REFINE_GOERTZEL: ctx->refine_goertzel = value != 0; return MSD_OK;
+        case MSD_OPT_CSTFT_RESERVE:
+            if (value < 0) return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_CSTFT_RESERVE must be >= 0");
+            ctx->cstft_reserve = value;
+            return MSD_OK;
         default: return fail(MSD_ERR_INVALID, "msd_set_option: unknown option");
     }
 }

@@ -389,7 +389,8 @@ int msd_cstft_psd_energy_dev(msd_cstft_plan *p, const void *x, int dtype, const 
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, CS_T, 0) != hipSuccess || per_cu < 1)
             per_cu = 3;
-        int64_t wgs = (int64_t)p->ctx->num_cu * per_cu;
+        int64_t wgs = (int64_t)p->ctx->num_cu * per_cu - p->ctx->cstft_reserve;
+        if (wgs < 1) wgs = 1;
         if (wgs > total) wgs = total;
         int64_t per = (total + wgs - 1) / wgs;
         if (etot) per = (per + 3) / 4 * 4;  // energy groups of 4 frames start at every workgroup's first

@@ -65,6 +65,7 @@ struct msd_ctx {
     void *i8_tab = nullptr;
     uint64_t i8_key = 0;
     bool refine_goertzel = false;  // MSD_OPT_REFINE_GOERTZEL: int16 refinement on the float64 Goertzel
+    int cstft_reserve = 0;         // MSD_OPT_CSTFT_RESERVE: workgroup slots the C5 spectrogram leaves free
 };
 
 struct msd_stft_plan {

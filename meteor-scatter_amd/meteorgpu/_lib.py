@@ -39,6 +39,7 @@ K_IQDELTA, K_FRESH, K_SSCAN, K_REFINE = 7, 8, 9, 10
 OPT_GENERIC_STFT = 1
 OPT_FRESH_ALL = 2
 OPT_REFINE_GOERTZEL = 3
+OPT_CSTFT_RESERVE = 4
 COMM_ID_BYTES = 128
 
 

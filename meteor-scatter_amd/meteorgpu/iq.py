@@ -186,7 +186,7 @@ class IQShardDetector:
                  threshold_freeze_before_detection_sec=3, threshold_freeze_after_detection_sec=20,
                  threshold_fixed_init_duration_sec=10, rank: int = 0, world: int = 1, dtype=np.int16,
                  seg_len: int = 8192, chunk_frames: int | None = None, certify: bool = True,
-                 delta: str = "auto"):
+                 delta: str = "auto", overlap: int = 0):
         """chunk_frames: keep only that many frames of spectrogram in HBM and stream the shard through
         it (``process_host``); the detector still sees the whole shard's delta.  A 24 h 192 kHz
         stream (66 GB of int16 I/Q, 265 GB of spectrogram) then runs on one GPU.
@@ -196,7 +196,12 @@ class IQShardDetector:
         certifying int16 input whose geometry the exact integer DFT on the matrix cores covers
         (REFINE_INT8_MFMA: blocks of 1024 samples, <= 10 bins, no band at 0 Hz -- C5), else fp32.
         With the exact delta every frame's error bound is ~1e-13 dB, so certification settles every
-        decision in one pass (no energy partials, no refinement, no second detector pass)."""
+        decision in one pass (no energy partials, no refinement, no second detector pass).
+        overlap: run the stream detector on a second context (own HIP stream) and let the
+        spectrogram leave that many workgroup slots free (MSD_OPT_CSTFT_RESERVE): with the exact
+        delta the detector does not need the spectrogram, so its latency-bound kernels and host
+        round trips run beside it (the exact delta first, then the spectrogram and the detector
+        concurrently).  0: one stream, in order."""
         self.ctx, self.fs, self.N = ctx, fs, int(nperseg)
         self.hop = self.N - int(noverlap)
         self.block_sec = self.hop / fs
@@ -227,7 +232,11 @@ class IQShardDetector:
         self.d_frames = ctx.alloc(8)
         self.d_frames.upload(np.array([self.batch.T if self.s1 > self.s0 else 0], np.int64))
         cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
-        self.plan = _lib.StreamPlan(ctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
+        self.overlap = int(overlap)
+        self.dctx = ctx.sibling() if self.overlap > 0 else ctx  # the detector's context
+        if self.overlap > 0:
+            ctx.set_option(_lib.OPT_CSTFT_RESERVE, self.overlap)
+        self.plan = _lib.StreamPlan(self.dctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
         self.ops = _stream.DeviceStreamOps(self.plan)
         self.d_etot = None
         self.certify = False
@@ -264,16 +273,24 @@ class IQShardDetector:
         self._refined = []
         if self.f1 > self.f0:
             if self.exact_delta:
-                self.batch.run()
+                # the exact delta first: the detector (on dctx) then runs beside the spectrogram
                 self._delta_exact(self.batch.n, self.f1 - self.f0, 0)
+                self._detector_ready()
+                self.batch.run()
             else:
                 etot = self.d_etot if self.certify else None
                 self.batch.run(etot)
                 _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                        self.noise, self.plan.d_delta, self.batch.T, etot=etot,
                                        ed=self.plan.d_ed if self.certify else None)
+                self._detector_ready()
         if self.exact_delta:
             self._refined = [[0, self.T]]  # every rank's frames are float64 (the ranks agree on this list)
+
+    def _detector_ready(self):
+        """the detector's context waits for the delta enqueued on the spectrogram's"""
+        if self.dctx is not self.ctx:
+            self.dctx.wait_for(self.ctx)
 
     def _delta_exact(self, n_samples: int, nframes: int, c0: int):
         """float64 delta and bound of the local frames [c0, c0 + nframes), whose samples start at the
@@ -307,8 +324,8 @@ class IQShardDetector:
             b = a + (nf - 1) * self.hop + self.N
             self.batch.upload(0, np.ascontiguousarray(read(a, b)))
             if self.exact_delta:
-                self.batch.run()  # frames past nf read stale samples; the spectrogram is the product
                 self._delta_exact(b - a, nf, c0)
+                self.batch.run()  # frames past nf read stale samples; the spectrogram is the product
                 continue
             self.d_frames.upload(np.array([nf], np.int64))
             etot = self.d_etot if self.certify else None
@@ -317,6 +334,7 @@ class IQShardDetector:
             _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                    self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T,
                                    etot=etot, ed=ed)
+        self._detector_ready()
         if self.exact_delta:
             self._refined = [[0, self.T]]
 
@@ -406,7 +424,7 @@ class IQShardDetector:
         if not len(loc):
             return
         if not self.chunk:  # the shard's samples are resident: frame j at sample j * hop
-            _lib.iq_delta64_dev(self.ctx, self.batch.d_x, self.batch.code, self.batch.n, self.N, self.hop, self.fs_,
+            _lib.iq_delta64_dev(self.dctx, self.batch.d_x, self.batch.code, self.batch.n, self.N, self.hop, self.fs_,
                                 self.band, self.noise, np.array(loc, np.int64), self.plan.d_delta, self.plan.d_ed)
             return
         # chunked: re-read each range's samples (<= chunk frames at a time) into the batch buffer
@@ -414,17 +432,28 @@ class IQShardDetector:
             for c in range(a, b, self.chunk):
                 e = min(b, c + self.chunk)
                 s0, s1 = c * self.hop, (e - 1) * self.hop + self.N
+                self.synchronize()  # every kernel reading the batch buffer (both contexts) has finished
                 self.batch.upload(0, np.ascontiguousarray(self._read(s0, s1)))
-                _lib.iq_delta64_dev(self.ctx, self.batch.d_x, self.batch.code, s1 - s0, self.N, self.hop, self.fs_,
+                _lib.iq_delta64_dev(self.dctx, self.batch.d_x, self.batch.code, s1 - s0, self.N, self.hop, self.fs_,
                                     self.band, self.noise, np.array([[0, e - c]], np.int64),
                                     _lib.C.c_void_p(self.plan.d_delta.value + 8 * c),
                                     _lib.C.c_void_p(self.plan.d_ed.value + 8 * c))
 
+    def synchronize(self):
+        """both contexts' work (spectrogram and detector) finished"""
+        self.ctx.synchronize()
+        if self.dctx is not self.ctx:
+            self.dctx.synchronize()
+
     def close(self):
+        self.synchronize()
         self.plan.close()
         self.batch.close()
         if self.d_etot is not None:
             self.d_etot.free()
+        if self.dctx is not self.ctx:
+            self.dctx.close()
+            self.ctx.set_option(_lib.OPT_CSTFT_RESERVE, 0)
 
 
 def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072, threshold_std_factor=4.0,

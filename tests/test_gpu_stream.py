@@ -642,3 +642,38 @@ def test_native_local_path_errors():
     d[-2], d[-1] = -50.0, 50.0  # one block above at the end: t_dur == 0 (main.py:437)
     with pytest.raises(AssertionError):
         stream.detect_stream(ctx, d, d.size, 0, adaptive=False, k_std=4.0)
+
+
+@pytest.mark.parametrize("chunk", [None, 1500])
+def test_overlapped_detector_matches_in_order(chunk):
+    """IQShardDetector(overlap=n): the exact delta first, then the spectrogram with n workgroup slots
+    left free and the stream detector on a second context beside it -- the same detections, dB
+    values and delta bit for bit as one in-order stream, and the same spectrogram (also when the
+    shard streams through HBM in chunks)"""
+    from meteorgpu import _lib, iq, synth
+    i, q, _ = synth.synth_iq(12, 192000, 30.0, 1000.0, rate_per_min=20)
+    buf, _ = iq.interleave(i, q)
+    kw = dict(threshold_estimation_window_sec=5, threshold_freeze_after_detection_sec=2,
+              threshold_fixed_init_duration_sec=1)
+    out = []
+    for ov in (0, 16):
+        ctx = _lib.Context(0)
+        try:
+            det = iq.IQShardDetector(ctx, i.size, 192000, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
+                                     5, 3, 2, 1, chunk_frames=chunk, overlap=ov)
+            try:
+                assert det.exact_delta
+                det.process_host(buf[2 * det.s0: 2 * det.s1])
+                res = det.detect()
+                det.synchronize()
+                spec = det.batch.frames(0, 0, 16) if chunk is None else None
+                out.append((res, det.plan.delta(), spec))
+            finally:
+                det.close()
+        finally:
+            ctx.close()
+    (a, da, sa), (b, db, sb) = out
+    assert a.certified and b.certified and len(a.detections) > 5
+    assert np.array_equal(a.detections, b.detections) and np.array_equal(da, db)
+    if chunk is None:
+        assert np.array_equal(sa, sb)
