@@ -348,7 +348,8 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
             const double a = -2.0 * M_PI * (double)m / (double)N;
             rt[(size_t)b * R + j] = make_double2(std::cos(a), std::sin(a));
         }
-    const size_t nb_blk = (sizeof(double2) * (size_t)nblocks * (K.nk + 2) + 255) / 256 * 256;
+    // + 64 scratch entries past the table: block_i8_kernel's lanes without a value store there
+    const size_t nb_blk = (sizeof(double2) * ((size_t)nblocks * (K.nk + 2) + 64) + 255) / 256 * 256;
     const size_t nb_rot = (sizeof(double2) * rt.size() + 255) / 256 * 256;
     const size_t nb_meta = sizeof(int64_t) * (4 * (size_t)nranges + 2);
     void *d = nullptr;

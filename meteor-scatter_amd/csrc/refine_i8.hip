@@ -11,21 +11,25 @@
 // block's bin is off by at most sqrt 2 * 2^-47 * sum (|I| + |Q|) -- 90.5 u (u = 2^-53) against the
 // float64 Goertzel's ~3 L / |sin theta| u (~6000 u at C5) -- before the float64 combination.
 //
-// GEMM shape per 16-row tile = one block of 1024 complex samples: rows = 16 sub-blocks of 64
-// samples, K = 128 (the sub-block's I, Q values interleaved as they sit in memory), columns = the
-// needed bins' real and imaginary parts times the six digits, packed in NT tiles of 16 columns:
+// GEMM shape per 16-row tile = four consecutive compact blocks of 1024 complex samples: row
+// 4 b + s = sub-block s (256 samples) of block b, K = 512 (the sub-block's I, Q values interleaved
+// as they sit in memory, 8 K steps of 64), columns = the needed bins' real and imaginary parts
+// times the six digits, packed in NT tiles of 16 columns:
 //   tiles 0..5: column c = component c (bin c >> 1, part c & 1) of bins 0..7, digit = tile;
-//   tile 6 + e: bin 8 + e, part c >> 3, digit c & 7 (< 6; columns with digit 6, 7 are zero).
-// A lane of the result (column c = lane & 15, rows 4 (lane >> 4) + r) thus holds all six digits of
-// its component in its own registers (tiles 0..5), and the extra bins' digits spread over 8 lanes.
-// The sub-block partials P_s (s = 0..15) combine to the block's bin with float64 twiddles
-// W^{64 k s}: each lane multiplies its 4 rows and the four lane groups are summed.  The output is
-// refine.hip's bin-major block table, which frame_kernel turns into frames, delta and ed.
+//   tile 6 + e: bin 8 + e, part c >> 3, digit c & 7 (< 6); tile 6's columns 6, 7: ones on I, Q.
+// A lane of the result (column c = lane & 15, rows 4 (lane >> 4) + r) thus holds, for block
+// lane >> 4, all four sub-blocks and all six digits of its component (tiles 0..5) in its own
+// registers: the sub-block partials combine with float64 twiddles W^{256 k s} without a
+// cross-lane sum; the extra bins' digits spread over 8 lanes of the half-row (3 DPP adds).  With
+// K = 512 the digit products reach 2^31 in the worst case, so 256 h_d + l_d is formed in float64
+// (exact) rather than int32.  The output is refine.hip's bin-major block table, which
+// frame_kernel turns into frames, delta and ed.
 //
-// One wave per contiguous range of compact blocks, 2 waves per SIMD (~220 VGPRs: the B fragments
-// of every tile, 56, stay in registers for the kernel's lifetime; the next block's samples are
-// loaded while the current one is reduced).  Bound by HBM (4 KB of samples per block) and the
-// float64 reduction; the matrix cores run 28 MFMAs (448 cycles) per block.
+// One wave per contiguous range of tiles, 2 waves per SIMD (~200 VGPRs: 56 accumulators, the
+// next tile's 256 B of samples per lane in flight); the B fragments (NT x 8 KB), lane twiddles and
+// column offsets sit in LDS.  Per block: 28 MFMAs (~850 cycles of the matrix core), 4 KB of
+// samples from HBM, ~30 float64 VALU ops per lane.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -40,8 +44,10 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int I8_ND = 6;     // twiddle digits
-constexpr int I8_SB = 16;    // sub-blocks per block (rows of the tile)
-constexpr int I8_SUB = 64;   // complex samples per sub-block
+constexpr int I8_BPT = 4;    // blocks per 16-row tile
+constexpr int I8_SB = 4;     // sub-blocks per block (rows of the tile per block)
+constexpr int I8_SUB = 256;  // complex samples per sub-block
+constexpr int I8_KS = 8;     // K steps of 64 int16 values per sub-block row (2 I8_SUB values)
 
 __device__ __forceinline__ int find_range_i8(const int64_t *cs, int nr, int64_t g) {
     int lo = 0, hi = nr - 1;
@@ -61,16 +67,6 @@ __device__ __forceinline__ double dpp64(double x) {
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
-struct Raw {
-    v4u a, b, c, d;  // the lane's 64 bytes: int16 values 32 q .. 32 q + 31 of its row
-};
-
-__device__ __forceinline__ Raw load_raw(const int16_t *tile, int l) {
-    const v4u *p = reinterpret_cast<const v4u *>(tile) + (l & 15) * 16 + (l >> 4) * 4;
-    return Raw{__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2),
-               __builtin_nontemporal_load(p + 3)};
-}
-
 // the A fragments of K step ks from the lane's dwords w[8 ks .. 8 ks + 7] (values 16 ks .. 16 ks + 15
 // of its chunk): the high bytes (h = x >> 8) and the low bytes minus 128 (l' = (x & 255) ^ 0x80 as int8)
 __device__ __forceinline__ void digits(const uint32_t *w, v4i &hi, v4i &lo, uint32_t &habs) {
@@ -85,23 +81,7 @@ __device__ __forceinline__ void digits(const uint32_t *w, v4i &hi, v4i &lo, uint
     }
 }
 
-// f64 sums of lane l and lane l ^ 16 / l ^ 32 (v_permlane16/32_swap: VALU, no LDS round trip)
-__device__ __forceinline__ double add_xor16(double x) {
-    const long long v = __builtin_bit_cast(long long, x);
-    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)(v & 0xffffffffll), (unsigned)(v & 0xffffffffll), false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
-    const double a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
-    const double b = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
-    return a + b;
-}
-__device__ __forceinline__ double add_xor32(double x) {
-    const long long v = __builtin_bit_cast(long long, x);
-    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)(v & 0xffffffffll), (unsigned)(v & 0xffffffffll), false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
-    const double a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
-    const double b = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
-    return a + b;
-}
+// int sums of lane l and lane l ^ 16 / l ^ 32 (v_permlane16/32_swap: VALU, no LDS round trip)
 __device__ __forceinline__ int add_xor16_i(int v) {
     const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
     return (int)(r[0] + r[1]);
@@ -119,9 +99,8 @@ struct Acc {
 // out (bin-major, refine.hip's block table): out[b * nblocks + g] = B_g[k_b] for b < nk, then the
 // block's sample sum (b = nk) and an upper bound of sum (|re| + |im|) (b = nk + 1, .x)
 //
-// Software-pipelined: while the VALU reduces block g from one accumulator set, the matrix cores
-// run block g + 1's 28 MFMAs into the other (the two sets, 112 VGPRs, are why the B fragments
-// live in LDS: 14 ds_read_b128 per block); the next block's samples are loaded one block ahead.
+// A wave walks its contiguous range of compact blocks four at a time (one 16-row tile); the next
+// tile's samples are requested K step by K step as the current one's are turned into digits.
 template <int NT>
 __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restrict__ x, int64_t D,
                                                           const int64_t *__restrict__ bstart,
@@ -130,132 +109,166 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
                                                           const int *__restrict__ colinit,
                                                           const double2 *__restrict__ ltw, double2 *__restrict__ out) {
     constexpr int NX = NT - 6;  // extra bins (8 + e), two components each, in tiles 6 ..
-    __shared__ v4i sB[NT * 2 * 64];
-    for (int i = threadIdx.x; i < NT * 2 * 64; i += 256) sB[i] = bfrag[i];
+    __shared__ v4i sB[NT * I8_KS * 64];
+    // per column: the lane twiddles (below) and the K offsets' column sums, read where used
+    __shared__ double2 sTw[(1 + NX) * I8_SB * 16];
+    __shared__ int sInit[NT * 16];
+    for (int i = threadIdx.x; i < NT * I8_KS * 64; i += 256) sB[i] = bfrag[i];
+    for (int i = threadIdx.x; i < (1 + NX) * I8_SB * 16; i += 256) sTw[i] = ltw[i];
+    for (int i = threadIdx.x; i < NT * 16; i += 256) sInit[i] = colinit[i];
     __syncthreads();
     const int l = threadIdx.x & 63;
-    const int c = l & 15;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int c = l & 15, grp = l >> 4;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform
     const int64_t g0 = wave * per_wave;
     const int64_t g1 = g0 + per_wave < nblocks ? g0 + per_wave : nblocks;
     if (g0 >= g1) return;
-    int cinit[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) cinit[t] = colinit[t * 16 + c];
-    // this lane's sub-block twiddles W^{64 k s} (s = 4 (l >> 4) + r) for its component's bin, the
-    // imaginary part signed by the component (re: +, im: -), and the same for its extra bins
-    double2 tw[1 + NX][4];
-#pragma unroll
-    for (int e = 0; e <= NX; ++e)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tw[e][r] = ltw[(e * 4 + r) * 64 + l];
+    // sTw[(e * I8_SB + r) * 16 + c]: column c's sub-block twiddle W^{256 k r} (a lane's C rows r =
+    // 0..3 are the 4 sub-blocks of block grp) for its component's bin, the imaginary part signed by
+    // the component (re: +, im: -); e > 0: the same for extra bin 8 + e - 1
+    auto tw = [&](int e, int r) { return sTw[(e * I8_SB + r) * 16 + c]; };
     const int ncomp = 2 * (nk < 8 ? nk : 8);
     const int dg = c & 7;  // extra tiles: this lane's digit (6, 7: the sum columns / zero)
     const double xscale = dg < 6 ? __builtin_ldexp(1.0, -6 - 8 * dg) : 0.0;
-    auto block_at = [&](int64_t g) {
-        const int r = find_range_i8(bcs, nr, g);
-        return bstart[r] + (g - bcs[r]);
+    // the lane's A row (l & 15) = sub-block (l & 3) of the tile's block (l & 15) >> 2; in K step ks
+    // its 16 values are the row's bytes 128 ks + 16 (l >> 4) and 128 ks + 64 + 16 (l >> 4), 16 each:
+    // each load instruction reads 64 contiguous bytes per row.  The compact-block -> sample-block
+    // map is walked forward by the wave for the tile's four blocks (uniform: scalar loads, ranges
+    // only ever advance).  No vector load but the samples' in the loop: a wait for one would also
+    // wait for the prefetched samples.
+    const int ab = (l & 15) >> 2, as = l & 3;
+    int rr = find_range_i8(bcs, nr, g0);
+    int64_t rend = bcs[rr + 1], rbase = bstart[rr] - bcs[rr];
+    auto src = [&](int64_t gt) {
+        int64_t mb[I8_BPT];
+#pragma unroll
+        for (int b = 0; b < I8_BPT; ++b) {
+            const int64_t gb = gt + b < g1 ? gt + b : g1 - 1;
+            while (gb >= rend) {
+                ++rr;
+                rend = bcs[rr + 1];
+                rbase = bstart[rr] - bcs[rr];
+            }
+            mb[b] = rbase + gb;
+        }
+        const int64_t m = ab == 0 ? mb[0] : ab == 1 ? mb[1] : ab == 2 ? mb[2] : mb[3];
+        return reinterpret_cast<const v4u *>(x + 2 * (m * D + as * I8_SUB)) + grp;
     };
-    // the MFMAs of one block from its raw samples (sum |h| into habs)
-    auto matmul = [&](const Raw &raw, Acc<NT> &A, uint32_t &habs) __attribute__((always_inline)) {
-        uint32_t w[16];
-        __builtin_memcpy(w, &raw, 64);
-        v4i ah[2], al[2];
-        habs = 0;
-        digits(w, ah[0], al[0], habs);
-        digits(w + 8, ah[1], al[1], habs);
+    v4u raw[2 * I8_KS];
+    {
+        const v4u *p = src(g0);
+#pragma unroll
+        for (int ks = 0; ks < I8_KS; ++ks) {
+            raw[2 * ks] = __builtin_nontemporal_load(p + 8 * ks);
+            raw[2 * ks + 1] = __builtin_nontemporal_load(p + 8 * ks + 4);
+        }
+    }
+    for (int64_t gt = g0; gt < g1; gt += I8_BPT) {
+        // the next tile (the last one reloads itself: no branch inside the unrolled K loop)
+        const v4u *pn = src(gt + I8_BPT < g1 ? gt + I8_BPT : gt);
+        Acc<NT> A;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             A.h[t] = v4i{0, 0, 0, 0};
-            A.l[t] = v4i{cinit[t], cinit[t], cinit[t], cinit[t]};
+            const int ci = sInit[t * 16 + c];
+            A.l[t] = v4i{ci, ci, ci, ci};
         }
+        uint32_t habs = 0;
+        // the B fragments are the same for every tile: an opaque offset keeps the compiler from
+        // hoisting all NT * I8_KS of them (4 VGPRs each) out of the loop
+        int boff = l;
+        asm volatile("" : "+v"(boff));
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < I8_KS; ++ks) {
+            // the step's B fragments requested first: their LDS latency runs under the digit
+            // extraction and the earlier tiles' MFMAs instead of one round trip per MFMA pair
+            v4i bk[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bk[t] = sB[(t * I8_KS + ks) * 64 + boff];
+            uint32_t w[8];
+            __builtin_memcpy(w, &raw[2 * ks], 32);
+            v4i ah, al;
+            digits(w, ah, al, habs);
+            raw[2 * ks] = __builtin_nontemporal_load(pn + 8 * ks);
+            raw[2 * ks + 1] = __builtin_nontemporal_load(pn + 8 * ks + 4);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const v4i b = sB[(t * 2 + ks) * 64 + l];
-                A.h[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[ks], b, A.h[t], 0, 0, 0);
-                A.l[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], b, A.l[t], 0, 0, 0);
+                A.h[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bk[t], A.h[t], 0, 0, 0);
+                A.l[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bk[t], A.l[t], 0, 0, 0);
             }
-    };
-    // the float64 reduction of one block and its stores
-    auto reduce = [&](const Acc<NT> &A, uint32_t habs, int64_t g) __attribute__((always_inline)) {
-        // this lane's component: P_s = 2^-6 sum_d 2^-8d (256 h_d + l_d) by Horner from the lowest digit
-        // (its first steps exact), then the twiddled sum over the lane's 4 rows with the partner
-        // component (lane ^ 1; the sign rides in tw.y)
+        }
+        // float64: this lane's component of block gt + grp.  Per sub-block P_r = 2^-6 sum_d 2^-8d
+        // (256 h_d + l_d) (each digit term exact; Horner from the lowest digit, its first steps
+        // exact), then the twiddled sum over the 4 sub-blocks with the partner component (lane ^ 1;
+        // the sign rides in tw.y).  No cross-lane sum: the lane holds its whole block.
         double ym = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double p = (double)((A.h[5][r] << 8) + A.l[5][r]);
+        for (int r = 0; r < I8_SB; ++r) {
+            double p = __builtin_fma(256.0, (double)A.h[5][r], (double)A.l[5][r]);
 #pragma unroll
-            for (int d = 4; d >= 0; --d) p = __builtin_fma(p, 0x1p-8, (double)((A.h[d][r] << 8) + A.l[d][r]));
+            for (int d = 4; d >= 0; --d)
+                p = __builtin_fma(p, 0x1p-8, __builtin_fma(256.0, (double)A.h[d][r], (double)A.l[d][r]));
             p *= 0x1p-6;
             const double q = dpp64<0xB1>(p);
-            ym = __builtin_fma(p, tw[0][r].x, ym);
-            ym = __builtin_fma(q, tw[0][r].y, ym);
+            const double2 w = tw(0, r);
+            ym = __builtin_fma(p, w.x, ym);
+            ym = __builtin_fma(q, w.y, ym);
         }
-        ym = add_xor32(add_xor16(ym));  // the four lane groups (rows 0-3, 4-7, 8-11, 12-15)
         // extra bins: each lane one digit of one component; twiddle its rows (partner: lane ^ 8,
-        // same digit), scale, then sum the 6 digit lanes of the half-row and the lane groups
+        // same digit), scale, then sum the 6 digit lanes of the half-row
         double yx[NX > 0 ? NX : 1];
-        int32_t bsum = 0;
+        uint32_t bsum = 0;
 #pragma unroll
         for (int e = 0; e < NX; ++e) {
             double acc = 0.0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int32_t tv = (A.h[6 + e][r] << 8) + A.l[6 + e][r];
-                if (e == 0) bsum += tv;  // columns 6 / 7 of tile 6: the sub-block sums of I / Q
-                const double v = (double)tv;
+            for (int r = 0; r < I8_SB; ++r) {
+                // columns 6 / 7 of tile 6: the sub-block sums of I / Q, exact in int32 (|.| <= 2^23)
+                if (e == 0) bsum += ((uint32_t)A.h[6][r] << 8) + (uint32_t)A.l[6][r];
+                const double v = __builtin_fma(256.0, (double)A.h[6 + e][r], (double)A.l[6 + e][r]);
                 const double u = dpp64<0x128>(v);  // row_ror:8 -- the other component, same digit
-                acc = __builtin_fma(v, tw[1 + e][r].x, acc);
-                acc = __builtin_fma(u, tw[1 + e][r].y, acc);
+                const double2 w = tw(1 + e, r);
+                acc = __builtin_fma(v, w.x, acc);
+                acc = __builtin_fma(u, w.y, acc);
             }
             acc *= xscale;  // 0 on the lanes without a digit
             acc += dpp64<0xB1>(acc);  // the 8 lanes of the half-row: xor 1, xor 2, mirror
             acc += dpp64<0x4E>(acc);
             acc += dpp64<0x141>(acc);
-            yx[e] = add_xor32(add_xor16(acc));
+            yx[e] = acc;
         }
-        if constexpr (NX > 0) bsum = add_xor32_i(add_xor16_i(bsum));
-        const int hsum = wave_sum_i((int)habs);
-        if (l < 16) {
-            double *o = reinterpret_cast<double *>(out);
-            if (c < ncomp) o[2 * ((int64_t)(c >> 1) * nblocks + g) + (c & 1)] = ym;
+        // sum |h| per block: the A rows of block b are lanes with (l >> 2) & 3 == b -- sum over lane
+        // bits 0, 1 (quad DPP) and 4, 5 (lane groups); lane c == 4 grp then holds block grp's
+        int hs = (int)habs;
+        hs += __builtin_amdgcn_mov_dpp(hs, 0xB1, 0xf, 0xf, true);
+        hs += __builtin_amdgcn_mov_dpp(hs, 0x4E, 0xf, 0xf, true);
+        hs = add_xor32_i(add_xor16_i(hs));
+        // stores without branches (every lane stores; the ones without a value write their own slot
+        // of the 64-entry scratch row past the table): a fixed number of store instructions per tile
+        // lets the compiler wait for the next tile's samples with vmcnt(stores) instead of vmcnt(0),
+        // i.e. without a store round trip per tile
+        const int64_t g = gt + grp;
+        const bool ok = g < g1;
+        double *o = reinterpret_cast<double *>(out);
+        double *const dump = reinterpret_cast<double *>(out + (int64_t)(nk + 2) * nblocks + l);
+        auto put = [&](bool want, int64_t row, int part, double v) __attribute__((always_inline)) {
+            *(want && ok ? o + 2 * (row * nblocks + g) + part : dump) = v;
+        };
+        put(c < ncomp, c >> 1, c & 1, ym);
 #pragma unroll
-            for (int e = 0; e < NX; ++e)
-                if (dg == 0) o[2 * ((int64_t)(8 + e) * nblocks + g) + (c >> 3)] = yx[e];
-            // sum (|I| + |Q|) <= 256 (sum |h| + values): x = 256 h + (x & 255).  frame_kernel bounds the
-            // detrended frame's sum |v| by it plus N |mean|, the mean from the block sums (NX > 0:
-            // exact; else unknown, the sum row 0 and the bound doubled instead, N |mean| <= sum |x|)
-            const double l1 = 256.0 * ((double)hsum + 2.0 * D);
-            if constexpr (NX > 0) {
-                if (c == 6 || c == 7) o[2 * ((int64_t)nk * nblocks + g) + (c - 6)] = (double)bsum;
-                if (l == 0) out[(int64_t)(nk + 1) * nblocks + g] = make_double2(l1, 0.0);
-            } else if (l == 0) {
-                out[(int64_t)nk * nblocks + g] = make_double2(0.0, 0.0);
-                out[(int64_t)(nk + 1) * nblocks + g] = make_double2(2.0 * l1, 0.0);
-            }
+        for (int e = 0; e < NX; ++e) put(dg == 0, 8 + e, c >> 3, yx[e]);
+        // sum (|I| + |Q|) <= 256 (sum |h| + values): x = 256 h + (x & 255).  frame_kernel bounds the
+        // detrended frame's sum |v| by it plus N |mean|, the mean from the block sums (NX > 0:
+        // exact; else unknown, the sum row 0 and the bound doubled instead, N |mean| <= sum |x|)
+        const double l1 = 256.0 * ((double)hs + 2.0 * D);
+        if constexpr (NX > 0) {
+            // lanes 6, 7: the I / Q block sums; lane 4 grp: the bound (its .y 0 from lane 4 grp + 1)
+            const bool sl = c == 6 || c == 7, bl = c == 4 * grp || c == 4 * grp + 1;
+            put(sl || bl, sl ? nk : nk + 1, sl ? c - 6 : c - 4 * grp, sl ? (double)(int32_t)bsum : c == 4 * grp ? l1 : 0.0);
+        } else {
+            const int cc = c - 4 * grp;  // lanes 4 grp .. 4 grp + 3: the sum row (0) and the bound row
+            put(cc >= 0 && cc < 4, cc < 2 ? nk : nk + 1, cc & 1, cc == 2 ? 2.0 * l1 : 0.0);
         }
-    };
-    Acc<NT> A0, A1;
-    uint32_t h0 = 0, h1 = 0;
-    Raw raw = load_raw(x + 2 * block_at(g0) * D, l);
-    matmul(raw, A0, h0);
-    if (g0 + 1 < g1) raw = load_raw(x + 2 * block_at(g0 + 1) * D, l);
-    for (int64_t g = g0; g < g1; g += 2) {
-        // block g in A0: block g + 1's MFMAs into A1 (its samples loaded), g + 2's samples requested
-        if (g + 1 < g1) {
-            matmul(raw, A1, h1);
-            if (g + 2 < g1) raw = load_raw(x + 2 * block_at(g + 2) * D, l);
-        }
-        reduce(A0, h0, g);
-        if (g + 1 >= g1) break;
-        if (g + 2 < g1) {
-            matmul(raw, A0, h0);
-            if (g + 3 < g1) raw = load_raw(x + 2 * block_at(g + 3) * D, l);
-        }
-        reduce(A1, h1, g + 1);
     }
 }
 
@@ -283,9 +296,9 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
     // host tables (B fragments, column starts, lane twiddles), built once per (N, bins) and kept
     uint64_t key = (uint64_t)N * 1000003u + (uint64_t)nk;
     for (int b = 0; b < nk; ++b) key = key * 1000003u + (uint64_t)K.km[b];
-    const size_t nb_frag = sizeof(v4i) * (size_t)NT * 2 * 64;
+    const size_t nb_frag = sizeof(v4i) * (size_t)NT * I8_KS * 64;
     const size_t nb_init = sizeof(int) * (size_t)NT * 16;
-    const size_t nb_tw = sizeof(double2) * (size_t)(1 + (NT - 6)) * 4 * 64;
+    const size_t nb_tw = sizeof(double2) * (size_t)(1 + (NT - 6)) * I8_SB * 16;
     const size_t nb_all = nb_frag + nb_init + nb_tw;
     if (ctx->i8_key != key || !ctx->i8_tab) {
         // column (t, c) -> (bin, part, digit), or -1
@@ -299,20 +312,21 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
         };
         // tile 6, columns 6 / 7: ones on the I / Q values (the sub-block sums, block_i8_kernel)
         auto sumcol = [&](int t, int cc) { return t == 6 && (cc == 6 || cc == 7); };
-        // B[t][v][c] for v = 0..127: value v of a sub-block row = sample v >> 1, I (v even) or Q
-        std::vector<int8_t> Bm((size_t)NT * 128 * 16, 0);
+        // B[t][v][c] for v < KV: value v of a sub-block row = sample v >> 1, I (v even) or Q
+        constexpr int KV = 2 * I8_SUB;
+        std::vector<int8_t> Bm((size_t)NT * KV * 16, 0);
         std::vector<int> init((size_t)NT * 16, 0);
         for (int t = 0; t < NT; ++t)
             for (int cc = 0; cc < 16; ++cc) {
                 if (sumcol(t, cc)) {
-                    for (int v = 0; v < 128; ++v) Bm[((size_t)t * 128 + v) * 16 + cc] = (v & 1) == cc - 6 ? 1 : 0;
-                    init[t * 16 + cc] = 128 * 64;
+                    for (int v = 0; v < KV; ++v) Bm[((size_t)t * KV + v) * 16 + cc] = (v & 1) == cc - 6 ? 1 : 0;
+                    init[t * 16 + cc] = 128 * I8_SUB;
                     continue;
                 }
                 int bin, part, dig;
                 if (!colmap(t, cc, bin, part, dig)) continue;
                 const int64_t km = K.km[bin];
-                for (int v = 0; v < 128; ++v) {
+                for (int v = 0; v < KV; ++v) {
                     const int64_t m = v >> 1;
                     const double a = 2.0 * M_PI * (double)((km * m) % N) / (double)N;
                     const double C = std::cos(a), S = std::sin(a);
@@ -320,34 +334,36 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
                     const double val = part == 0 ? ((v & 1) ? S : C) : ((v & 1) ? C : -S);
                     int8_t d[I8_ND];
                     balanced_digits((int64_t)std::llround(std::ldexp(val, 46)), d);
-                    Bm[((size_t)t * 128 + v) * 16 + cc] = d[dig];
+                    Bm[((size_t)t * KV + v) * 16 + cc] = d[dig];
                     init[t * 16 + cc] += 128 * (int)d[dig];
                 }
             }
         std::vector<char> tab(nb_all);
         auto *frag = reinterpret_cast<int8_t *>(tab.data());
         for (int t = 0; t < NT; ++t)
-            for (int ks = 0; ks < 2; ++ks)
+            for (int ks = 0; ks < I8_KS; ++ks)
                 for (int l = 0; l < 64; ++l)
-                    for (int j = 0; j < 16; ++j)  // lane l byte j: k = 16 (l >> 4) + j of step ks
-                        frag[(((size_t)t * 2 + ks) * 64 + l) * 16 + j] = Bm[((size_t)t * 128 + 32 * (l >> 4) + 16 * ks + j) * 16 + (l & 15)];
+                    for (int j = 0; j < 16; ++j) {  // lane l byte j of step ks (block_i8_kernel's loads)
+                        const int v = 64 * ks + 32 * (j >> 3) + 8 * (l >> 4) + (j & 7);
+                        frag[(((size_t)t * I8_KS + ks) * 64 + l) * 16 + j] = Bm[((size_t)t * KV + v) * 16 + (l & 15)];
+                    }
         std::memcpy(tab.data() + nb_frag, init.data(), nb_init);
         auto *ltw = reinterpret_cast<double2 *>(tab.data() + nb_frag + nb_init);
         for (int e = 0; e <= NT - 6; ++e)
-            for (int r = 0; r < 4; ++r)
-                for (int l = 0; l < 64; ++l) {
-                    const int cc = l & 15, s = 4 * (l >> 4) + r;
+            for (int r = 0; r < I8_SB; ++r)
+                for (int cc = 0; cc < 16; ++cc) {
+                    const int s = r;  // C row r of every lane group: sub-block r of its block
                     int bin, part;
                     if (e == 0) bin = cc >> 1, part = cc & 1;
                     else bin = 8 + (e - 1), part = cc >> 3;
                     double2 w = make_double2(0.0, 0.0);
                     if (bin < nk && (e > 0 || bin < 8)) {
-                        // W^{64 k s} = cos - i sin: own part p, partner q: re = p cos + q sin (own re),
+                        // W^{256 k s} = cos - i sin: own part p, partner q: re = p cos + q sin (own re),
                         // im = p cos - q sin (own im, partner re)
-                        const double a = 2.0 * M_PI * (double)(((int64_t)K.km[bin] * 64 * s) % N) / (double)N;
+                        const double a = 2.0 * M_PI * (double)(((int64_t)K.km[bin] * I8_SUB * s) % N) / (double)N;
                         w = make_double2(std::cos(a), part == 0 ? std::sin(a) : -std::sin(a));
                     }
-                    ltw[(e * 4 + r) * 64 + l] = w;
+                    ltw[(e * I8_SB + r) * 16 + cc] = w;
                 }
         DeviceGuard gd(ctx->device);
         MSD_HIP(hipStreamSynchronize(ctx->stream));
@@ -362,10 +378,10 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
     const v4i *d_frag = reinterpret_cast<const v4i *>(tb);
     const int *d_init = reinterpret_cast<const int *>(tb + nb_frag);
     const double2 *d_tw = reinterpret_cast<const double2 *>(tb + nb_frag + nb_init);
-    // persistent: 8 waves per CU (2 workgroups of 4), contiguous block ranges per wave
+    // persistent: 8 waves per CU (2 workgroups of 4), contiguous ranges of whole tiles per wave
     const int64_t waves_max = (int64_t)ctx->num_cu * 8;
-    int64_t per = (nblocks + waves_max - 1) / waves_max;
-    if (per < 1) per = 1;
+    const int64_t ntiles = (nblocks + I8_BPT - 1) / I8_BPT;
+    const int64_t per = I8_BPT * std::max<int64_t>(1, (ntiles + waves_max - 1) / waves_max);
     const int64_t waves = (nblocks + per - 1) / per;
     const unsigned grid = (unsigned)((waves + 3) / 4);
     hipStream_t st = ctx->stream;
@@ -389,8 +405,9 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
 }
 
 // our float64-side rounding chain in units of u = 2^-53 (refine_plan.h's `own`): the twiddles'
-// quantisation sqrt 2 * 2^-47 per unit |x| (90.5), the digit Horner sum (6), the 16 sub-block
-// products summed with rounded twiddles over two lane levels (16 + 6)
+// quantisation sqrt 2 * 2^-47 per unit |x| (90.5), the digit Horner sum (6), the 4 sub-block
+// products summed with rounded twiddles in one 8-FMA chain (10; the budget kept at 22, the
+// 16-sub-block layout's figure)
 double i8_chain_own() { return 91.0 + 6.0 + 22.0; }
 
 }  // namespace msd

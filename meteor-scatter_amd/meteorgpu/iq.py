@@ -122,33 +122,39 @@ def frame_shard(n_samples: int, nperseg: int, hop: int, rank: int, world: int):
 
 
 def _as_iv(iv) -> np.ndarray:
-    a = np.asarray(list(iv) if not isinstance(iv, np.ndarray) else iv, dtype=np.int64)
-    return a.reshape(-1, 2)
+    if isinstance(iv, np.ndarray):
+        return iv.astype(np.int64, copy=False).reshape(-1, 2)
+    return np.asarray(list(iv), dtype=np.int64).reshape(-1, 2)
 
 
-def _merge(iv) -> list:
-    """sorted, merged [a, b) intervals (touching ones joined), as a list of [a, b]"""
+_NO_IV = np.zeros((0, 2), np.int64)
+
+
+def _merge_a(iv) -> np.ndarray:
+    """sorted, merged [a, b) intervals (touching ones joined), as an (n, 2) int64 array"""
     a = _as_iv(iv)
     a = a[a[:, 1] > a[:, 0]]
     if a.size == 0:
-        return []
+        return _NO_IV
     a = a[np.argsort(a[:, 0], kind="stable")]
     ends = np.maximum.accumulate(a[:, 1])
     new = np.ones(len(a), bool)
     new[1:] = a[1:, 0] > ends[:-1]  # a start past every earlier end opens a new interval
     heads = np.flatnonzero(new)
     tails = np.r_[heads[1:] - 1, len(a) - 1]
-    return np.stack([a[heads, 0], ends[tails]], 1).tolist()
+    return np.stack([a[heads, 0], ends[tails]], 1)
 
 
-def _subtract(iv, done) -> list:
+def _subtract_a(iv, done) -> np.ndarray:
     """the (merged) intervals iv minus the (merged) intervals done: the elementary segments between
     all their boundaries that iv covers and done does not, merged"""
     a, d = _as_iv(iv), _as_iv(done)
     if a.size == 0:
-        return []
+        return _NO_IV
     if d.size == 0:
-        return a.tolist()
+        return a
+    if len(d) == 1 and d[0, 0] <= a[0, 0] and a[-1, 1] <= d[0, 1]:  # all refined already (the exact delta)
+        return _NO_IV
     pts = np.unique(np.concatenate([a.reshape(-1), d.reshape(-1)]))
     lo, hi = pts[:-1], pts[1:]
 
@@ -156,7 +162,22 @@ def _subtract(iv, done) -> list:
         return np.searchsorted(seg[:, 0], x, "right") > np.searchsorted(seg[:, 1], x, "right")
 
     keep = covered(lo, a) & ~covered(lo, d)
-    return _merge(np.stack([lo[keep], hi[keep]], 1))
+    return _merge_a(np.stack([lo[keep], hi[keep]], 1))
+
+
+def _merge(iv) -> list:
+    """_merge_a as a list of [a, b]"""
+    return _merge_a(iv).tolist()
+
+
+def _subtract(iv, done) -> list:
+    """_subtract_a as a list of [a, b]"""
+    return _subtract_a(iv, done).tolist()
+
+
+def _iv_len(iv) -> int:
+    a = _as_iv(iv)
+    return int((a[:, 1] - a[:, 0]).sum())
 
 
 class IQShardDetector:
@@ -243,7 +264,7 @@ class IQShardDetector:
         self.set_certify(certify)
         self.fs_ = float(fs)
         self._read = None      # the shard's sample source when chunked (refinement re-reads samples)
-        self._refined = []     # global frame ranges whose delta is float64 already
+        self._refined = _NO_IV  # global frame ranges whose delta is float64 already (merged, (n, 2))
 
     def set_delta(self, mode: str):
         """the delta source ("auto", "fp32", "exact"; class docstring), from the next
@@ -270,7 +291,7 @@ class IQShardDetector:
 
     def spectrogram_and_delta(self):
         """async: spectrogram of the shard and its per-frame band delta (into the stream plan)"""
-        self._refined = []
+        self._refined = _NO_IV
         if self.f1 > self.f0:
             if self.exact_delta:
                 # the exact delta first: the detector (on dctx) then runs beside the spectrogram
@@ -285,7 +306,7 @@ class IQShardDetector:
                                        ed=self.plan.d_ed if self.certify else None)
                 self._detector_ready()
         if self.exact_delta:
-            self._refined = [[0, self.T]]  # every rank's frames are float64 (the ranks agree on this list)
+            self._refined = np.array([[0, self.T]], np.int64)  # every rank's frames are float64 (the ranks agree on this list)
 
     def _detector_ready(self):
         """the detector's context waits for the delta enqueued on the spectrogram's"""
@@ -317,7 +338,7 @@ class IQShardDetector:
             self.spectrogram_and_delta()
             return
         self._read = read
-        self._refined = []
+        self._refined = _NO_IV
         for c0 in range(0, nloc, self.chunk):
             nf = min(self.chunk, nloc - c0)
             a = c0 * self.hop
@@ -336,7 +357,7 @@ class IQShardDetector:
                                    etot=etot, ed=ed)
         self._detector_ready()
         if self.exact_delta:
-            self._refined = [[0, self.T]]
+            self._refined = np.array([[0, self.T]], np.int64)
 
     MAX_REFINE = 8  # refinement rounds before giving up (refine_budget_exhausted)
 
@@ -367,10 +388,10 @@ class IQShardDetector:
                 exhausted = True
                 break
             need = self._dependencies(res.uncertain_frames)
-            if not need:  # every uncertain decision already reads float64 values: a float64 near tie
+            if not len(need):  # every uncertain decision already reads float64 values: a float64 near tie
                 break
-            self._refined = _merge(self._refined + need)
-            refined += sum(b - a for a, b in need)
+            self._refined = _merge_a(np.concatenate([self._refined, need]))
+            refined += _iv_len(need)
         if self.certify:
             if exact_decisions and not res.certified:  # a near tie / exhausted budget: the dB still float64
                 n = self._refine_detections(res)
@@ -395,14 +416,17 @@ class IQShardDetector:
         dets = res.detections
         if dets is None or len(dets) == 0:
             return 0
-        need = _subtract(_merge(zip(dets["start"], dets["stop"])), self._refined)
-        if not need:
+        r = self._refined
+        if len(r) == 1 and r[0, 0] <= dets["start"].min() and dets["stop"].max() <= r[0, 1]:
+            return 0  # every frame float64 already (the exact delta): no interval work per step
+        need = _subtract_a(_merge_a(np.stack([dets["start"], dets["stop"]], 1)), r)
+        if not len(need):
             return 0
         self._refine_local(need)
-        self._refined = _merge(self._refined + need)
-        return sum(b - a for a, b in need)
+        self._refined = _merge_a(np.concatenate([self._refined, need]))
+        return _iv_len(need)
 
-    def _dependencies(self, uncertain) -> list:
+    def _dependencies(self, uncertain) -> np.ndarray:
         """global frame ranges the uncertain decisions (frame, threshold source) depend on, and
         refines this rank's part of them"""
         iv = []
@@ -412,7 +436,7 @@ class IQShardDetector:
             else:
                 iv.append((max(0, int(src) - self.W), int(src)))  # the window delta[src - W : src]
             iv.append((int(f), int(f) + 1))
-        need = _subtract(_merge(iv), self._refined)
+        need = _subtract_a(_merge_a(iv), self._refined)
         self._refine_local(need)
         return need
 
