@@ -224,6 +224,13 @@ int msd_cstft_psd_dev(msd_cstft_plan *plan, const void *x, int dtype, const int6
  * 4 consecutive frames */
 int msd_cstft_psd_energy_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                              int64_t nstreams, int64_t max_frames, float *out, float *etot);
+/* the same, with each frame's complex sample sum given (frame_sums: device double [nstreams *
+ * max_frames][2], (sum I, sum Q) of frame s*max_frames + t, e.g. from msd_iq_delta64_sums_dev):
+ * the plan's C5 geometry (hop 1024, a window whose DFT vanishes outside bins 0, +-1 such as the
+ * periodic Hann) then detrends after the FFT from these sums and computes none itself; other
+ * geometries ignore them.  Same output as msd_cstft_psd_energy_dev within float32 rounding. */
+int msd_cstft_psd_fsums_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
+                            int64_t nstreams, int64_t max_frames, float *out, float *etot, const double *frame_sums);
 int64_t msd_cstft_energy_stride(int64_t nstreams, int64_t max_frames);
 /* one stream, host buffers: n complex samples in, out float32 [T][N] */
 int msd_cstft_psd(msd_cstft_plan *plan, const void *x, int dtype, int64_t n, float *out, int64_t *frames);
@@ -360,6 +367,13 @@ int msd_stream_certificate(msd_stream_plan *plan, int64_t *uncertain, double *mi
 int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg, int64_t hop,
                        double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo, int32_t noise_hi,
                        const int64_t *ranges, int64_t nranges, double *delta, double *ed);
+/* the same, plus each refined frame's complex sample sum (frame_sums[2 t], [2 t + 1]: sum I, sum Q
+ * as float64 -- exact for int16 input) for msd_cstft_psd_fsums_dev.  MSD_ERR_UNSUPPORTED (nothing
+ * launched) when the block step carries no sums: the int8 path with at most 8 needed bins. */
+int msd_iq_delta64_sums_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg,
+                            int64_t hop, double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
+                            int32_t noise_hi, const int64_t *ranges, int64_t nranges, double *delta, double *ed,
+                            double *frame_sums);
 /* Which block step msd_iq_delta64_dev takes for a geometry (host only, no GPU): int16 input with
  * blocks of D = gcd(nperseg, hop) = 1024 samples, no band touching bin 0 and at most 10 needed
  * bins (band and noise bins +- 1) runs the EXACT integer DFT on the matrix cores (int16 samples as

@@ -50,9 +50,10 @@ struct msd_ctx {
     double total_ms[msd::K_COUNT] = {};
     int64_t launches[msd::K_COUNT] = {};
     // scratch device buffers for the host-pointer convenience entry points
-    // (slot 4: msd_iq_delta64_dev's block table, rotations and ranges)
-    void *scratch[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    size_t scratch_bytes[5] = {0, 0, 0, 0, 0};
+    // (slot 4: msd_iq_delta64_dev's block table, rotations and ranges; slot 5: cstft4096_kernel's
+    // per-frame sums and raw DC-bin values for its post-FFT detrend)
+    void *scratch[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t scratch_bytes[6] = {0, 0, 0, 0, 0, 0};
     // msd_iq_delta64_dev's twiddle table W^m (m < rf_w_n), built once per frame length
     double2 *rf_w = nullptr;
     int rf_w_n = 0;

@@ -243,7 +243,8 @@ __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, 
                                                     const int64_t *__restrict__ fcs, const int64_t *__restrict__ bstart,
                                                     const int64_t *__restrict__ bcs, int64_t nframes, int64_t nblocks,
                                                     const double2 *__restrict__ rot, const double2 *__restrict__ blk,
-                                                    double *__restrict__ delta, double *__restrict__ ed) {
+                                                    double *__restrict__ delta, double *__restrict__ ed,
+                                                    double2 *__restrict__ fsum) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
     const int r = find_range(fcs, G.nr, f);
@@ -258,6 +259,7 @@ __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, 
         sum = cadd(sum, b0[K.nk * stride + j]);
         l1 += b0[(K.nk + 1) * stride + j].x;
     }
+    if (fsum) fsum[t] = sum;  // the frame's sample sums (exact for int16), for the spectrogram's detrend
     const double2 mean = make_double2(sum.x / G.N, sum.y / G.N);
     // V[k'] of the detrended frame at needed bin b
     auto V = [&](int b) {
@@ -306,6 +308,15 @@ int msd_iq_delta64_path(int32_t nperseg, int64_t hop, double fs, int32_t band_lo
 int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg, int64_t hop,
                        double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo, int32_t noise_hi,
                        const int64_t *ranges, int64_t nranges, double *delta, double *ed) {
+    return msd_iq_delta64_sums_dev(ctx, x, dtype, n_samples, nperseg, hop, fs, band_lo, band_hi, noise_lo, noise_hi,
+                                   ranges, nranges, delta, ed, nullptr);
+}
+
+int msd_iq_delta64_sums_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_samples, int32_t nperseg,
+                            int64_t hop, double fs, int32_t band_lo, int32_t band_hi, int32_t noise_lo,
+                            int32_t noise_hi, const int64_t *ranges, int64_t nranges, double *delta, double *ed,
+                            double *frame_sums) {
+    double2 *fsum = reinterpret_cast<double2 *>(frame_sums);
     if (!ctx || (!x && n_samples) || !delta || !ed || (!ranges && nranges) || nranges < 0 || nperseg < 4 ||
         hop <= 0 || !(fs > 0))
         return fail(MSD_ERR_INVALID, "msd_iq_delta64_dev: bad args");
@@ -314,10 +325,12 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
     std::string msg;
     if (int rc = plan_refine(nperseg, hop, fs, band_lo, band_hi, noise_lo, noise_hi, ranges, nranges, n_samples, P, msg))
         return fail(rc, "msd_iq_delta64_dev: " + msg);
-    if (nranges == 0) return MSD_OK;
     const int N = nperseg;
     RefineBins &K = P.K;
     RefineGeom &G = P.G;
+    if (fsum && dtype == MSD_CI16 && !ctx->refine_goertzel && i8_supported(G, K) && K.nk <= 8)
+        return fail(MSD_ERR_UNSUPPORTED, "msd_iq_delta64_sums_dev: this block step carries no sums (int8, <= 8 bins)");
+    if (nranges == 0) return MSD_OK;
     const std::vector<int64_t> &fstart = P.fstart, &fcs = P.fcs, &bstart = P.bstart, &bcs = P.bcs;
     const int64_t nblocks = P.nblocks, nframes = P.nframes;
     DeviceGuard g(ctx->device);
@@ -348,8 +361,7 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
             const double a = -2.0 * M_PI * (double)m / (double)N;
             rt[(size_t)b * R + j] = make_double2(std::cos(a), std::sin(a));
         }
-    // + 64 scratch entries past the table: block_i8_kernel's lanes without a value store there
-    const size_t nb_blk = (sizeof(double2) * ((size_t)nblocks * (K.nk + 2) + 64) + 255) / 256 * 256;
+    const size_t nb_blk = (sizeof(double2) * (size_t)nblocks * (K.nk + 2) + 255) / 256 * 256;
     const size_t nb_rot = (sizeof(double2) * rt.size() + 255) / 256 * 256;
     const size_t nb_meta = sizeof(int64_t) * (4 * (size_t)nranges + 2);
     void *d = nullptr;
@@ -393,7 +405,7 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
         if (int rc = launch_refine_i8(ctx, static_cast<const int16_t *>(x), G, K, d_bstart, d_bcs, nblocks, blk))
             return rc;
         hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, GF, K, d_fstart,
-                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed);
+                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed, fsum);
         e = hipGetLastError();
     } else if (e == hipSuccess) {
         KernelTimer timer(ctx, K_REFINE);
@@ -427,7 +439,7 @@ int msd_iq_delta64_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t n_sam
                                    static_cast<const float *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
         }
         hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, G, K, d_fstart,
-                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed);
+                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed, fsum);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return hip_fail(e, "msd_iq_delta64_dev");

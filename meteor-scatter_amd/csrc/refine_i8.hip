@@ -22,8 +22,8 @@
 // registers: the sub-block partials combine with float64 twiddles W^{256 k s} without a
 // cross-lane sum; the extra bins' digits spread over 8 lanes of the half-row (3 DPP adds).  With
 // K = 512 the digit products reach 2^31 in the worst case, so 256 h_d + l_d is formed in float64
-// (exact) rather than int32.  The output is refine.hip's bin-major block table, which
-// frame_kernel turns into frames, delta and ed.
+// (exact) rather than int32.  The output is refine.hip's bin-major block table (a tile's values
+// staged in LDS, then one store instruction), which frame_kernel turns into frames, delta and ed.
 //
 // One wave per contiguous range of tiles, 2 waves per SIMD (~200 VGPRs: 56 accumulators, the
 // next tile's 256 B of samples per lane in flight); the B fragments (NT x 8 KB), lane twiddles and
@@ -113,13 +113,17 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
     // per column: the lane twiddles (below) and the K offsets' column sums, read where used
     __shared__ double2 sTw[(1 + NX) * I8_SB * 16];
     __shared__ int sInit[NT * 16];
+    // per wave: one tile's output rows (4 blocks x RW entries)
+    constexpr int RW = 12;  // >= nk + 2 (nk <= 10)
+    __shared__ double2 sOut[4][I8_BPT * RW];
     for (int i = threadIdx.x; i < NT * I8_KS * 64; i += 256) sB[i] = bfrag[i];
     for (int i = threadIdx.x; i < (1 + NX) * I8_SB * 16; i += 256) sTw[i] = ltw[i];
     for (int i = threadIdx.x; i < NT * 16; i += 256) sInit[i] = colinit[i];
     __syncthreads();
     const int l = threadIdx.x & 63;
     const int c = l & 15, grp = l >> 4;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform
+    const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
     const int64_t g0 = wave * per_wave;
     const int64_t g1 = g0 + per_wave < nblocks ? g0 + per_wave : nblocks;
     if (g0 >= g1) return;
@@ -153,6 +157,18 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
         }
         const int64_t m = ab == 0 ? mb[0] : ab == 1 ? mb[1] : ab == 2 ? mb[2] : mb[3];
         return reinterpret_cast<const v4u *>(x + 2 * (m * D + as * I8_SUB)) + grp;
+    };
+    // the staged tile [pend, pend + 4) to out (bin-major): lane 4 row + b one 16-B entry, one
+    // store instruction per tile (nk + 2 segments of 64 B)
+    const int rw = nk + 2;
+    int64_t pend = -1;
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (pend < 0) return;
+        const int64_t nv = g1 - pend < I8_BPT ? g1 - pend : I8_BPT;
+        const int row = l >> 2, b = l & 3;
+        __builtin_amdgcn_wave_barrier();
+        if (row < rw && b < nv) out[row * nblocks + pend + b] = sOut[wv][b * RW + row];
+        __builtin_amdgcn_wave_barrier();
     };
     v4u raw[2 * I8_KS];
     {
@@ -191,6 +207,9 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
             digits(w, ah, al, habs);
             raw[2 * ks] = __builtin_nontemporal_load(pn + 8 * ks);
             raw[2 * ks + 1] = __builtin_nontemporal_load(pn + 8 * ks + 4);
+            // the previous tile's values leave after this tile's samples have arrived and the first
+            // prefetch is out: the wait for those samples never waits for these stores
+            if (ks == 0) flush();
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 A.h[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bk[t], A.h[t], 0, 0, 0);
@@ -243,33 +262,27 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
         hs += __builtin_amdgcn_mov_dpp(hs, 0xB1, 0xf, 0xf, true);
         hs += __builtin_amdgcn_mov_dpp(hs, 0x4E, 0xf, 0xf, true);
         hs = add_xor32_i(add_xor16_i(hs));
-        // stores without branches (every lane stores; the ones without a value write their own slot
-        // of the 64-entry scratch row past the table): a fixed number of store instructions per tile
-        // lets the compiler wait for the next tile's samples with vmcnt(stores) instead of vmcnt(0),
-        // i.e. without a store round trip per tile
-        const int64_t g = gt + grp;
-        const bool ok = g < g1;
-        double *o = reinterpret_cast<double *>(out);
-        double *const dump = reinterpret_cast<double *>(out + (int64_t)(nk + 2) * nblocks + l);
-        auto put = [&](bool want, int64_t row, int part, double v) __attribute__((always_inline)) {
-            *(want && ok ? o + 2 * (row * nblocks + g) + part : dump) = v;
-        };
-        put(c < ncomp, c >> 1, c & 1, ym);
+        // the tile's values into the wave's LDS staging row (block grp's rows at grp * RW); written
+        // out as one store instruction early in the next tile (flush)
+        double *st = reinterpret_cast<double *>(sOut[wv]);
+        if (c < ncomp) st[2 * (grp * RW + (c >> 1)) + (c & 1)] = ym;
 #pragma unroll
-        for (int e = 0; e < NX; ++e) put(dg == 0, 8 + e, c >> 3, yx[e]);
+        for (int e = 0; e < NX; ++e)
+            if (dg == 0) st[2 * (grp * RW + 8 + e) + (c >> 3)] = yx[e];
         // sum (|I| + |Q|) <= 256 (sum |h| + values): x = 256 h + (x & 255).  frame_kernel bounds the
         // detrended frame's sum |v| by it plus N |mean|, the mean from the block sums (NX > 0:
         // exact; else unknown, the sum row 0 and the bound doubled instead, N |mean| <= sum |x|)
         const double l1 = 256.0 * ((double)hs + 2.0 * D);
         if constexpr (NX > 0) {
-            // lanes 6, 7: the I / Q block sums; lane 4 grp: the bound (its .y 0 from lane 4 grp + 1)
-            const bool sl = c == 6 || c == 7, bl = c == 4 * grp || c == 4 * grp + 1;
-            put(sl || bl, sl ? nk : nk + 1, sl ? c - 6 : c - 4 * grp, sl ? (double)(int32_t)bsum : c == 4 * grp ? l1 : 0.0);
-        } else {
-            const int cc = c - 4 * grp;  // lanes 4 grp .. 4 grp + 3: the sum row (0) and the bound row
-            put(cc >= 0 && cc < 4, cc < 2 ? nk : nk + 1, cc & 1, cc == 2 ? 2.0 * l1 : 0.0);
+            if (c == 6 || c == 7) st[2 * (grp * RW + nk) + (c - 6)] = (double)(int32_t)bsum;
+            if (c == 4 * grp) sOut[wv][grp * RW + nk + 1] = make_double2(l1, 0.0);
+        } else if (c == 4 * grp) {
+            sOut[wv][grp * RW + nk] = make_double2(0.0, 0.0);
+            sOut[wv][grp * RW + nk + 1] = make_double2(2.0 * l1, 0.0);
         }
+        pend = gt;
     }
+    flush();
 }
 
 // one balanced base-256 digit expansion of T (|T| <= 2^46): T = sum_b d[b] 256^(5 - b)

@@ -186,6 +186,7 @@ _SIGS = [
     ("msd_cstft_psd_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P]),
     ("msd_cstft_psd", C.c_int, [_P, _P, C.c_int, C.c_int64, _P, C.POINTER(C.c_int64)]),
     ("msd_cstft_psd_energy_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, _P]),
+    ("msd_cstft_psd_fsums_dev", C.c_int, [_P, _P, C.c_int, _P, _P, C.c_int64, C.c_int64, _P, _P, _P]),
     ("msd_cstft_energy_stride", C.c_int64, [C.c_int64, C.c_int64]),
     ("msd_spec_band_sum_dev", C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
     ("msd_spec_band_sum_f64_dev", C.c_int,
@@ -221,6 +222,9 @@ _SIGS = [
     ("msd_iq_delta64_dev", C.c_int,
      [_P, _P, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_double, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
       _P, C.c_int64, _P, _P]),
+    ("msd_iq_delta64_sums_dev", C.c_int,
+     [_P, _P, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_double, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+      _P, C.c_int64, _P, _P, _P]),
     ("msd_iq_delta64_path", C.c_int,
      [C.c_int32, C.c_int64, C.c_double, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     ("msd_stream_plan_create", C.c_int,
@@ -640,11 +644,13 @@ class CStftPlan:
         return out
 
     def run_dev(self, x: DeviceBuffer, dtype_code_iq: int, off: DeviceBuffer, length: DeviceBuffer, nstreams: int,
-                max_frames: int, out: DeviceBuffer, etot: DeviceBuffer | None = None):
-        """etot: also each frame's 16 total-power partials (msd_cstft_psd_energy_dev)"""
-        check(self.ctx.lib.msd_cstft_psd_energy_dev(self.h, x.ptr, int(dtype_code_iq), off.ptr, length.ptr,
-                                                    int(nstreams), int(max_frames), out.ptr,
-                                                    None if etot is None else etot.ptr))
+                max_frames: int, out: DeviceBuffer, etot: DeviceBuffer | None = None, fsums=None):
+        """etot: also each frame's 16 total-power partials (msd_cstft_psd_energy_dev); fsums: each
+        frame's (sum I, sum Q) float64 on the device (msd_cstft_psd_fsums_dev, e.g. from
+        iq_delta64_dev(..., frame_sums=...))"""
+        check(self.ctx.lib.msd_cstft_psd_fsums_dev(self.h, x.ptr, int(dtype_code_iq), off.ptr, length.ptr,
+                                                   int(nstreams), int(max_frames), out.ptr,
+                                                   None if etot is None else etot.ptr, _dp(fsums)))
 
 
 class StreamPlan:
@@ -848,10 +854,12 @@ def iq_delta64_path(nperseg: int, hop: int, fs: float, band: tuple[int, int], no
 
 
 def iq_delta64_dev(ctx: Context, x, dtype_code_iq: int, n_samples: int, nperseg: int, hop: int, fs: float,
-                   band: tuple[int, int], noise: tuple[int, int], ranges: np.ndarray, delta, ed):
+                   band: tuple[int, int], noise: tuple[int, int], ranges: np.ndarray, delta, ed, frame_sums=None):
     """float64 delta of the frames in ranges ([n][2] frame [first, end), frame t at sample t*hop of
-    x) and its error bound, into delta[t] / ed[t] (device pointers)"""
+    x) and its error bound, into delta[t] / ed[t] (device pointers); frame_sums: also each frame's
+    (sum I, sum Q) as float64 pairs at frame_sums[2 t] (MsdError UNSUPPORTED, nothing launched, on a
+    block step without sums)"""
     r = np.ascontiguousarray(ranges, dtype=np.int64).reshape(-1, 2)
-    check(ctx.lib.msd_iq_delta64_dev(ctx.h, _dp(x), int(dtype_code_iq), int(n_samples), int(nperseg), int(hop),
-                                     float(fs), int(band[0]), int(band[1]), int(noise[0]), int(noise[1]), ptr(r),
-                                     r.shape[0], _dp(delta), _dp(ed)))
+    check(ctx.lib.msd_iq_delta64_sums_dev(ctx.h, _dp(x), int(dtype_code_iq), int(n_samples), int(nperseg), int(hop),
+                                          float(fs), int(band[0]), int(band[1]), int(noise[0]), int(noise[1]),
+                                          ptr(r), r.shape[0], _dp(delta), _dp(ed), _dp(frame_sums)))

@@ -84,9 +84,11 @@ class IQBatch:
         iq = np.ascontiguousarray(iq, dtype=self.dtype)
         self.d_x.upload(iq, byte_offset=(s * 2 * self.n_pad + 2 * sample_offset) * self.dtype.itemsize)
 
-    def run(self, etot: _lib.DeviceBuffer | None = None):
-        """etot: also each frame's 16 energy partials (float32 [ns][T][16], the error bound's input)"""
-        self.plan.run_dev(self.d_x, self.code, self.d_off, self.d_len, self.ns, self.T, self.d_out, etot)
+    def run(self, etot: _lib.DeviceBuffer | None = None, fsums: _lib.DeviceBuffer | None = None):
+        """etot: also each frame's 16 energy partials (float32 [ns][T][16], the error bound's input);
+        fsums: each frame's (sum I, sum Q) float64 already on the device (from the exact delta), so
+        the spectrogram's detrend needs no sums of its own (msd_cstft_psd_fsums_dev)"""
+        self.plan.run_dev(self.d_x, self.code, self.d_off, self.d_len, self.ns, self.T, self.d_out, etot, fsums)
 
     def close(self):
         self.plan.close()
@@ -260,6 +262,8 @@ class IQShardDetector:
         self.plan = _lib.StreamPlan(self.dctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
         self.ops = _stream.DeviceStreamOps(self.plan)
         self.d_etot = None
+        self.d_fsum = None  # exact delta: the frames' sample sums, shared with the spectrogram's detrend
+        self._fsums_ok = True
         self.certify = False
         self.set_certify(certify)
         self.fs_ = float(fs)
@@ -278,6 +282,8 @@ class IQShardDetector:
                                                self.delta_path == _lib.REFINE_INT8_MFMA)
         if self.certify and not self.exact_delta and self.d_etot is None:
             self.d_etot = self.ctx.alloc(16 * 4 * self.ctx.lib.msd_cstft_energy_stride(1, max(self.batch.T, 1)))
+        if self.exact_delta and self.d_fsum is None:
+            self.d_fsum = self.ctx.alloc(16 * max(self.batch.T, 1))
 
     def set_certify(self, on: bool):
         """certification on / off (takes effect at the next spectrogram_and_delta)"""
@@ -297,7 +303,7 @@ class IQShardDetector:
                 # the exact delta first: the detector (on dctx) then runs beside the spectrogram
                 self._delta_exact(self.batch.n, self.f1 - self.f0, 0)
                 self._detector_ready()
-                self.batch.run()
+                self.batch.run(fsums=self._fsums())
             else:
                 etot = self.d_etot if self.certify else None
                 self.batch.run(etot)
@@ -313,13 +319,25 @@ class IQShardDetector:
         if self.dctx is not self.ctx:
             self.dctx.wait_for(self.ctx)
 
+    def _fsums(self):
+        return self.d_fsum if self._fsums_ok else None
+
     def _delta_exact(self, n_samples: int, nframes: int, c0: int):
         """float64 delta and bound of the local frames [c0, c0 + nframes), whose samples start at the
-        batch buffer's first sample (frame c0 + j at sample j * hop)"""
-        _lib.iq_delta64_dev(self.ctx, self.batch.d_x, self.batch.code, n_samples, self.N, self.hop, self.fs_,
-                            self.band, self.noise, np.array([[0, nframes]], np.int64),
-                            _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0),
-                            _lib.C.c_void_p(self.plan.d_ed.value + 8 * c0))
+        batch buffer's first sample (frame c0 + j at sample j * hop); with them the frames' sample sums
+        (batch-local frame j) for the spectrogram's detrend, where the block step carries them"""
+        args = (self.ctx, self.batch.d_x, self.batch.code, n_samples, self.N, self.hop, self.fs_, self.band,
+                self.noise, np.array([[0, nframes]], np.int64), _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0),
+                _lib.C.c_void_p(self.plan.d_ed.value + 8 * c0))
+        if self._fsums_ok:
+            try:
+                _lib.iq_delta64_dev(*args, frame_sums=self.d_fsum)
+                return
+            except _lib.MsdError as e:
+                if e.code != _lib.MSD_ERR_UNSUPPORTED:
+                    raise
+                self._fsums_ok = False  # no sums on this block step: the spectrogram sums itself
+        _lib.iq_delta64_dev(*args)
 
     def process_host(self, iq_shard: np.ndarray):
         """interleaved I/Q of the shard's samples [s0, s1) on the host → the shard's delta in the
@@ -346,7 +364,8 @@ class IQShardDetector:
             self.batch.upload(0, np.ascontiguousarray(read(a, b)))
             if self.exact_delta:
                 self._delta_exact(b - a, nf, c0)
-                self.batch.run()  # frames past nf read stale samples; the spectrogram is the product
+                # frames past nf read stale samples (and sums); the spectrogram is the product
+                self.batch.run(fsums=self._fsums())
                 continue
             self.d_frames.upload(np.array([nf], np.int64))
             etot = self.d_etot if self.certify else None
@@ -475,6 +494,8 @@ class IQShardDetector:
         self.batch.close()
         if self.d_etot is not None:
             self.d_etot.free()
+        if self.d_fsum is not None:
+            self.d_fsum.free()
         if self.dctx is not self.ctx:
             self.dctx.close()
             self.ctx.set_option(_lib.OPT_CSTFT_RESERVE, 0)

@@ -107,3 +107,46 @@ def test_batch_ragged_persistent(kind, noverlap):
             _, _, rS = Q.spectrogram_iq_ref(i, q, 192000, 4096, noverlap)
             assert rS.shape[1] == nf
             assert _frame_rel(got[:nf].T.astype(np.float64), rS) < SPEC_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dc", [0.0, 700.0])
+def test_detrend_from_given_frame_sums(dc):
+    """C5's post-FFT detrend (cstft4096_kernel PD): with the frames' sample sums computed by the
+    spectrogram itself and with the exact sums the int8 delta step leaves (msd_iq_delta64_sums_dev
+    -> msd_cstft_psd_fsums_dev) the spectrogram matches scipy within SPEC_TOL, also with a DC
+    offset (the three corrected bins carry it), and the two agree to float32 rounding"""
+    from meteorgpu import _lib, iq
+    from meteorgpu.dsp import context
+    rng = np.random.default_rng(11)
+    fs, n = 192000, 60000
+    tt = np.arange(n) / fs
+    z = 3000 * np.exp(2j * np.pi * 1000.0 * tt) + 600 * (rng.standard_normal(n) + 1j * rng.standard_normal(n)) + dc * (1 + 1j)
+    i, q = np.round(z.real).astype(np.int16), np.round(z.imag).astype(np.int16)
+    x = np.empty(2 * n, np.int16)
+    x[0::2], x[1::2] = i, q
+    ctx = context(0)
+    b = iq.IQBatch(ctx, 1, n, fs)
+    b.upload(0, x)
+    b.run()
+    own = b.frames(0, 0, b.T)
+    T = b.T
+    fsum = ctx.alloc(16 * T)
+    d = ctx.alloc(8 * T)
+    e = ctx.alloc(8 * T)
+    band, noise = iq.iq_band_bins(4096, fs, (950.0, 1050.0)), iq.iq_band_bins(4096, fs, (-3050.0, -2950.0))
+    _lib.iq_delta64_dev(ctx, b.d_x, _lib.MSD_CI16, n, 4096, 1024, float(fs), band, noise,
+                        np.array([[0, T]], np.int64), d, e, frame_sums=fsum)
+    sums = np.empty(2 * T, np.float64)
+    fsum.download(sums)
+    w = np.lib.stride_tricks.sliding_window_view(x.astype(np.int64).reshape(-1, 2), 4096, axis=0)[::1024][:T]
+    np.testing.assert_array_equal(sums.reshape(T, 2), w.sum(axis=2))  # exact integer sums
+    b.run(fsums=fsum)
+    given = b.frames(0, 0, b.T)
+    _, _, rS = Q.spectrogram_iq_ref(i, q, fs, 4096, 3072)
+    assert _frame_rel(own.T.astype(np.float64), rS) < SPEC_TOL
+    assert _frame_rel(given.T.astype(np.float64), rS) < SPEC_TOL
+    assert _frame_rel(given.T.astype(np.float64), own.T.astype(np.float64)) < 1e-6
+    for buf in (fsum, d, e):
+        buf.free()
+    b.close()
