@@ -338,11 +338,9 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
             if constexpr (PD) {  // the raw DC bins for dc_fix_kernel (threads 0, 1: v[0]; 255: v[15])
                 const int o = tid <= 1 ? (int)offsetof(CsSide<T>, raw) + 8 * tid
                                        : tid == CS_T - 1 ? (int)offsetof(CsSide<T>, raw) + 16 : 1 << 20;
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
                 const float2 b = tid == CS_T - 1 ? v[15] : v[0];
-                const uint64_t bits = __builtin_bit_cast(uint64_t, b);
-                const auto rs = side_rsrc(g);
-                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)bits, rs, o, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(bits >> 32), rs, o + 4, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), side_rsrc(g), o, 0, 0);
             }
             // the frame's 16 KB through a buffer resource on its (wave-uniform) base: the thread's
             // byte offset in a VGPR, the row offset 1 KB * k2b as the scalar offset, no per-lane

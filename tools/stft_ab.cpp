@@ -8,6 +8,8 @@
 //                              (STFT_AB_F32=1: the same samples as float32 I/Q)
 //   STFT_AB_ENERGY=0,1,...: per variant, 1 = msd_cstft_psd_energy_dev (c5; the certification's frame
 //                  energy partials) instead of msd_cstft_psd_dev -- the same library can be listed twice
+//   STFT_AB_FSUMS=0,1,...: per variant, 1 = msd_cstft_psd_fsums_dev with the frames' exact sample
+//                  sums (computed here) -- the exact C5 path's detrend input
 //   STFT_AB_CLK=1: a variant built with -DXP_CLK leaves block 0's shader-cycle and 100 MHz
 //                  realtime counts in the first 16 output bytes; printed per round.
 // Build: g++ -O2 -std=c++17 tools/stft_ab.cpp -I include -I /opt/rocm/include -D__HIP_PLATFORM_AMD__
@@ -48,6 +50,9 @@ struct Lib {
     int (*cpsd_en)(msd_cstft_plan *, const void *, int, const int64_t *, const int64_t *, int64_t, int64_t, float *,
                    float *) = nullptr;
     bool energy = false;  // STFT_AB_ENERGY: this variant also writes the frame energy partials
+    int (*cpsd_fs)(msd_cstft_plan *, const void *, int, const int64_t *, const int64_t *, int64_t, int64_t, float *,
+                   float *, const double *) = nullptr;
+    bool fsums = false;   // STFT_AB_FSUMS: this variant gets the frame sums
     int (*sync)(msd_ctx *);
     int (*t_enable)(msd_ctx *, int);
     int (*t_reset)(msd_ctx *);
@@ -120,6 +125,19 @@ int main(int argc, char **argv) {
                 return 2;
             }
         }
+        l.cpsd_fs = reinterpret_cast<decltype(l.cpsd_fs)>(dlsym(l.h, "msd_cstft_psd_fsums_dev"));
+        if (const char *ev = getenv("STFT_AB_FSUMS")) {
+            const char *c = ev;
+            for (int k = 0; k < (int)libs.size() && c; ++k) {
+                c = strchr(c, ',');
+                if (c) ++c;
+            }
+            l.fsums = c && *c == '1';
+            if (l.fsums && !l.cpsd_fs) {
+                fprintf(stderr, "%s: no msd_cstft_psd_fsums_dev\n", argv[i]);
+                return 2;
+            }
+        }
         libs.push_back(l);
     }
     // periodic Hann (float32) and scipy's density scale 1 / (fs * sum w^2)
@@ -186,7 +204,21 @@ int main(int argc, char **argv) {
     const double gbytes = (double)nfiles * ((double)esz * n + 4.0 * K * T) * 1e-9;
     float *detot = nullptr;
     if (c5) CK(hipMalloc(&detot, sizeof(float) * 16 * (T + 4)));
+    double *dfs = nullptr;  // STFT_AB_FSUMS: frame t's (sum I, sum Q) of the periodic c5 stream
+    if (c5 && getenv("STFT_AB_FSUMS")) {
+        std::vector<int64_t> P(2 * (blk + 1), 0);
+        for (int64_t i = 0; i < blk; ++i)
+            for (int c = 0; c < 2; ++c) P[2 * (i + 1) + c] = P[2 * i + c] + host[2 * i + c];
+        auto F = [&](int64_t x, int c) { return (x / blk) * P[2 * blk + c] + P[2 * (x % blk) + c]; };
+        std::vector<double> fs(2 * T);
+        for (int64_t t = 0; t < T; ++t)
+            for (int c = 0; c < 2; ++c) fs[2 * t + c] = (double)(F(t * hop + N, c) - F(t * hop, c));
+        CK(hipMalloc(&dfs, sizeof(double) * 2 * T));
+        CK(hipMemcpy(dfs, fs.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice));
+    }
     auto launch = [&](Lib &l) {
+        if (c5 && l.fsums)
+            return l.cpsd_fs(l.cplan, dx, f32 ? MSD_CF32 : MSD_CI16, doff, dlen, nfiles, T, dout, l.energy ? detot : nullptr, dfs);
         if (c5 && l.energy) return l.cpsd_en(l.cplan, dx, f32 ? MSD_CF32 : MSD_CI16, doff, dlen, nfiles, T, dout, detot);
         return c5 ? l.cpsd_dev(l.cplan, dx, f32 ? MSD_CF32 : MSD_CI16, doff, dlen, nfiles, T, dout)
                   : l.psd_dev(l.plan, dx, MSD_I16, doff, dlen, nfiles, T, dout, ld);
