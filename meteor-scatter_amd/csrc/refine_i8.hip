@@ -25,7 +25,7 @@
 // (exact) rather than int32.  The output is refine.hip's bin-major block table (a tile's values
 // staged in LDS, then one store instruction), which frame_kernel turns into frames, delta and ed.
 //
-// One wave per contiguous range of tiles, 2 waves per SIMD (~200 VGPRs: 56 accumulators, the
+// Tiles interleaved over the waves, 2 waves per SIMD (~200 VGPRs: 56 accumulators, the
 // next tile's 256 B of samples per lane in flight); the B fragments (NT x 8 KB), lane twiddles and
 // column offsets sit in LDS.  Per block: 28 MFMAs (~850 cycles of the matrix core), 4 KB of
 // samples from HBM, ~30 float64 VALU ops per lane.
@@ -99,13 +99,14 @@ struct Acc {
 // out (bin-major, refine.hip's block table): out[b * nblocks + g] = B_g[k_b] for b < nk, then the
 // block's sample sum (b = nk) and an upper bound of sum (|re| + |im|) (b = nk + 1, .x)
 //
-// A wave walks its contiguous range of compact blocks four at a time (one 16-row tile); the next
-// tile's samples are requested K step by K step as the current one's are turned into digits.
+// A wave takes every nwaves-th tile of four compact blocks (one 16-row tile; the chip sweeps the
+// samples in order: 4 % faster than contiguous per-wave ranges); the next tile's samples are
+// requested K step by K step as the current one's are turned into digits.
 template <int NT>
 __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restrict__ x, int64_t D,
                                                           const int64_t *__restrict__ bstart,
                                                           const int64_t *__restrict__ bcs, int nr, int64_t nblocks,
-                                                          int64_t per_wave, int nk, const v4i *__restrict__ bfrag,
+                                                          int nk, const v4i *__restrict__ bfrag,
                                                           const int *__restrict__ colinit,
                                                           const double2 *__restrict__ ltw, double2 *__restrict__ out) {
     constexpr int NX = NT - 6;  // extra bins (8 + e), two components each, in tiles 6 ..
@@ -124,9 +125,12 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
     const int c = l & 15, grp = l >> 4;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform
     const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
-    const int64_t g0 = wave * per_wave;
-    const int64_t g1 = g0 + per_wave < nblocks ? g0 + per_wave : nblocks;
-    if (g0 >= g1) return;
+    // tiles interleaved over the waves (tile = wave + j * nwaves): the chip sweeps the samples in
+    // order, a window of ~nwaves tiles at a time
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const int64_t ntiles = (nblocks + I8_BPT - 1) / I8_BPT;
+    if (wave >= ntiles) return;
+    const int64_t g1 = nblocks;
     // sTw[(e * I8_SB + r) * 16 + c]: column c's sub-block twiddle W^{256 k r} (a lane's C rows r =
     // 0..3 are the 4 sub-blocks of block grp) for its component's bin, the imaginary part signed by
     // the component (re: +, im: -); e > 0: the same for extra bin 8 + e - 1
@@ -136,24 +140,18 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
     const double xscale = dg < 6 ? __builtin_ldexp(1.0, -6 - 8 * dg) : 0.0;
     // the lane's A row (l & 15) = sub-block (l & 3) of the tile's block (l & 15) >> 2; in K step ks
     // its 16 values are the row's bytes 128 ks + 16 (l >> 4) and 128 ks + 64 + 16 (l >> 4), 16 each:
-    // each load instruction reads 64 contiguous bytes per row.  The compact-block -> sample-block
-    // map is walked forward by the wave for the tile's four blocks (uniform: scalar loads, ranges
-    // only ever advance).  No vector load but the samples' in the loop: a wait for one would also
-    // wait for the prefetched samples.
+    // each load instruction reads 64 contiguous bytes per row (plain loads: non-temporal ones
+    // measured 2.5 % slower).  The compact-block -> sample-block map is looked up per tile for its
+    // four blocks (uniform: scalar loads).  No vector load but the samples' in the loop: a wait for
+    // one would also wait for the prefetched samples.
     const int ab = (l & 15) >> 2, as = l & 3;
-    int rr = find_range_i8(bcs, nr, g0);
-    int64_t rend = bcs[rr + 1], rbase = bstart[rr] - bcs[rr];
     auto src = [&](int64_t gt) {
         int64_t mb[I8_BPT];
 #pragma unroll
         for (int b = 0; b < I8_BPT; ++b) {
             const int64_t gb = gt + b < g1 ? gt + b : g1 - 1;
-            while (gb >= rend) {
-                ++rr;
-                rend = bcs[rr + 1];
-                rbase = bstart[rr] - bcs[rr];
-            }
-            mb[b] = rbase + gb;
+            const int r = find_range_i8(bcs, nr, gb);
+            mb[b] = bstart[r] + (gb - bcs[r]);
         }
         const int64_t m = ab == 0 ? mb[0] : ab == 1 ? mb[1] : ab == 2 ? mb[2] : mb[3];
         return reinterpret_cast<const v4u *>(x + 2 * (m * D + as * I8_SUB)) + grp;
@@ -172,16 +170,17 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
     };
     v4u raw[2 * I8_KS];
     {
-        const v4u *p = src(g0);
+        const v4u *p = src(wave * I8_BPT);
 #pragma unroll
         for (int ks = 0; ks < I8_KS; ++ks) {
-            raw[2 * ks] = __builtin_nontemporal_load(p + 8 * ks);
-            raw[2 * ks + 1] = __builtin_nontemporal_load(p + 8 * ks + 4);
+            raw[2 * ks] = p[8 * ks];
+            raw[2 * ks + 1] = p[8 * ks + 4];
         }
     }
-    for (int64_t gt = g0; gt < g1; gt += I8_BPT) {
+    for (int64_t tile = wave; tile < ntiles; tile += nwaves) {
+        const int64_t gt = tile * I8_BPT;
         // the next tile (the last one reloads itself: no branch inside the unrolled K loop)
-        const v4u *pn = src(gt + I8_BPT < g1 ? gt + I8_BPT : gt);
+        const v4u *pn = src((tile + nwaves < ntiles ? tile + nwaves : tile) * I8_BPT);
         Acc<NT> A;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -205,8 +204,8 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
             __builtin_memcpy(w, &raw[2 * ks], 32);
             v4i ah, al;
             digits(w, ah, al, habs);
-            raw[2 * ks] = __builtin_nontemporal_load(pn + 8 * ks);
-            raw[2 * ks + 1] = __builtin_nontemporal_load(pn + 8 * ks + 4);
+            raw[2 * ks] = pn[8 * ks];
+            raw[2 * ks + 1] = pn[8 * ks + 4];
             // the previous tile's values leave after this tile's samples have arrived and the first
             // prefetch is out: the wait for those samples never waits for these stores
             if (ks == 0) flush();
@@ -391,25 +390,23 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
     const v4i *d_frag = reinterpret_cast<const v4i *>(tb);
     const int *d_init = reinterpret_cast<const int *>(tb + nb_frag);
     const double2 *d_tw = reinterpret_cast<const double2 *>(tb + nb_frag + nb_init);
-    // persistent: 8 waves per CU (2 workgroups of 4), contiguous ranges of whole tiles per wave
+    // persistent: 8 waves per CU (2 workgroups of 4), the tiles interleaved over them
     const int64_t waves_max = (int64_t)ctx->num_cu * 8;
     const int64_t ntiles = (nblocks + I8_BPT - 1) / I8_BPT;
-    const int64_t per = I8_BPT * std::max<int64_t>(1, (ntiles + waves_max - 1) / waves_max);
-    const int64_t waves = (nblocks + per - 1) / per;
-    const unsigned grid = (unsigned)((waves + 3) / 4);
+    const unsigned grid = (unsigned)((std::min(waves_max, ntiles) + 3) / 4);
     hipStream_t st = ctx->stream;
     switch (NT) {
         case 6:
             hipLaunchKernelGGL(block_i8_kernel<6>, dim3(grid), dim3(256), 0, st, x, (int64_t)G.D, d_bstart, d_bcs, G.nr,
-                               nblocks, per, nk, d_frag, d_init, d_tw, blk);
+                               nblocks, nk, d_frag, d_init, d_tw, blk);
             break;
         case 7:
             hipLaunchKernelGGL(block_i8_kernel<7>, dim3(grid), dim3(256), 0, st, x, (int64_t)G.D, d_bstart, d_bcs, G.nr,
-                               nblocks, per, nk, d_frag, d_init, d_tw, blk);
+                               nblocks, nk, d_frag, d_init, d_tw, blk);
             break;
         case 8:
             hipLaunchKernelGGL(block_i8_kernel<8>, dim3(grid), dim3(256), 0, st, x, (int64_t)G.D, d_bstart, d_bcs, G.nr,
-                               nblocks, per, nk, d_frag, d_init, d_tw, blk);
+                               nblocks, nk, d_frag, d_init, d_tw, blk);
             break;
         default: return fail(MSD_ERR_UNSUPPORTED, "refine_i8: bins");
     }

@@ -22,5 +22,6 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_c5x" -o kt -- \
     python3 "$ROOT/bench.py" --workload c5 --steps $KS --warmup $KW --no-cpu-baseline --c5-mode exact > "$OUT/kt_c5x.log" 2>&1 || exit 1
 bash "$ROOT/tools/pmc_stft.sh" "$TAG" || exit 1
-REGEX=cstft bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline --c5-mode off
+REGEX=cstft bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline --c5-mode exact
+REGEX="block_i8|frame_kernel" bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5i8" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline --c5-mode exact
 REGEX="fresh_list_kernel|scan_kernel|approx_kernel|iq_band_delta" bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5det" --workload c5 --steps 1 --warmup 0 --no-cpu-baseline --c5-mode off
