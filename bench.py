@@ -341,8 +341,8 @@ def run_c5(a, ctx, job, rank, world):
     step()
     sync_all()
     kms = {}
-    for name, kid in (("cstft", _lib.K_CSTFT), ("band_delta", _lib.K_IQDELTA), ("fresh_thresholds", _lib.K_FRESH),
-                      ("scan", _lib.K_SSCAN), ("delta64", _lib.K_REFINE)):
+    for name, kid in (("cstft", _lib.K_CSTFT), ("cstft_dc_fix", _lib.K_CSTFT_DC), ("band_delta", _lib.K_IQDELTA),
+                      ("fresh_thresholds", _lib.K_FRESH), ("scan", _lib.K_SSCAN), ("delta64", _lib.K_REFINE)):
         ms, cnt = ctx.timing_get(kid)
         if dctx is not None:
             ms += dctx.timing_get(kid)[0]

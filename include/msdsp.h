@@ -87,7 +87,8 @@ int msd_set_option(msd_ctx *ctx, int option, int value);
 /* Per-kernel device timing with HIP events on the context stream.
  * kernel id: 0 = STFT power, 1 = block delta, 2 = detector stats, 3 = detector scan,
  * 4 = Welch band powers, 5 = live detector, 6 = complex (I/Q) STFT, 7 = I/Q band delta,
- * 8 = stream fresh thresholds, 9 = stream scan. */
+ * 8 = stream fresh thresholds, 9 = stream scan, 10 = float64 delta (msd_iq_delta64_dev),
+ * 11 = the I/Q STFT's post-FFT detrend of bins 0, +-1 (its separate fix-up kernels). */
 int msd_timing_enable(msd_ctx *ctx, int enable);
 /* which kernels get events while timing is on: bit k = kernel id k (default all); a timed
  * region that times only its roofline kernel carries no events around the others */

@@ -568,7 +568,6 @@ int msd_cstft_psd_fsums_dev(msd_cstft_plan *p, const void *x, int dtype, const i
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
     DeviceGuard g(p->ctx->device);
     const int64_t total = nstreams * max_frames;
-    KernelTimer timer(p->ctx, K_CSTFT);
     const bool pd = p->post_dt && p->detrend && p->hop == 4 * 256;  // the PD kernels: C5's hop
     void *side = nullptr;  // PD: CsSide per frame (64 B), then CsHead per stream
     if (pd) {
@@ -588,10 +587,15 @@ int msd_cstft_psd_fsums_dev(msd_cstft_plan *p, const void *x, int dtype, const i
         int64_t per = (total + wgs - 1) / wgs;
         if (etot) per = (per + 3) / 4 * 4;  // energy groups of 4 frames start at every workgroup's first
         wgs = (total + per - 1) / per;
-        hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
-                           max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out, etot,
-                           msd_cstft_energy_stride(nstreams, max_frames), static_cast<CsSide<T> *>(side));
+        {
+            KernelTimer timer(p->ctx, K_CSTFT);  // the FFT kernel alone: the roofline's
+            hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
+                               max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out, etot,
+                               msd_cstft_energy_stride(nstreams, max_frames), static_cast<CsSide<T> *>(side));
+        }
         static_assert(sizeof(CsHead<T>) <= 64, "CsHead");
+        if (!pd_kern) return;
+        KernelTimer dc_timer(p->ctx, K_CSTFT_DC);  // the fix-up kernels apart from the FFT's roofline
         auto *head = reinterpret_cast<CsHead<T> *>(static_cast<char *>(side) + 64 * (size_t)total);
         const dim3 fg((unsigned)((total + 255) / 256));
         if (pd_kern == 1) {

@@ -25,7 +25,7 @@ int ensure_dyn_lds(const void *kernel, int bytes);
     } while (0)
 
 enum KernelId { K_STFT = 0, K_BLOCK = 1, K_DSTAT = 2, K_DSCAN = 3, K_WELCH = 4, K_LIVE = 5, K_CSTFT = 6, K_IQDELTA = 7, K_FRESH = 8, K_SSCAN = 9,
-               K_REFINE = 10, K_COUNT = 11 };
+               K_REFINE = 10, K_CSTFT_DC = 11, K_COUNT = 12 };
 
 struct EventPair {
     hipEvent_t a, b;

@@ -35,7 +35,7 @@ DTYPE_CODES = {
 }
 
 K_STFT, K_BLOCK, K_DSTAT, K_DSCAN, K_WELCH, K_LIVE, K_CSTFT = 0, 1, 2, 3, 4, 5, 6
-K_IQDELTA, K_FRESH, K_SSCAN, K_REFINE = 7, 8, 9, 10
+K_IQDELTA, K_FRESH, K_SSCAN, K_REFINE, K_CSTFT_DC = 7, 8, 9, 10, 11
 OPT_GENERIC_STFT = 1
 OPT_FRESH_ALL = 2
 OPT_REFINE_GOERTZEL = 3
