@@ -25,13 +25,16 @@
 // (exact) rather than int32.  The output is refine.hip's bin-major block table (a tile's values
 // staged in LDS, then one store instruction), which frame_kernel turns into frames, delta and ed.
 //
-// Tiles interleaved over the waves, 2 waves per SIMD (~200 VGPRs: 56 accumulators, the
-// next tile's 256 B of samples per lane in flight); the B fragments (NT x 8 KB), lane twiddles and
+// Tiles interleaved over the waves, one wave per SIMD (~370 VGPRs: two accumulator sets of 56 and
+// two tiles of samples, 2 x 256 B per lane, in flight), software-pipelined: tile k's MFMAs run
+// while tile k - 1's float64 reduction is interleaved slice by slice (1.98 -> 1.93 ms for the delta
+// step against two waves per SIMD without it); the B fragments (NT x 8 KB), lane twiddles and
 // column offsets sit in LDS.  Per block: 28 MFMAs (~850 cycles of the matrix core), 4 KB of
 // samples from HBM, ~30 float64 VALU ops per lane.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "msd_internal.h"
@@ -103,7 +106,7 @@ struct Acc {
 // samples in order: 4 % faster than contiguous per-wave ranges); the next tile's samples are
 // requested K step by K step as the current one's are turned into digits.
 template <int NT>
-__global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restrict__ x, int64_t D,
+__global__ __launch_bounds__(256, 1) void block_i8_kernel(const int16_t *__restrict__ x, int64_t D,
                                                           const int64_t *__restrict__ bstart,
                                                           const int64_t *__restrict__ bcs, int nr, int64_t nblocks,
                                                           int nk, const v4i *__restrict__ bfrag,
@@ -168,60 +171,17 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
         if (row < rw && b < nv) out[row * nblocks + pend + b] = sOut[wv][b * RW + row];
         __builtin_amdgcn_wave_barrier();
     };
-    v4u raw[2 * I8_KS];
-    {
-        const v4u *p = src(wave * I8_BPT);
-#pragma unroll
-        for (int ks = 0; ks < I8_KS; ++ks) {
-            raw[2 * ks] = p[8 * ks];
-            raw[2 * ks + 1] = p[8 * ks + 4];
-        }
-    }
-    for (int64_t tile = wave; tile < ntiles; tile += nwaves) {
-        const int64_t gt = tile * I8_BPT;
-        // the next tile (the last one reloads itself: no branch inside the unrolled K loop)
-        const v4u *pn = src((tile + nwaves < ntiles ? tile + nwaves : tile) * I8_BPT);
-        Acc<NT> A;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            A.h[t] = v4i{0, 0, 0, 0};
-            const int ci = sInit[t * 16 + c];
-            A.l[t] = v4i{ci, ci, ci, ci};
-        }
-        uint32_t habs = 0;
-        // the B fragments are the same for every tile: an opaque offset keeps the compiler from
-        // hoisting all NT * I8_KS of them (4 VGPRs each) out of the loop
-        int boff = l;
-        asm volatile("" : "+v"(boff));
-#pragma unroll
-        for (int ks = 0; ks < I8_KS; ++ks) {
-            // the step's B fragments requested first: their LDS latency runs under the digit
-            // extraction and the earlier tiles' MFMAs instead of one round trip per MFMA pair
-            v4i bk[NT];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) bk[t] = sB[(t * I8_KS + ks) * 64 + boff];
-            uint32_t w[8];
-            __builtin_memcpy(w, &raw[2 * ks], 32);
-            v4i ah, al;
-            digits(w, ah, al, habs);
-            raw[2 * ks] = pn[8 * ks];
-            raw[2 * ks + 1] = pn[8 * ks + 4];
-            // the previous tile's values leave after this tile's samples have arrived and the first
-            // prefetch is out: the wait for those samples never waits for these stores
-            if (ks == 0) flush();
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                A.h[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bk[t], A.h[t], 0, 0, 0);
-                A.l[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bk[t], A.l[t], 0, 0, 0);
-            }
-        }
-        // float64: this lane's component of block gt + grp.  Per sub-block P_r = 2^-6 sum_d 2^-8d
-        // (256 h_d + l_d) (each digit term exact; Horner from the lowest digit, its first steps
-        // exact), then the twiddled sum over the 4 sub-blocks with the partner component (lane ^ 1;
-        // the sign rides in tw.y).  No cross-lane sum: the lane holds its whole block.
-        double ym = 0.0;
-#pragma unroll
-        for (int r = 0; r < I8_SB; ++r) {
+    // Software-pipelined over tile pairs, one wave per SIMD (512 VGPRs): tile k's MFMAs run into
+    // one accumulator set while the float64 reduction of tile k - 1 (the other set) is interleaved
+    // slice by slice between its K steps; two tiles of samples in flight per wave.
+    struct Post {
+        double ym;
+        double ax[NX > 0 ? NX : 1];
+        uint32_t bsum;
+    };
+    auto slice = [&](const Acc<NT> &A, int s, Post &P) __attribute__((always_inline)) {
+        if (s < I8_SB) {  // this lane's component, sub-block s
+            const int r = s;
             double p = __builtin_fma(256.0, (double)A.h[5][r], (double)A.l[5][r]);
 #pragma unroll
             for (int d = 4; d >= 0; --d)
@@ -229,57 +189,121 @@ __global__ __launch_bounds__(256, 2) void block_i8_kernel(const int16_t *__restr
             p *= 0x1p-6;
             const double q = dpp64<0xB1>(p);
             const double2 w = tw(0, r);
-            ym = __builtin_fma(p, w.x, ym);
-            ym = __builtin_fma(q, w.y, ym);
+            P.ym = __builtin_fma(p, w.x, P.ym);
+            P.ym = __builtin_fma(q, w.y, P.ym);
+        } else {  // the extra bins' digit lanes, sub-block s - 4
+            const int r = s - I8_SB;
+#pragma unroll
+            for (int e = 0; e < NX; ++e) {
+                if (e == 0) P.bsum += ((uint32_t)A.h[6][r] << 8) + (uint32_t)A.l[6][r];
+                const double v = __builtin_fma(256.0, (double)A.h[6 + e][r], (double)A.l[6 + e][r]);
+                const double u = dpp64<0x128>(v);
+                const double2 w = tw(1 + e, r);
+                P.ax[e] = __builtin_fma(v, w.x, P.ax[e]);
+                P.ax[e] = __builtin_fma(u, w.y, P.ax[e]);
+            }
         }
-        // extra bins: each lane one digit of one component; twiddle its rows (partner: lane ^ 8,
-        // same digit), scale, then sum the 6 digit lanes of the half-row
+    };
+    auto finish = [&](Post &P, uint32_t habs, int64_t gt) __attribute__((always_inline)) {
         double yx[NX > 0 ? NX : 1];
-        uint32_t bsum = 0;
 #pragma unroll
         for (int e = 0; e < NX; ++e) {
-            double acc = 0.0;
-#pragma unroll
-            for (int r = 0; r < I8_SB; ++r) {
-                // columns 6 / 7 of tile 6: the sub-block sums of I / Q, exact in int32 (|.| <= 2^23)
-                if (e == 0) bsum += ((uint32_t)A.h[6][r] << 8) + (uint32_t)A.l[6][r];
-                const double v = __builtin_fma(256.0, (double)A.h[6 + e][r], (double)A.l[6 + e][r]);
-                const double u = dpp64<0x128>(v);  // row_ror:8 -- the other component, same digit
-                const double2 w = tw(1 + e, r);
-                acc = __builtin_fma(v, w.x, acc);
-                acc = __builtin_fma(u, w.y, acc);
-            }
-            acc *= xscale;  // 0 on the lanes without a digit
-            acc += dpp64<0xB1>(acc);  // the 8 lanes of the half-row: xor 1, xor 2, mirror
+            double acc = P.ax[e] * xscale;
+            acc += dpp64<0xB1>(acc);
             acc += dpp64<0x4E>(acc);
             acc += dpp64<0x141>(acc);
             yx[e] = acc;
         }
-        // sum |h| per block: the A rows of block b are lanes with (l >> 2) & 3 == b -- sum over lane
-        // bits 0, 1 (quad DPP) and 4, 5 (lane groups); lane c == 4 grp then holds block grp's
         int hs = (int)habs;
         hs += __builtin_amdgcn_mov_dpp(hs, 0xB1, 0xf, 0xf, true);
         hs += __builtin_amdgcn_mov_dpp(hs, 0x4E, 0xf, 0xf, true);
         hs = add_xor32_i(add_xor16_i(hs));
-        // the tile's values into the wave's LDS staging row (block grp's rows at grp * RW); written
-        // out as one store instruction early in the next tile (flush)
         double *st = reinterpret_cast<double *>(sOut[wv]);
-        if (c < ncomp) st[2 * (grp * RW + (c >> 1)) + (c & 1)] = ym;
+        if (c < ncomp) st[2 * (grp * RW + (c >> 1)) + (c & 1)] = P.ym;
 #pragma unroll
         for (int e = 0; e < NX; ++e)
             if (dg == 0) st[2 * (grp * RW + 8 + e) + (c >> 3)] = yx[e];
-        // sum (|I| + |Q|) <= 256 (sum |h| + values): x = 256 h + (x & 255).  frame_kernel bounds the
-        // detrended frame's sum |v| by it plus N |mean|, the mean from the block sums (NX > 0:
-        // exact; else unknown, the sum row 0 and the bound doubled instead, N |mean| <= sum |x|)
         const double l1 = 256.0 * ((double)hs + 2.0 * D);
         if constexpr (NX > 0) {
-            if (c == 6 || c == 7) st[2 * (grp * RW + nk) + (c - 6)] = (double)(int32_t)bsum;
+            if (c == 6 || c == 7) st[2 * (grp * RW + nk) + (c - 6)] = (double)(int32_t)P.bsum;
             if (c == 4 * grp) sOut[wv][grp * RW + nk + 1] = make_double2(l1, 0.0);
         } else if (c == 4 * grp) {
             sOut[wv][grp * RW + nk] = make_double2(0.0, 0.0);
             sOut[wv][grp * RW + nk + 1] = make_double2(2.0 * l1, 0.0);
         }
         pend = gt;
+    };
+    auto post_all = [&](const Acc<NT> &A, uint32_t habs, int64_t gt) __attribute__((always_inline)) {
+        Post P{};
+#pragma unroll
+        for (int s = 0; s < 2 * I8_SB; ++s) slice(A, s, P);
+        finish(P, habs, gt);
+    };
+    const int64_t cnt = (ntiles - wave + nwaves - 1) / nwaves;  // this wave's tiles: wave + k nwaves
+    auto tg = [&](int64_t k) { return (wave + (k < cnt ? k : cnt - 1) * nwaves) * I8_BPT; };
+    // tile k's MFMAs from R into A (R refilled with tile k2's samples), the reduction of the other
+    // set PA (tile kp) interleaved when DO_POST
+    auto kloop = [&](v4u (&R)[2 * I8_KS], Acc<NT> &A, uint32_t &habs, int64_t k2, auto do_post, const Acc<NT> &PA,
+                     uint32_t phabs, int64_t pgt) __attribute__((always_inline)) {
+        const v4u *pn = src(tg(k2));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            A.h[t] = v4i{0, 0, 0, 0};
+            const int ci = sInit[t * 16 + c];
+            A.l[t] = v4i{ci, ci, ci, ci};
+        }
+        habs = 0;
+        int boff = l;
+        asm volatile("" : "+v"(boff));
+        Post P{};
+#pragma unroll
+        for (int ks = 0; ks < I8_KS; ++ks) {
+            v4i bk[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bk[t] = sB[(t * I8_KS + ks) * 64 + boff];
+            uint32_t w[8];
+            __builtin_memcpy(w, &R[2 * ks], 32);
+            v4i ah, al;
+            digits(w, ah, al, habs);
+            R[2 * ks] = pn[8 * ks];
+            R[2 * ks + 1] = pn[8 * ks + 4];
+            if (ks == 0) flush();
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                A.h[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bk[t], A.h[t], 0, 0, 0);
+                A.l[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bk[t], A.l[t], 0, 0, 0);
+                if constexpr (decltype(do_post)::value)
+                    if (t == NT / 2) slice(PA, ks, P);  // a slice of the other tile's reduction
+            }
+        }
+        if constexpr (decltype(do_post)::value) finish(P, phabs, pgt);
+    };
+    v4u R0[2 * I8_KS], R1[2 * I8_KS];
+    {
+        const v4u *p0 = src(tg(0)), *p1 = src(tg(1));
+#pragma unroll
+        for (int ks = 0; ks < I8_KS; ++ks) {
+            R0[2 * ks] = p0[8 * ks];
+            R0[2 * ks + 1] = p0[8 * ks + 4];
+            R1[2 * ks] = p1[8 * ks];
+            R1[2 * ks + 1] = p1[8 * ks + 4];
+        }
+    }
+    Acc<NT> A0, A1;
+    uint32_t h0 = 0, h1 = 0;
+    kloop(R0, A0, h0, 2, std::false_type{}, A1, 0u, 0);
+    int64_t k = 1;
+    for (; k + 1 < cnt; k += 2) {
+        kloop(R1, A1, h1, k + 2, std::true_type{}, A0, h0, tg(k - 1));
+        kloop(R0, A0, h0, k + 3, std::true_type{}, A1, h1, tg(k));
+    }
+    if (k < cnt) {
+        kloop(R1, A1, h1, k, std::true_type{}, A0, h0, tg(k - 1));
+        flush();
+        post_all(A1, h1, tg(k));
+    } else {
+        flush();
+        post_all(A0, h0, tg(k - 1));
     }
     flush();
 }
@@ -391,7 +415,7 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
     const int *d_init = reinterpret_cast<const int *>(tb + nb_frag);
     const double2 *d_tw = reinterpret_cast<const double2 *>(tb + nb_frag + nb_init);
     // persistent: 8 waves per CU (2 workgroups of 4), the tiles interleaved over them
-    const int64_t waves_max = (int64_t)ctx->num_cu * 8;
+    const int64_t waves_max = (int64_t)ctx->num_cu * 4;
     const int64_t ntiles = (nblocks + I8_BPT - 1) / I8_BPT;
     const unsigned grid = (unsigned)((std::min(waves_max, ntiles) + 3) / 4);
     hipStream_t st = ctx->stream;
