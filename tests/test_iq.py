@@ -111,7 +111,8 @@ def test_batch_ragged_persistent(kind, noverlap):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dc", [0.0, 700.0])
-def test_detrend_from_given_frame_sums(dc):
+@pytest.mark.parametrize("kind", ["int16", "float32"])
+def test_detrend_from_given_frame_sums(dc, kind):
     """C5's post-FFT detrend (cstft4096_kernel PD): with the frames' sample sums computed by the
     spectrogram itself and with the exact sums the int8 delta step leaves (msd_iq_delta64_sums_dev
     -> msd_cstft_psd_fsums_dev) the spectrogram matches scipy within SPEC_TOL, also with a DC
@@ -123,10 +124,13 @@ def test_detrend_from_given_frame_sums(dc):
     tt = np.arange(n) / fs
     z = 3000 * np.exp(2j * np.pi * 1000.0 * tt) + 600 * (rng.standard_normal(n) + 1j * rng.standard_normal(n)) + dc * (1 + 1j)
     i, q = np.round(z.real).astype(np.int16), np.round(z.imag).astype(np.int16)
-    x = np.empty(2 * n, np.int16)
+    dt = np.int16 if kind == "int16" else np.float32
+    if kind == "float32":  # the same samples as float32 I/Q (the delta step's float64 Goertzel path)
+        i, q = (i / 32768).astype(np.float32), (q / 32768).astype(np.float32)
+    x = np.empty(2 * n, dt)
     x[0::2], x[1::2] = i, q
     ctx = context(0)
-    b = iq.IQBatch(ctx, 1, n, fs)
+    b = iq.IQBatch(ctx, 1, n, fs, dtype=dt)
     b.upload(0, x)
     b.run()
     own = b.frames(0, 0, b.T)
@@ -135,12 +139,16 @@ def test_detrend_from_given_frame_sums(dc):
     d = ctx.alloc(8 * T)
     e = ctx.alloc(8 * T)
     band, noise = iq.iq_band_bins(4096, fs, (950.0, 1050.0)), iq.iq_band_bins(4096, fs, (-3050.0, -2950.0))
-    _lib.iq_delta64_dev(ctx, b.d_x, _lib.MSD_CI16, n, 4096, 1024, float(fs), band, noise,
+    _lib.iq_delta64_dev(ctx, b.d_x, b.code, n, 4096, 1024, float(fs), band, noise,
                         np.array([[0, T]], np.int64), d, e, frame_sums=fsum)
     sums = np.empty(2 * T, np.float64)
     fsum.download(sums)
-    w = np.lib.stride_tricks.sliding_window_view(x.astype(np.int64).reshape(-1, 2), 4096, axis=0)[::1024][:T]
-    np.testing.assert_array_equal(sums.reshape(T, 2), w.sum(axis=2))  # exact integer sums
+    if kind == "int16":
+        w = np.lib.stride_tricks.sliding_window_view(x.astype(np.int64).reshape(-1, 2), 4096, axis=0)[::1024][:T]
+        np.testing.assert_array_equal(sums.reshape(T, 2), w.sum(axis=2))  # exact integer sums
+    else:
+        w = np.lib.stride_tricks.sliding_window_view(x.astype(np.float64).reshape(-1, 2), 4096, axis=0)[::1024][:T]
+        np.testing.assert_allclose(sums.reshape(T, 2), w.sum(axis=2), rtol=0, atol=1e-9)
     b.run(fsums=fsum)
     given = b.frames(0, 0, b.T)
     _, _, rS = Q.spectrogram_iq_ref(i, q, fs, 4096, 3072)
