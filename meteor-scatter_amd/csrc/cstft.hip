@@ -165,8 +165,9 @@ struct CsTune {
 // powers.  The barrier that had to follow the sums now only has to precede the pass-1 LDS write
 // (every wave past the previous frame's pass-3 reads), so pass 1 runs beside the slower waves'
 // pass 3; the thread partials (4 rows instead of 16) ride in the pass-1 layout's spare LDS
-// columns and one wave in turn reduces them.  The energy partials (EN) see the raw powers of the
-// three bins: the FFT input is w x.
+// columns and one wave in turn reduces them (PD 1).  PD 2 (msd_cstft_psd_fsums_dev: the frame
+// sums given, from the exact delta step) computes no sums at all; dc_fix_kernel reads them.  The
+// energy partials (EN) see the raw powers of the three bins: the FFT input is w x.
 template <typename T>
 struct alignas(64) CsSide {
     typename IQ<T>::acc_t sum[2];  // the I and Q sums of block t + 3
