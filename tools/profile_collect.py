@@ -57,8 +57,11 @@ KW, KS = kt0.get("warmup", 1), kt0.get("steps", 5)
 lines = ["roofline kernel, per-dispatch durations (ms) from rocprofv3 --kernel-trace; the run is "
          f"bench.py --steps {KS} --warmup {KW}: dispatches 1-{KW} are the warm-up, {KW + 1}-{KW + KS} the timed "
          f"steps, {KW + KS + 1} the step after the timed region that times every kernel for the breakdown"]
-for wl, key in (("", "stft1024_kernel"), ("_live", "welch_bands_kernel"), ("_c5", "cstft4096_kernel")):
-    import csv
+import csv
+for wl, key in (("", "stft1024_kernel"), ("_live", "welch_bands_kernel"), ("_c5", "cstft4096_kernel"),
+                ("_c5x", "cstft4096_kernel")):
+    if not os.path.exists(f"{src}/kt{wl}"):
+        continue
     rows = list(csv.DictReader(open(f"{src}/kt{wl}/kt_kernel_trace.csv")))
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if key in r["Kernel_Name"]]
     b = last_json(f"{src}/kt{wl}.log")
