@@ -238,7 +238,11 @@ __device__ __forceinline__ double band_db_bound64(double E, int n, double d) {
 }
 
 // one thread per frame: combine the R blocks (rot[b][j] = W^{k_b j D}, host table, uniform reads),
-// the Hann taps, |Y|^2 * scale, the band sums in np.sum order, 10 log10(E + 1e-12); delta and its bound
+// the Hann taps, |Y|^2 * scale, the band sums in np.sum order, 10 log10(E + 1e-12); delta and its bound.
+// RC: R at compile time (C5: 4; a band bin's 3 R block loads then issue together: -0.033 ms of the
+// 1.92 ms delta step, tools/i8_time.py against tools/experiments/r4_frame_kernel_old.patch) or 0 (runtime R).
+// Loading the next bin's taps ahead did not pipeline: the compiler sinks the loads below the sums.
+template <int RC>
 __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, const int64_t *__restrict__ fstart,
                                                     const int64_t *__restrict__ fcs, const int64_t *__restrict__ bstart,
                                                     const int64_t *__restrict__ bcs, int64_t nframes, int64_t nblocks,
@@ -247,33 +251,46 @@ __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, 
                                                     double2 *__restrict__ fsum) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
+    const int R = RC ? RC : G.R;
     const int r = find_range(fcs, G.nr, f);
     const int64_t t = fstart[r] + (f - fcs[r]);
-    const int64_t m0 = t * G.hop / G.D;            // first block of the frame
+    const int64_t m0 = t * (G.hop / G.D);  // first block of the frame (D = gcd(N, hop) divides hop)
     // bin-major blocks: neighbouring frames read neighbouring addresses
     const double2 *b0 = blk + (bcs[r] + (m0 - bstart[r]));
     const int64_t stride = nblocks;
     double2 sum = make_double2(0.0, 0.0);
     double l1 = 0.0;
-    for (int j = 0; j < G.R; ++j) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
         sum = cadd(sum, b0[K.nk * stride + j]);
         l1 += b0[(K.nk + 1) * stride + j].x;
     }
     if (fsum) fsum[t] = sum;  // the frame's sample sums (exact for int16), for the spectrogram's detrend
     const double2 mean = make_double2(sum.x / G.N, sum.y / G.N);
-    // V[k'] of the detrended frame at needed bin b
-    auto V = [&](int b) {
-        const double2 *rb = rot + b * G.R;
-        const double2 *bb = b0 + b * stride;
-        double2 z = bb[0];
-        for (int j = 1; j < G.R; ++j) z = cadd(z, cmul(rb[j], bb[j]));
-        if (b == K.dc) z = csub(z, make_double2(mean.x * G.N, mean.y * G.N));
-        return z;
+    // V[k'] of the detrended frame at needed bin b from its R block values v
+    const double2 dcm = make_double2(mean.x * G.N, mean.y * G.N);
+    auto V = [&](int b, const double2 *v) {
+        const double2 *rb = rot + b * R;
+        double2 z = v[0];
+#pragma unroll
+        for (int j = 1; j < R; ++j) z = cadd(z, cmul(rb[j], v[j]));
+        return b == K.dc ? csub(z, dcm) : z;
     };
     auto energy = [&](const int (*idx)[3], int n) {
         double E = 0.0;
         for (int q = 0; q < n; ++q) {
-            const double2 a = V(idx[q][0]), c = V(idx[q][1]), e = V(idx[q][2]);
+            double2 a, c, e;
+            if constexpr (RC > 0) {  // the three taps' 3 R loads issued together, then the sums
+                double2 v[3][RC];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < RC; ++j) v[i][j] = b0[idx[q][i] * stride + j];
+                a = V(idx[q][0], v[0]), c = V(idx[q][1], v[1]), e = V(idx[q][2], v[2]);
+            } else {
+                auto Vb = [&](int b) { return V(b, b0 + b * stride); };
+                a = Vb(idx[q][0]), c = Vb(idx[q][1]), e = Vb(idx[q][2]);
+            }
             const double2 y = make_double2(0.5 * c.x - 0.25 * a.x - 0.25 * e.x, 0.5 * c.y - 0.25 * a.y - 0.25 * e.y);
             E += (y.x * y.x + y.y * y.y) * G.scale;
         }
@@ -285,6 +302,17 @@ __global__ __launch_bounds__(256) void frame_kernel(RefineGeom G, RefineBins K, 
     const double amp = (l1 + (double)G.N * (fabs(mean.x) + fabs(mean.y))) * sqrt(G.scale);
     const double d = G.chain * 0x1p-53 * amp;
     ed[t] = band_db_bound64(Eb, K.nb, d) + band_db_bound64(En, K.nn, d) + 1e-13;
+}
+
+// frame_kernel with a compile-time R = 4 (C5) or the runtime loop
+inline void launch_frame(hipStream_t st, const RefineGeom &G, const RefineBins &K, const int64_t *fstart,
+                         const int64_t *fcs, const int64_t *bstart, const int64_t *bcs, int64_t nframes,
+                         int64_t nblocks, const double2 *rot, const double2 *blk, double *delta, double *ed,
+                         double2 *fsum) {
+    const dim3 grid((unsigned)((nframes + 255) / 256));
+    auto kern = G.R == 4 ? frame_kernel<4> : frame_kernel<0>;
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, G, K, fstart, fcs, bstart, bcs, nframes, nblocks, rot, blk,
+                       delta, ed, fsum);
 }
 
 }  // namespace
@@ -404,8 +432,7 @@ int msd_iq_delta64_sums_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t 
         KernelTimer timer(ctx, K_REFINE);
         if (int rc = launch_refine_i8(ctx, static_cast<const int16_t *>(x), G, K, d_bstart, d_bcs, nblocks, blk))
             return rc;
-        hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, GF, K, d_fstart,
-                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed, fsum);
+        launch_frame(st, GF, K, d_fstart, d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed, fsum);
         e = hipGetLastError();
     } else if (e == hipSuccess) {
         KernelTimer timer(ctx, K_REFINE);
@@ -438,8 +465,7 @@ int msd_iq_delta64_sums_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t 
                 hipLaunchKernelGGL(block_small_kernel<float>, dim3(grid), dim3(256), 0, st,
                                    static_cast<const float *>(x), G, K, d_bstart, d_bcs, nblocks, Wd, blk);
         }
-        hipLaunchKernelGGL(frame_kernel, dim3((unsigned)((nframes + 255) / 256)), dim3(256), 0, st, G, K, d_fstart,
-                           d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed, fsum);
+        launch_frame(st, G, K, d_fstart, d_fcs, d_bstart, d_bcs, nframes, nblocks, rot, blk, delta, ed, fsum);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return hip_fail(e, "msd_iq_delta64_dev");
