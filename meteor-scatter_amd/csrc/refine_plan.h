@@ -113,13 +113,21 @@ inline int plan_refine(int nperseg, int64_t hop, double fs, int band_lo, int ban
     G.rows = G.D % 64 == 0 ? 1 : 0;
     G.L = G.rows ? G.D / 16 : G.D;  // samples per Goertzel segment (direct products)
     // periodic Hann: sum w^2 = 3N/8 exactly; scipy's scale 1/(fs * sum(w^2)) from its float64 window
+    // (the sum per frame length kept per thread: N cosines cost ~0.1 ms of host time per call,
+    // which the C5 step paid between every two steps)
     {
-        double sw = 0.0;
-        for (int n = 0; n < N; ++n) {
-            const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * (double)n / (double)N);
-            sw += w * w;
+        static thread_local int sw_n = 0;
+        static thread_local double sw_v = 0.0;
+        if (sw_n != N) {
+            double sw = 0.0;
+            for (int n = 0; n < N; ++n) {
+                const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * (double)n / (double)N);
+                sw += w * w;
+            }
+            sw_v = sw;
+            sw_n = N;
         }
-        G.scale = 1.0 / (fs * sw);
+        G.scale = 1.0 / (fs * sw_v);
     }
     // rounding chains in units of u = 2^-53: ours -- the Goertzel recurrence over L samples (3 L
     // Gmax + 8, Gmax = min(1/|sin theta|, L) its error gain), the wave sum (6), the R-block
