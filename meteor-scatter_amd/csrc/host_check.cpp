@@ -354,6 +354,17 @@ int cmd_fuzz(uint64_t seed, int64_t iters) {
             std::printf("bad plan N %d hop %" PRId64 ": %s\n", N, hop, why.c_str());
             return 1;
         }
+        // the density scale from a fresh window sum (the planner keeps its sum per frame length;
+        // N changes between the plans here)
+        double sw = 0.0;
+        for (int n = 0; n < N; ++n) {
+            const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * (double)n / (double)N);
+            sw += w * w;
+        }
+        if (P.G.scale != 1.0 / (48000.0 * sw)) {
+            std::printf("bad plan N %d: density scale\n", N);
+            return 1;
+        }
         ++plans;
     }
     std::printf("ok %" PRId64 " parsed %" PRId64 " rejected %" PRId64 " plans\n", parsed, rejected, plans);
