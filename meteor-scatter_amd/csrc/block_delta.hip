@@ -304,8 +304,10 @@ int launch_bd2(msd_block_plan *p, const void *x, const int64_t *off, const int64
         MSD_HIP(hipMalloc(&p->d_energy, sizeof(double2) * (size_t)blocks));
         p->energy_cap = (size_t)blocks;
     }
-    // persistent grid: a few workgroups per CU, each walking groups of 16 blocks
-    const int64_t grid = std::min<int64_t>((blocks + BD2_GROUPS - 1) / BD2_GROUPS, (int64_t)p->ctx->num_cu * 8);
+    // persistent grid: a few workgroups per CU, each walking groups of 16 blocks (4 resident per CU;
+    // C3 A/B over two boxes, tools/gpu_r4s.sh: 4 per CU 0.409 ms, 8 0.381-0.393, 16 0.372-0.383,
+    // 32 0.382, one per group 0.398)
+    const int64_t grid = std::min<int64_t>((blocks + BD2_GROUPS - 1) / BD2_GROUPS, (int64_t)p->ctx->num_cu * 16);
     const size_t lds = sizeof(double) * (16 * bd2_pitch(SPL) + BD2_GROUPS * (size_t)(p->nbins > 0 ? p->nbins : 1));
     hipLaunchKernelGGL((block_delta2_kernel<T, SPL>), dim3((unsigned)grid), dim3(256), lds, p->ctx->stream,
                        static_cast<const T *>(x), off, len, nfiles, max_blocks, p->block_size, p->L, p->d_window,
