@@ -405,6 +405,10 @@ def run_c5(a, ctx, job, rank, world):
                                "4096/1024 float32 [T][4096] frame-major + per-frame band dB (950..1050 Hz vs "
                                "-3050..-2950 Hz) + adaptive detector over the whole stream (k 4, window 120 s = "
                                f"{det.W} frames, freeze 20 s, fixed init 10 s)",
+                   # the timed step: run(thresholds=False) -- the decisions and the detections' dB,
+                   # not the per-frame thresholds list proc_iq_samples returns (the CSV, main.py:640-658,
+                   # does not use it)
+                   "detector": "decisions only (thresholds list not materialised)",
                    "samples_per_gpu": samples, "frames_per_gpu": T, "frames_total": det.T, "bins": C5_N,
                    "parallelism": f"time shards over {world} GPU(s), 1 process per GPU"},
         "detections_per_step": int(len(res.detections)),
@@ -518,6 +522,12 @@ def dry_run(rank, world, files):
         while pid_dir and len(os.listdir(pid_dir)) < world and time.monotonic() < t_end:
             time.sleep(0.01)
         sys.exit(7)
+    if os.environ.get("MSD_DRYRUN_RCCL_FAIL_RANK") == str(rank):
+        # test hook: this rank's communicator init fails as libmsdsp reports it (MsdError with the
+        # msd_last_error text), through the same wrapper launch.Group uses
+        from meteorgpu import _lib
+        launch.open_comm(lambda: (_ for _ in ()).throw(
+            _lib.MsdError(-6, "msd_comm_init: ncclCommInitRank: unhandled system error (simulated)")), rank)
     launch.share_bytes(0, lambda: hashlib.sha1(uid).digest(), tag=f"seen{rank}")
     if rank != 0:
         return
@@ -531,13 +541,25 @@ def dry_run(rank, world, files):
     # files over the ranks, contiguous slices
     strong = {"files_total": files, "files_per_rank": [int(np.subtract(*shard_range(files, r, world)[::-1]))
                                                        for r in range(world)], "scaling": "strong"}
+    # the real line carries ranks_seen for the C3 leg (top level) and for the C5 leg ("c5")
     print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": len(seen), "id_agreed": ok,
-                      "strong_scaling": strong}), flush=True)
+                      "strong_scaling": strong, "c5": {"ranks_seen": len(seen)}}), flush=True)
     if not ok:
         sys.exit(1)
 
 
 def main():
+    try:
+        _main()
+    except BaseException as e:  # noqa: BLE001 -- the parent (launch.spawn) prints this rank's reason
+        if not (isinstance(e, SystemExit) and e.code in (0, None)):
+            from meteorgpu import launch
+            if launch.launched():
+                launch.report_failure(int(os.environ.get("RANK", "0")), f"{type(e).__name__}: {e}")
+        raise
+
+
+def _main():
     a = parse()
     from meteorgpu import launch
     if not launch.launched() and (a.gpus > 1 or a.spawn):
@@ -650,7 +672,8 @@ def main():
             out["c5"] = {k: c5[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "scaling",
                                             "dtype", "roofline", "kernel_ms_per_step", "detections_per_step",
                                             "state_rounds", "exact_threshold_frames", "config", "cpu_baseline",
-                                            "decisions", "certification", "modes", "exact_delta") if k in c5}
+                                            "decisions", "certification", "modes", "exact_delta",
+                                            "ranks_seen") if k in c5}
         except Exception as e:  # noqa: BLE001 -- one rank: the C3 line stands; several: fail as one job
             if world > 1:
                 raise

@@ -65,9 +65,28 @@ struct msd_ctx {
     // built once per (frame length, bins)
     void *i8_tab = nullptr;
     uint64_t i8_key = 0;
+    // ...and the exact (N, bins) they were built for: the hash only picks the candidate, a match
+    // needs these equal (a hash collision must not reuse another geometry's tables)
+    int i8_n = 0, i8_nk = 0;
+    int i8_km[16] = {};
     bool refine_goertzel = false;  // MSD_OPT_REFINE_GOERTZEL: int16 refinement on the float64 Goertzel
     int cstft_reserve = 0;         // MSD_OPT_CSTFT_RESERVE: workgroup slots the C5 spectrogram leaves free
 };
+
+namespace msd {
+// cos and sin of 2 pi j / N for any integer j, for host-built twiddle tables: j is reduced mod N into
+// [-N/2, N/2] in exact integer arithmetic, the angle and the functions are evaluated in long double
+// (x86-64: 64-bit significand), so each value rounded to double is within ~0.5 ulp of the exact one.
+// (A double angle 2 pi m / N up to 2 pi is itself off by up to ~2 pi u, several u of twiddle error.)
+inline void unit_root_ld(int64_t j, int64_t N, long double &c, long double &s) {
+    int64_t r = j % N;
+    if (r < 0) r += N;
+    if (2 * r > N) r -= N;
+    const long double a = 6.283185307179586476925286766559005768L * (long double)r / (long double)N;
+    c = cosl(a);
+    s = sinl(a);
+}
+}  // namespace msd
 
 struct msd_stft_plan {
     msd_ctx *ctx = nullptr;

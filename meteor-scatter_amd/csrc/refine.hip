@@ -367,9 +367,10 @@ int msd_iq_delta64_sums_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t 
     // ~0.2 ms, more than the refinement's other host work), kept on the context
     if (ctx->rf_w_n != N) {
         std::vector<double2> W(N);
-        for (int m = 0; m < N; ++m) {
-            const double a = -2.0 * M_PI * (double)m / (double)N;
-            W[m] = make_double2(std::cos(a), std::sin(a));
+        for (int m = 0; m < N; ++m) {  // W^m = cos - i sin of 2 pi m / N, each within ~0.5 ulp
+            long double c, sn;
+            unit_root_ld(m, N, c, sn);
+            W[m] = make_double2((double)c, -(double)sn);
         }
         MSD_HIP(hipStreamSynchronize(st));
         if (ctx->rf_w) MSD_HIP(hipFree(ctx->rf_w));
@@ -386,8 +387,9 @@ int msd_iq_delta64_sums_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t 
     for (int b = 0; b < K.nk; ++b)
         for (int j = 0; j < R; ++j) {
             const int64_t m = (int64_t)G.D * (((int64_t)K.km[b] * j) % R);
-            const double a = -2.0 * M_PI * (double)m / (double)N;
-            rt[(size_t)b * R + j] = make_double2(std::cos(a), std::sin(a));
+            long double c, sn;
+            unit_root_ld(m, N, c, sn);
+            rt[(size_t)b * R + j] = make_double2((double)c, -(double)sn);
         }
     const size_t nb_blk = (sizeof(double2) * (size_t)nblocks * (K.nk + 2) + 255) / 256 * 256;
     const size_t nb_rot = (sizeof(double2) * rt.size() + 255) / 256 * 256;

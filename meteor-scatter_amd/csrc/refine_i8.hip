@@ -336,7 +336,9 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
     const size_t nb_init = sizeof(int) * (size_t)NT * 16;
     const size_t nb_tw = sizeof(double2) * (size_t)(1 + (NT - 6)) * I8_SB * 16;
     const size_t nb_all = nb_frag + nb_init + nb_tw;
-    if (ctx->i8_key != key || !ctx->i8_tab) {
+    bool same = ctx->i8_tab && ctx->i8_key == key && ctx->i8_n == N && ctx->i8_nk == nk;
+    for (int b = 0; same && b < nk; ++b) same = ctx->i8_km[b] == K.km[b];
+    if (!same) {
         // column (t, c) -> (bin, part, digit), or -1
         auto colmap = [&](int t, int cc, int &bin, int &part, int &dig) {
             if (t < 6) {
@@ -364,12 +366,13 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
                 const int64_t km = K.km[bin];
                 for (int v = 0; v < KV; ++v) {
                     const int64_t m = v >> 1;
-                    const double a = 2.0 * M_PI * (double)((km * m) % N) / (double)N;
-                    const double C = std::cos(a), S = std::sin(a);
+                    long double C, S;  // cos, sin of 2 pi km m / N (reduced, long double)
+                    unit_root_ld(km * m, N, C, S);
                     // W^{km} = C - i S;  Y = sum (I + i Q)(C - i S): re = I C + Q S, im = Q C - I S
-                    const double val = part == 0 ? ((v & 1) ? S : C) : ((v & 1) ? C : -S);
+                    const long double val = part == 0 ? ((v & 1) ? S : C) : ((v & 1) ? C : -S);
                     int8_t d[I8_ND];
-                    balanced_digits((int64_t)std::llround(std::ldexp(val, 46)), d);
+                    // T = round(val 2^46) from the long-double value: |T 2^-46 - w| <= 2^-47 (1 + 2^-16)
+                    balanced_digits((int64_t)llroundl(ldexpl(val, 46)), d);
                     Bm[((size_t)t * KV + v) * 16 + cc] = d[dig];
                     init[t * 16 + cc] += 128 * (int)d[dig];
                 }
@@ -396,8 +399,9 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
                     if (bin < nk && (e > 0 || bin < 8)) {
                         // W^{256 k s} = cos - i sin: own part p, partner q: re = p cos + q sin (own re),
                         // im = p cos - q sin (own im, partner re)
-                        const double a = 2.0 * M_PI * (double)(((int64_t)K.km[bin] * I8_SUB * s) % N) / (double)N;
-                        w = make_double2(std::cos(a), part == 0 ? std::sin(a) : -std::sin(a));
+                        long double c, sn;
+                        unit_root_ld((int64_t)K.km[bin] * I8_SUB * s, N, c, sn);
+                        w = make_double2((double)c, part == 0 ? (double)sn : -(double)sn);
                     }
                     ltw[(e * I8_SB + r) * 16 + cc] = w;
                 }
@@ -409,6 +413,9 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
         MSD_HIP(hipMalloc(&ctx->i8_tab, nb_all));
         MSD_HIP(hipMemcpy(ctx->i8_tab, tab.data(), nb_all, hipMemcpyHostToDevice));
         ctx->i8_key = key;
+        ctx->i8_n = N;
+        ctx->i8_nk = nk;
+        for (int b = 0; b < nk; ++b) ctx->i8_km[b] = K.km[b];
     }
     const char *tb = static_cast<const char *>(ctx->i8_tab);
     const v4i *d_frag = reinterpret_cast<const v4i *>(tb);
@@ -439,7 +446,8 @@ int launch_refine_i8(msd_ctx *ctx, const int16_t *x, const RefineGeom &G, const 
 }
 
 // our float64-side rounding chain in units of u = 2^-53 (refine_plan.h's `own`): the twiddles'
-// quantisation sqrt 2 * 2^-47 per unit |x| (90.5), the digit Horner sum (6), the 4 sub-block
+// quantisation sqrt 2 * 2^-47 (1 + 2^-16) per unit |x| (90.5; each entry rounded from a long-double
+// unit root whose argument was reduced exactly, unit_root_ld), the digit Horner sum (6), the 4 sub-block
 // products summed with rounded twiddles in one 8-FMA chain (10; the budget kept at 22, the
 // 16-sub-block layout's figure)
 double i8_chain_own() { return 91.0 + 6.0 + 22.0; }

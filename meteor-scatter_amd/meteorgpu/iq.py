@@ -256,16 +256,28 @@ class IQShardDetector:
         self.d_frames.upload(np.array([self.batch.T if self.s1 > self.s0 else 0], np.int64))
         cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
         self.overlap = int(overlap)
-        self.dctx = ctx.sibling() if self.overlap > 0 else ctx  # the detector's context
-        if self.overlap > 0:
-            ctx.set_option(_lib.OPT_CSTFT_RESERVE, self.overlap)
-        self.plan = _lib.StreamPlan(self.dctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
-        self.ops = _stream.DeviceStreamOps(self.plan)
-        self.d_etot = None
-        self.d_fsum = None  # exact delta: the frames' sample sums, shared with the spectrogram's detrend
-        self._fsums_ok = True
-        self.certify = False
-        self.set_certify(certify)
+        self.dctx = ctx  # the detector's context
+        self.plan = None
+        # the caller's spectrogram reserve (MSD_OPT_CSTFT_RESERVE is context-wide and ctx may be the
+        # process-wide one): restored by close(), or here if the constructor fails after changing it
+        self._reserve_prev = ctx.options.get(_lib.OPT_CSTFT_RESERVE, 0)
+        try:
+            if self.overlap > 0:
+                self.dctx = ctx.sibling()
+                ctx.set_option(_lib.OPT_CSTFT_RESERVE, self.overlap)
+            self.plan = _lib.StreamPlan(self.dctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
+            self.ops = _stream.DeviceStreamOps(self.plan)
+            self.d_etot = None
+            self.d_fsum = None  # exact delta: the frames' sample sums, shared with the spectrogram's detrend
+            self._fsums_ok = True
+            self.certify = False
+            self.set_certify(certify)
+        except BaseException:
+            self._release_overlap()
+            if self.plan is not None:
+                self.plan.close()
+            self.batch.close()
+            raise
         self.fs_ = float(fs)
         self._read = None      # the shard's sample source when chunked (refinement re-reads samples)
         self._refined = _NO_IV  # global frame ranges whose delta is float64 already (merged, (n, 2))
@@ -496,9 +508,15 @@ class IQShardDetector:
             self.d_etot.free()
         if self.d_fsum is not None:
             self.d_fsum.free()
+        self._release_overlap()
+
+    def _release_overlap(self):
+        """the sibling context closed, the caller's reserve value back"""
         if self.dctx is not self.ctx:
             self.dctx.close()
-            self.ctx.set_option(_lib.OPT_CSTFT_RESERVE, 0)
+            self.dctx = self.ctx
+        if self.ctx.options.get(_lib.OPT_CSTFT_RESERVE, 0) != self._reserve_prev:
+            self.ctx.set_option(_lib.OPT_CSTFT_RESERVE, self._reserve_prev)
 
 
 def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072, threshold_std_factor=4.0,

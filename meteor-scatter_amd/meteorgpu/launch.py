@@ -115,6 +115,36 @@ def release(rank: int, tag: str = "rccl") -> None:
             pass
 
 
+def report_failure(rank: int, text: str) -> None:
+    """A rank's failure text for the parent: spawn() prints it beside the exit code (only under
+    spawn, whose rendezvous key names the file and whose cleanup removes it)."""
+    if not os.environ.get("MSD_RDZV_KEY"):
+        return
+    try:
+        with open(rdzv_path(f"err{rank}"), "w") as fh:
+            fh.write(text[-4000:])
+    except OSError:
+        pass
+
+
+def _failure_text(key: str, rank: int) -> str:
+    try:
+        with open(os.path.join(_rdzv_dir(), f"msd_rdzv_{key}_err{rank}.bin")) as fh:
+            return fh.read().strip()
+    except OSError:
+        return ""
+
+
+def open_comm(make, rank: int):
+    """``make()`` → the job's RCCL communicator.  A failure keeps libmsdsp's own message (the
+    ``msd_last_error`` text MsdError carries: RCCL's error string, a missing librccl, a bad id)
+    and names the rank, so the parent's exit message says why the job failed."""
+    try:
+        return make()
+    except Exception as e:  # noqa: BLE001 -- re-raised with the rank and the library's text
+        raise RuntimeError(f"rank {rank}: RCCL communicator init failed: {e}") from e
+
+
 def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -148,6 +178,10 @@ def spawn(argv: list[str], nprocs: int, env: dict | None = None, poll_s: float =
                 live.remove(p)
                 if code != 0 and rc == 0:
                     rc = code if code > 0 else 128 - code
+                    r = procs.index(p)
+                    why = _failure_text(base["MSD_RDZV_KEY"], r)
+                    print(f"meteorgpu.launch: rank {r} of {nprocs} exited with code {code}"
+                          + (f": {why}" if why else ""), file=sys.stderr, flush=True)
                     for q in live:
                         q.terminate()
             time.sleep(poll_s)
@@ -178,7 +212,7 @@ class Group:
         from .stream import RcclComm
         self.ctx, self.rank, self.world = ctx, int(rank), int(world)
         uid = share_bytes(self.rank, Communicator.unique_id)
-        self.rccl = Communicator(ctx, self.world, uid, self.rank)
+        self.rccl = open_comm(lambda: Communicator(ctx, self.world, uid, self.rank), self.rank)
         self.comm = RcclComm(self.rccl, self.rank, self.world)
         self._one = ctx.alloc(8)
         self._lib = _lib

@@ -30,7 +30,9 @@ def test_bench_spawns_n_ranks(n, tmp_path):
     assert len(lines) == 1, r.stdout  # only rank 0 prints
     d = json.loads(lines[0])
     strong = d.pop("strong_scaling")
+    c5 = d.pop("c5")
     assert d == {"dry_run": True, "n_gpus": n, "ranks_seen": n, "id_agreed": True}
+    assert c5 == {"ranks_seen": n}  # the C5 leg's own rank count (weak-scaled stream)
     # the C4 (strong scaling) pass the real N-rank line carries: one 1440-file day over the n ranks
     assert strong["scaling"] == "strong" and strong["files_total"] == 1440
     assert sum(strong["files_per_rank"]) == 1440 and max(strong["files_per_rank"]) == -(-1440 // n)
@@ -131,3 +133,15 @@ def test_rank_dying_after_init_fails_the_job(tmp_path):
         with pytest.raises(ProcessLookupError):
             os.kill(pid, 0)  # gone (spawn waited for it: no zombie left either)
     assert not [p for p in tmp_path.iterdir() if p.name.startswith("msd_rdzv_")]  # rendezvous cleaned up
+
+
+def test_rccl_init_failure_text_reaches_the_parent(tmp_path):
+    """a rank whose communicator init fails: the parent's exit message names the rank and carries
+    libmsdsp's own error text (msd_last_error through MsdError), not only an exit code"""
+    r = _run([sys.executable, BENCH, "--gpus", "3", "--dry-run"],
+             env={"MSD_RDZV_DIR": str(tmp_path), "MSD_DRYRUN_RCCL_FAIL_RANK": "1"}, timeout=100)
+    assert r.returncode != 0
+    line = [ln for ln in r.stderr.splitlines() if ln.startswith("meteorgpu.launch: rank 1 of 3")]
+    assert line, r.stderr[-2000:]
+    assert "RCCL communicator init failed" in line[0] and "ncclCommInitRank" in line[0], line[0]
+    assert not [p for p in tmp_path.iterdir() if p.name.startswith("msd_rdzv_")]

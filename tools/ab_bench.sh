@@ -9,7 +9,7 @@ WL=${WL:-c3}
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 for i in $(seq 1 "$N"); do
   for t in "$@"; do
-    lib=$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp_$t.so
+    lib=$ROOT/tools/ubench/bin/libmsdsp_$t.so
     [ "$t" = cur ] && lib=$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp.so
     extra=""; [ "$WL" = c3 ] && extra="--no-c5"
     MSD_LIB_PATH=$lib timeout -k 10 200 python3 "$ROOT/bench.py" --workload "$WL" --steps 10 --warmup 2 \

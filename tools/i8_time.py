@@ -46,7 +46,8 @@ if __name__ == "__main__":
         one(sys.argv[2])
         sys.exit(0)
     for t in sys.argv[1:] or ["cur"]:
-        lib = os.path.join(ROOT, "meteor-scatter_amd/meteorgpu", "libmsdsp.so" if t == "cur" else f"libmsdsp_{t}.so")
+        lib = (os.path.join(ROOT, "meteor-scatter_amd/meteorgpu", "libmsdsp.so") if t == "cur"
+               else os.path.join(ROOT, "tools/ubench/bin", f"libmsdsp_{t}.so"))
         env = dict(os.environ, MSD_LIB_PATH=lib)
         rc = subprocess.run([sys.executable, __file__, "--one", t], env=env, timeout=300).returncode
         if rc:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the working tree's libmsdsp.so with experiment patches applied to a temporary copy of
-# csrc into meteorgpu/libmsdsp_<tag>.so (A/B variants stay out of the product sources; time them
+# csrc into tools/ubench/bin/libmsdsp_<tag>.so (A/B variants stay out of the product sources; time them
 # with tools/stft_ab or tools/ab_bench.sh).  Usage: tools/patch_build.sh TAG [PATCH ...]
 # (patches: unified diffs relative to meteor-scatter_amd/csrc, e.g. tools/experiments/*.patch)
 set -euo pipefail
@@ -12,6 +12,7 @@ rm -rf "$W/meteor-scatter_amd/csrc/build"
 for p in "$@"; do
   patch -s -d "$W/meteor-scatter_amd/csrc" -p1 < "$ROOT/$p"
 done
-make -s -C "$W/meteor-scatter_amd/csrc" -j8 ${MKARGS:-} OUT="$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp_$TAG.so" >/dev/null
+mkdir -p "$ROOT/tools/ubench/bin"
+make -s -C "$W/meteor-scatter_amd/csrc" -j8 ${MKARGS:-} OUT="$ROOT/tools/ubench/bin/libmsdsp_$TAG.so" >/dev/null
 rm -rf "$W"
-echo "built meteorgpu/libmsdsp_$TAG.so ($*)"
+echo "built tools/ubench/bin/libmsdsp_$TAG.so ($*)"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the WORKING TREE's libmsdsp.so with extra compiler flags into
-# meteorgpu/libmsdsp_<tag>.so (experiment variants selected by -D macros; timing with
+# tools/ubench/bin/libmsdsp_<tag>.so (experiment variants selected by -D macros; timing with
 # tools/ab_bench.sh).  Usage: tools/variant_build.sh TAG "EXTRA FLAGS"
 set -euo pipefail
 TAG=$1; EXTRA=${2:-}
@@ -8,6 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 W=$(mktemp -d /tmp/var_XXXX)
 mkdir -p "$W/meteor-scatter_amd" && cp -r "$ROOT/meteor-scatter_amd/csrc" "$W/meteor-scatter_amd/" && cp -r "$ROOT/include" "$W/"
 rm -rf "$W/meteor-scatter_amd/csrc/build"
-make -s -C "$W/meteor-scatter_amd/csrc" -j8 EXTRA="$EXTRA" ${MKARGS:-} OUT="$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp_$TAG.so" >/dev/null
+mkdir -p "$ROOT/tools/ubench/bin"
+make -s -C "$W/meteor-scatter_amd/csrc" -j8 EXTRA="$EXTRA" ${MKARGS:-} OUT="$ROOT/tools/ubench/bin/libmsdsp_$TAG.so" >/dev/null
 rm -rf "$W"
-echo "built meteorgpu/libmsdsp_$TAG.so (EXTRA=$EXTRA)"
+echo "built tools/ubench/bin/libmsdsp_$TAG.so (EXTRA=$EXTRA)"
