@@ -75,9 +75,9 @@ def parse():
                          "ones and every detection's frames recomputed in float64 (round 3's certified path); "
                          "all = the line on 'exact', plus the other modes timed under \"modes\"")
     ap.add_argument("--c5-overlap", type=int, default=0,
-                    help="C5: run the stream detector on a second HIP stream beside the spectrogram, which leaves "
-                         "this many workgroup slots free (exact delta only: the detector does not read the "
-                         "spectrogram); 0 = one stream")
+                    help="C5: split the chip after the delta step -- the stream detector on this many CUs, the "
+                         "spectrogram on the rest, side by side (CU-masked streams; exact delta only: the "
+                         "detector does not read the spectrogram); 0 = one stream, in order")
     ap.add_argument("--shard-day", action="store_true",
                     help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
                          "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "
@@ -318,11 +318,14 @@ def run_c5(a, ctx, job, rank, world):
     for _ in range(a.warmup):
         res = step()
     sync_all()
-    # the timed region carries events only around the roofline kernel; the per-kernel breakdown
+    # the timed region carries events only around the roofline kernel (on the spectrogram's context:
+    # the caller's, or its CU-split sibling with --c5-overlap); the per-kernel breakdown
     # (kernel_ms_per_step) comes from one more step with every kernel timed, after it
-    ctx.timing_select([_lib.K_CSTFT])
-    ctx.timing(True)
-    ctx.timing_reset()
+    sctx = det.sctx
+    ctxs = [ctx] + [c for c in {id(det.sctx): det.sctx, id(det.dctx): det.dctx}.values() if c is not ctx]
+    sctx.timing_select([_lib.K_CSTFT])
+    sctx.timing(True)
+    sctx.timing_reset()
     sync_all()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -331,24 +334,20 @@ def run_c5(a, ctx, job, rank, world):
     elapsed = time.perf_counter() - t0
     if job is not None:
         elapsed = job.max_f64(elapsed)
-    k_ms, k_n = ctx.timing_get(_lib.K_CSTFT)
-    ctx.timing_select(None)
-    ctx.timing_reset()
-    dctx = det.dctx if det.dctx is not ctx else None
-    if dctx is not None:  # the detector's own context (overlap)
-        dctx.timing(True)
-        dctx.timing_reset()
+    k_ms, k_n = sctx.timing_get(_lib.K_CSTFT)
+    sctx.timing_select(None)
+    for c in ctxs:
+        c.timing(True)
+        c.timing_reset()
     step()
     sync_all()
     kms = {}
-    for name, kid in (("cstft", _lib.K_CSTFT), ("cstft_dc_fix", _lib.K_CSTFT_DC), ("band_delta", _lib.K_IQDELTA),
+    for name, kid in (("cstft", _lib.K_CSTFT), ("band_delta", _lib.K_IQDELTA),
                       ("fresh_thresholds", _lib.K_FRESH), ("scan", _lib.K_SSCAN), ("delta64", _lib.K_REFINE)):
-        ms, cnt = ctx.timing_get(kid)
-        if dctx is not None:
-            ms += dctx.timing_get(kid)[0]
-        kms[name] = round(ms, 4)
-    if dctx is not None:
-        dctx.timing(False)
+        kms[name] = round(sum(c.timing_get(kid)[0] for c in ctxs), 4)
+    for c in ctxs:
+        if c is not ctx:
+            c.timing(False)
     kms["cstft"] = round(k_ms / max(k_n, 1), 4)  # the timed region's average
 
     def cert_info(r, m):

@@ -77,11 +77,16 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
  * Goertzel kernel instead of the exact int8-MFMA one (A/B; both within their bounds).
  * MSD_OPT_CSTFT_RESERVE = n → the persistent C5 spectrogram kernel (msd_cstft_psd_dev) leaves n
  * of its resident workgroup slots free, so that small kernels on another context's stream (the
- * stream detector, when its delta does not come from the spectrogram) run beside it. */
+ * stream detector, when its delta does not come from the spectrogram) run beside it.
+ * MSD_OPT_STREAM_CUS = n → the context's stream is re-created on a subset of the device's CUs
+ * (hipExtStreamCreateWithCUMask): n > 0 the first n CUs, n < 0 all but those |n| -- two contexts
+ * set to n and -n split the chip into disjoint parts --, 0 all CUs again; persistent grids are
+ * sized for the CUs the stream may use.  Synchronises the context's stream first. */
 #define MSD_OPT_GENERIC_STFT 1
 #define MSD_OPT_FRESH_ALL 2
 #define MSD_OPT_REFINE_GOERTZEL 3
 #define MSD_OPT_CSTFT_RESERVE 4
+#define MSD_OPT_STREAM_CUS 5
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.
@@ -227,9 +232,11 @@ int msd_cstft_psd_energy_dev(msd_cstft_plan *plan, const void *x, int dtype, con
                              int64_t nstreams, int64_t max_frames, float *out, float *etot);
 /* the same, with each frame's complex sample sum given (frame_sums: device double [nstreams *
  * max_frames][2], (sum I, sum Q) of frame s*max_frames + t, e.g. from msd_iq_delta64_sums_dev):
- * the plan's C5 geometry (hop 1024, a window whose DFT vanishes outside bins 0, +-1 such as the
- * periodic Hann) then detrends after the FFT from these sums and computes none itself; other
- * geometries ignore them.  Same output as msd_cstft_psd_energy_dev within float32 rounding. */
+ * at the C5 hop (1024) the kernel then takes each frame's detrend mean from these sums and computes
+ * none itself; other hops ignore them.  Exact sums (int16 input) give output bit-identical to
+ * msd_cstft_psd_energy_dev.  Either way the mean is subtracted before the window as an exact
+ * two-part float32 value (hi + lo), so the result is scipy's within float32 rounding of the
+ * detrended samples whatever the DC offset. */
 int msd_cstft_psd_fsums_dev(msd_cstft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                             int64_t nstreams, int64_t max_frames, float *out, float *etot, const double *frame_sums);
 int64_t msd_cstft_energy_stride(int64_t nstreams, int64_t max_frames);

@@ -11,6 +11,8 @@
 #include <set>
 #include <tuple>
 
+#include <vector>
+
 #include "msd_internal.h"
 
 namespace msd {
@@ -158,6 +160,7 @@ int msd_create(int device, msd_ctx **out) {
     if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
         c->num_cu <= 0)
         c->num_cu = 256;  // grid sizing only: a wrong count costs balance, not correctness
+    c->num_cu_dev = c->num_cu;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -252,6 +255,29 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
             if (value < 0) return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_CSTFT_RESERVE must be >= 0");
             ctx->cstft_reserve = value;
             return MSD_OK;
+        case MSD_OPT_STREAM_CUS: {
+            // the context's stream re-created on a CU subset: n > 0 the first n CUs of the mask, n < 0
+            // all but those |n| (the two are disjoint), 0 every CU; grid sizing follows (num_cu)
+            const int total = ctx->num_cu_dev;
+            if (value >= total || -value >= total)
+                return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_STREAM_CUS out of range");
+            DeviceGuard g(ctx->device);
+            MSD_HIP(hipStreamSynchronize(ctx->stream));
+            hipStream_t st = nullptr;
+            if (value == 0) {
+                MSD_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            } else {
+                std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
+                const int lo = value > 0 ? 0 : -value, hi = value > 0 ? value : total;
+                for (int c = lo; c < hi; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+                MSD_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+            }
+            MSD_HIP(hipStreamDestroy(ctx->stream));
+            ctx->stream = st;
+            ctx->num_cu = value == 0 ? total : value > 0 ? value : total + value;
+            ctx->stream_cus = value;
+            return MSD_OK;
+        }
         default: return fail(MSD_ERR_INVALID, "msd_set_option: unknown option");
     }
 }

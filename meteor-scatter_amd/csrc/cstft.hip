@@ -102,13 +102,18 @@ struct IQ<int16_t> {  // interleaved int16 I, Q
         sr = (int)a;
         si = (int)b;
     }
-    // the frame mean from the four waves' exact sums (|total| <= 2^27): float(total) / 4096 is
-    // float((double)total / 4096), the power-of-two scale commuting with the rounding
-    __device__ static float mean(const int *red) {
-        return (float)(red[0] + red[1] + red[2] + red[3]) * (1.0f / CS_N);
+    // the frame total from the four waves' exact sums (|total| < 2^28)
+    __device__ static int total(const int *red) { return red[0] + red[1] + red[2] + red[3]; }
+    // the same from an exact float64 total (msd_cstft_psd_fsums_dev: integer-valued)
+    __device__ static int total_d(double t) { return (int)t; }
+    // the mean total / 4096 as hi + lo, both exact: hi = float(total) / 4096 (float(total) rounds
+    // the integer to 24 bits; |total| < 2^24, i.e. |mean| < 4096, is exact already and lo = 0), lo =
+    // (total - float(total)) / 4096 (an integer of at most 4 bits / 4096)
+    __device__ static void mean2(int tot, float &hi, float &lo) {
+        const float f = (float)tot;
+        hi = f * (1.0f / CS_N);
+        lo = (float)(tot - (int)f) * (1.0f / CS_N);
     }
-    // the same from an exact float64 total (msd_cstft_psd_fsums_dev)
-    __device__ static float mean_d(double total) { return (float)total * (1.0f / CS_N); }
 };
 template <>
 struct IQ<float> {  // interleaved float32 I, Q (complex64)
@@ -127,10 +132,16 @@ struct IQ<float> {  // interleaved float32 I, Q (complex64)
             si += v[r].y;
         }
     }
-    __device__ static float mean(const float *red) {
-        return (float)(((double)red[0] + (double)red[1] + (double)red[2] + (double)red[3]) * (1.0 / CS_N));
+    __device__ static double total(const float *red) {
+        return (double)red[0] + (double)red[1] + (double)red[2] + (double)red[3];
     }
-    __device__ static float mean_d(double total) { return (float)(total * (1.0 / CS_N)); }
+    __device__ static double total_d(double t) { return t; }
+    // mean = hi + lo to float64 precision (hi its float32 rounding, lo the float32 of the rest)
+    __device__ static void mean2(double tot, float &hi, float &lo) {
+        const double m = tot * (1.0 / CS_N);
+        hi = (float)m;
+        lo = (float)(m - (double)hi);
+    }
 };
 
 // int16 I/Q runs 4 waves per SIMD: 128 VGPRs with the [k][j1] pass-2 twiddle table (its reads need
@@ -155,38 +166,24 @@ struct CsTune {
 // frame a row DPP reduction gives the row's partial (>= every frame's: a sum of maxima), stored for
 // each frame of the group -- 16 adds and a max per thread and frame, the reduction and 4 stores per
 // 4 frames (per frame: +5.6 % of the kernel, 12.03 -> 12.71 ms at C5)
-// PD (post-FFT detrend at C5's hop of 1024, windows whose DFT is nonzero only at bins 0 and +-1 --
-// the periodic Hann): the FFT runs on w x, and bins 0, 1, N - 1 get - mean * W_k afterwards (W =
-// the window's DFT), equal to the FFT of w (x - mean) in exact arithmetic.  The frame's mean then
-// never waits for a cross-wave sum: the kernel leaves the sums of the frame's NEWEST block (its
-// 1024 new samples: a frame is 4 blocks, each block new in exactly one frame) and the three raw
-// bins in `side` (CsSide per frame); dc_fix_kernel adds the frame's four blocks (the records of
-// frames t - 3 .. t, the stream's first three blocks from cs_head_kernel) and rewrites the three
-// powers.  The barrier that had to follow the sums now only has to precede the pass-1 LDS write
-// (every wave past the previous frame's pass-3 reads), so pass 1 runs beside the slower waves'
-// pass 3; the thread partials (4 rows instead of 16) ride in the pass-1 layout's spare LDS
-// columns and one wave in turn reduces them (PD 1).  PD 2 (msd_cstft_psd_fsums_dev: the frame
-// sums given, from the exact delta step) computes no sums at all; dc_fix_kernel reads them.  The
-// energy partials (EN) see the raw powers of the three bins: the FFT input is w x.
-template <typename T>
-struct alignas(64) CsSide {
-    typename IQ<T>::acc_t sum[2];  // the I and Q sums of block t + 3
-    float pad_;
-    float pad2_;
-    float2 raw[3];                 // X[0], X[1], X[N - 1] of w x
-};
-// per stream: the I and Q sums of blocks 0, 1, 2 (frame 0's older blocks)
-template <typename T>
-struct CsHead {
-    typename IQ<T>::acc_t sum[3][2];
-};
-
+// Detrend (scipy 'constant', before the window): the frame's complex mean m is subtracted from every
+// sample in float32 as (x - hi) - lo, m = hi + lo both exact (IQ<T>::mean2), so the detrended sample
+// is the float32 rounding of the float64 x - m.  A single float32 mean would leave the coherent error
+// |m - float(m)| <= 2^-24 |m| in every sample, i.e. a residual DC of that size at bins 0, +-1 (for
+// int16 I/Q from |m| >= 4096 on: up to 2e-3 relative per frame against scipy at a 16000 offset over
+// quiet noise, tools/dbg/dc_precision.py); lo is zero below that and the frame then takes the
+// one-subtraction path (a wave-uniform branch).  The round-4 post-FFT detrend (FFT of w x, bins 0,
+// +-1 corrected afterwards) was cheaper but its rounding scales with the DC energy in EVERY bin:
+// 2.7e-5 per frame at a 700 offset over sigma-3 noise; removed.
+// PD 0: the sums in the kernel (exact integer DPP sums per wave, one LDS slot per wave, a barrier);
+// PD 2 (msd_cstft_psd_fsums_dev): the frames' sums given (fsum[g], the exact delta step's): no
+// reduction and no barrier before pass 1, the next frame's sums prefetched with its samples.
 template <typename T, int SH, bool EN, int PD>
 __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft4096_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len, int64_t nstreams,
     int64_t max_frames, int64_t total, int64_t per, int hop, int detrend, const float *__restrict__ g_win,
     const float2 *__restrict__ g_tw, float *__restrict__ out, float *__restrict__ etot, int64_t estride,
-    CsSide<T> *__restrict__ side) {
+    const double2 *__restrict__ fsum) {
     using io = IQ<T>;
     __shared__ float2 buf[CS_LDS_F2];
     // pass-2 twiddles W256^(j1 k).  kW4: at k * 16 + j1 — a half-wave reads 16 consecutive entries
@@ -212,10 +209,6 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
     float emax = 0.f;  // EN: max over the frames of the current group of this thread's power sum
     const int q2 = tid >> 4, j1 = tid & 15;   // pass-2 thread: (q, j1)
     const int q3 = tid & 15, k2a = tid >> 4;  // pass-3 thread: t = q + 16 k2a
-    auto side_rsrc = [&](int64_t g) {  // PD: frame g's CsSide (64 B records)
-        return __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<char *>(uniform_i64(reinterpret_cast<int64_t>(side) + 64 * g)), 0, 64, 0x00020000);
-    };
     __syncthreads();
 
     const int64_t g0 = (int64_t)blockIdx.x * per;
@@ -242,20 +235,30 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
         const int64_t base = off[s];
         float *of = out + ga * (int64_t)CS_N;
         // one frame: consumes raw (frame g), prefetches frame g + 1 into raw, writes `of`
+        double2 fnext = make_double2(0.0, 0.0);  // PD 2: the sums of the frame raw holds
+        // float32 I/Q, PD 0: the frame's first sample, subtracted before the float sums so that they
+        // accumulate the variation, not the offset (a float sum of 4096 values near a DC m is off by
+        // ~24 u |m|, which would leave that as a residual DC); the mean is then xref + sum / 4096
+        constexpr bool REF = std::is_same<T, float>::value && PD == 0;
+        float2 xnext = make_float2(0.f, 0.f);
+        auto first_sample = [&](int64_t t) {
+            return *reinterpret_cast<const float2 *>(x + 2 * uniform_i64(base + t * (int64_t)hop));
+        };
         auto frame = [&](int64_t g, float *of) __attribute__((always_inline)) {
             float2 v[16];
             // ---- detrend: the frame's complex mean (scipy 'constant'): exact integer sums for
-            // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; !PD: per wave, then one LDS
-            // slot per wave
+            // int16 I/Q (|sum| < 2^28), float sums for float32 I/Q; PD 0: per wave, then one LDS
+            // slot per wave; PD 2: given
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = io::f(raw[r]);
-            // PD: the thread's part of the frame's newest block (rows 12..15: block t + 3 of the
-            // stream), reduced after the pass-1 barrier by one wave (below)
-            float pa = 0.f, pb = 0.f;
-            if constexpr (PD == 1) {
+            const float2 xref = xnext;
+            if constexpr (REF) {
+                if (detrend) {
 #pragma unroll
-                for (int r = 12; r < 16; ++r) pa += v[r].x, pb += v[r].y;
-            } else if constexpr (PD == 0) {
+                    for (int r = 0; r < 16; ++r) v[r] = c_sub(v[r], xref);
+                }
+            }
+            if constexpr (PD == 0) {
                 typename io::acc_t sr, si;
                 io::thread_sums(v, sr, si);
                 sr = io::wave_sum(sr);  // DPP row sums + readlane: no LDS round trips
@@ -265,6 +268,7 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
                     red[1][wave] = si;
                 }
             }
+            const double2 fcur = fnext;
             {  // prefetch frame t + 1 (raw is consumed); the segment's last frame reloads itself
                 const int64_t tn = (g + 1 < gv ? g + 1 : g) - s * max_frames;
                 if constexpr (SH > 0) {  // (after the segment's last frame raw is dead)
@@ -274,17 +278,26 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
                 } else {
                     load_rows(base, tn, std::integral_constant<int, 0>{});
                 }
+                if constexpr (PD == 2) fnext = fsum[uniform_i64(s * max_frames + tn)];
+                if constexpr (REF) xnext = first_sample(tn);
             }
-            if constexpr (PD) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = make_float2(v[r].x * wr[r], v[r].y * wr[r]);
+            float mr = 0.f, lr = 0.f, mi = 0.f, li = 0.f;
+            if constexpr (PD == 2) {
+                io::mean2(io::total_d(fcur.x), mr, lr);
+                io::mean2(io::total_d(fcur.y), mi, li);
             } else {
                 lds_barrier();
-                float mr = 0.f, mi = 0.f;
-                if (detrend) {
-                    mr = io::mean(red[0]);
-                    mi = io::mean(red[1]);
-                }
+                io::mean2(io::total(red[0]), mr, lr);
+                io::mean2(io::total(red[1]), mi, li);
+            }
+            if (!detrend) mr = lr = mi = li = 0.f;
+            // lo is wave-uniform: a branch, not a select -- frames with |mean| < 4096 (int16) pay one
+            // subtraction per value
+            if (__builtin_amdgcn_readfirstlane(lr != 0.f || li != 0.f)) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    v[r] = make_float2(((v[r].x - mr) - lr) * wr[r], ((v[r].y - mi) - li) * wr[r]);
+            } else {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) v[r] = make_float2((v[r].x - mr) * wr[r], (v[r].y - mi) * wr[r]);
             }
@@ -292,36 +305,10 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
             dft16(v);
 #pragma unroll
             for (int q = 1; q < 16; ++q) v[q] = c_mul(v[q], tw1[q]);
-            if constexpr (PD) {
-                lds_barrier();  // everyone has read the previous frame's pass-2 layout
-                // PD 1: the block partials into the pass-1 layout's spare columns 256..271
-                if constexpr (PD == 1) buf[(tid >> 4) * CS_P + CS_T + (tid & 15)] = make_float2(pa, pb);
-            }
+            if constexpr (PD == 2) lds_barrier();  // everyone has read the previous frame's pass-2 layout
 #pragma unroll
             for (int q = 0; q < 16; ++q) buf[q * CS_P + tid] = v[q];
             lds_barrier();
-            if constexpr (PD == 1) {
-                // one wave per frame (in turn) sums the 256 partials -- a quarter of the reduction
-                // work of every wave reducing its own -- and leaves the block's sums in the frame's
-                // CsSide (lane 0, through a buffer resource on its uniform address)
-                if (wave == (int)(g & 3)) {
-                    float a = 0.f, b = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int t = lane + 64 * k;
-                        const float2 pp = buf[(t >> 4) * CS_P + CS_T + (t & 15)];
-                        a += pp.x;
-                        b += pp.y;
-                    }
-                    const typename io::acc_t sa = io::wave_sum((typename io::acc_t)a);
-                    const typename io::acc_t sb = io::wave_sum((typename io::acc_t)b);
-                    if (lane == 0) {
-                        const auto rs = side_rsrc(g);
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sa), rs, 0, 0, 0);
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sb), rs, 4, 0, 0);
-                    }
-                }
-            }
             // ---- pass 2: thread (q, j1): DFT over j2 of y[q][j1 + 16 j2], twiddle W256^(j1 k2a)
 #pragma unroll
             for (int j2 = 0; j2 < 16; ++j2) v[j2] = buf[q2 * CS_P + j1 + 16 * j2];
@@ -336,13 +323,6 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
 #pragma unroll
             for (int j = 0; j < 16; ++j) v[j] = buf[(16 * k2a + j) * 17 + q3];
             dft16(v);
-            if constexpr (PD) {  // the raw DC bins for dc_fix_kernel (threads 0, 1: v[0]; 255: v[15])
-                const int o = tid <= 1 ? (int)offsetof(CsSide<T>, raw) + 8 * tid
-                                       : tid == CS_T - 1 ? (int)offsetof(CsSide<T>, raw) + 16 : 1 << 20;
-                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                const float2 b = tid == CS_T - 1 ? v[15] : v[0];
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), side_rsrc(g), o, 0, 0);
-            }
             // the frame's 16 KB through a buffer resource on its (wave-uniform) base: the thread's
             // byte offset in a VGPR, the row offset 1 KB * k2b as the scalar offset, no per-lane
             // 64-bit address arithmetic; streaming (non-temporal) stores, written once (A/B: -1 to -2 %)
@@ -367,7 +347,7 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
                     emax = 0.f;
                 }
             }
-            // no barrier at the end: the next frame writes buf (and, !PD, red) only after its first
+            // no barrier at the end: the next frame writes buf (and, PD 0, red) only after its first
             // barrier, which every wave reaches after its pass-3 reads of this frame
         };
         // The first frame is peeled off the loop: both ways into the loop then end with the
@@ -376,6 +356,8 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
         // stores in one vmcnt; a loop entered straight after a load would wait vmcnt(0)).
         if (ga < gv) {
             load_rows(base, ga - s * max_frames, std::integral_constant<int, 0>{});
+            if constexpr (PD == 2) fnext = fsum[uniform_i64(ga)];
+            if constexpr (REF) xnext = first_sample(ga - s * max_frames);
             frame(ga, of);
             of += CS_N;
             for (int64_t g = ga + 1; g < gv; ++g, of += CS_N) frame(g, of);
@@ -387,88 +369,12 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
     }
 }
 
-// PD, before dc_fix_kernel: the sums of blocks 0, 1, 2 of every stream with a frame (one workgroup
-// per stream and block; exact integer sums for int16, float per thread then double for float32)
-template <typename T>
-__global__ __launch_bounds__(256) void cs_head_kernel(const T *__restrict__ x, const int64_t *__restrict__ off,
-                                                      const int64_t *__restrict__ len, int hop,
-                                                      CsHead<T> *__restrict__ head) {
-    using io = IQ<T>;
-    const int64_t s = blockIdx.x / 3;
-    const int b = blockIdx.x % 3;
-    if (len[s] < CS_N) return;
-    const T *p = x + 2 * (off[s] + (int64_t)b * hop);
-    float a = 0.f, c = 0.f;
-    for (int i = threadIdx.x; i < hop; i += 256) {
-        const float2 z = io::f(io::load(p + 2 * i));
-        a += z.x;
-        c += z.y;
-    }
-    __shared__ double red[2][256];
-    red[0][threadIdx.x] = a;
-    red[1][threadIdx.x] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double u = 0.0, w = 0.0;
-        for (int i = 0; i < 256; ++i) u += red[0][i], w += red[1][i];
-        head[s].sum[b][0] = (typename io::acc_t)u;
-        head[s].sum[b][1] = (typename io::acc_t)w;
-    }
-}
-
-// PD's second half: one thread per frame t of a stream, the frame sums from its four blocks (blocks
-// 3.. from the records of frames t - 3 .. t, blocks 0..2 from the stream's head), the mean as
-// IQ<T>::mean forms it from wave sums, and bins 0, 1, N - 1 rewritten; frames past a stream's end
-// stay zero
-// (XS: the frame sums given, fsum[g] -- msd_cstft_psd_fsums_dev -- no records or head needed).
-// Workgroups bps per stream, so the stream index is a wave-uniform 32-bit division and the frame
-// test a multiply (≈ 100 instructions against ≈ 400 with per-thread int64 divisions; the time did not
-// move, 0.152-0.155 ms for C5's 2.0 M frames: it is the two partial-line writes per 16 KB row).
-template <typename T, bool XS>
-__global__ __launch_bounds__(256) void dc_fix_kernel(const CsSide<T> *__restrict__ side,
-                                                     const CsHead<T> *__restrict__ head,
-                                                     const double2 *__restrict__ fsum,
-                                                     const int64_t *__restrict__ len, int64_t max_frames,
-                                                     unsigned bps, int hop, float2 wk0, float2 wk1, float2 wkm1,
-                                                     float *__restrict__ out) {
-    using acc = typename IQ<T>::acc_t;
-    const unsigned s = blockIdx.x / bps;
-    const int64_t t = (int64_t)(blockIdx.x - s * bps) * 256 + threadIdx.x;
-    if (t >= max_frames || t * hop + CS_N > len[s]) return;
-    const int64_t g = (int64_t)s * max_frames + t;
-    float2 m;
-    if constexpr (XS) {
-        const double2 f = fsum[g];
-        m = make_float2(IQ<T>::mean_d(f.x), IQ<T>::mean_d(f.y));
-    } else {
-        // four "wave" slots as IQ<T>::mean takes them: slot k = block t + k's sum
-        acc sum[2][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t b = t + k;  // the stream's block
-#pragma unroll
-            for (int c = 0; c < 2; ++c) sum[c][k] = b >= 3 ? side[g + k - 3].sum[c] : head[s].sum[b][c];
-        }
-        m = make_float2(IQ<T>::mean(sum[0]), IQ<T>::mean(sum[1]));
-    }
-    const CsSide<T> &sd = side[g];
-    const float2 w[3] = {wk0, wk1, wkm1};
-    const int64_t bin[3] = {0, 1, CS_N - 1};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float2 X = c_sub(sd.raw[k], c_mul(m, w[k]));
-        out[g * CS_N + bin[k]] = X.x * X.x + X.y * X.y;
-    }
-}
-
 }  // namespace
 }  // namespace msd
 
 struct msd_cstft_plan {
     msd_ctx *ctx = nullptr;
     int nperseg = 0, hop = 0, detrend = 1;
-    bool post_dt = false;     // the window's DFT is (numerically) zero but at bins 0, +-1: PD kernels
-    float2 wk[3] = {};        // DFT of the scaled window at bins 0, 1, N - 1
     float *d_win = nullptr;   // window x sqrt(scale)
     float2 *d_tw = nullptr;   // W4096^m, m = 0..4095
 };
@@ -492,27 +398,6 @@ int msd_cstft_plan_create(msd_ctx *ctx, int32_t nperseg, int32_t hop, const floa
     std::vector<float> w(nperseg);
     const double rs = std::sqrt(scale);
     for (int i = 0; i < nperseg; ++i) w[i] = (float)((double)window[i] * rs);
-    {  // the float window's DFT at bins 0, +-1 (double); PD when the window is those three bins'
-       // inverse DFT up to a residual r with sum |r| <= 1e-6 sum |w| (which bounds every other bin)
-        double W[3][2] = {};
-        for (int i = 0; i < nperseg; ++i) {
-            const double a = 2.0 * M_PI * (double)i / (double)nperseg;
-            W[0][0] += w[i];
-            W[1][0] += w[i] * std::cos(a), W[1][1] -= w[i] * std::sin(a);  // k = 1: e^{-i a}
-            W[2][0] += w[i] * std::cos(a), W[2][1] += w[i] * std::sin(a);  // k = N - 1: e^{+i a}
-        }
-        double l1 = 0.0, res = 0.0;
-        for (int i = 0; i < nperseg; ++i) {
-            const double a = 2.0 * M_PI * (double)i / (double)nperseg, c = std::cos(a), sn = std::sin(a);
-            // (W0 + W1 e^{i a} + W_{N-1} e^{-i a}) / N
-            const double mr = (W[0][0] + W[1][0] * c - W[1][1] * sn + W[2][0] * c + W[2][1] * sn) / nperseg;
-            const double mi = (W[0][1] + W[1][0] * sn + W[1][1] * c - W[2][0] * sn + W[2][1] * c) / nperseg;
-            l1 += std::fabs((double)w[i]);
-            res += std::hypot((double)w[i] - mr, mi);
-        }
-        for (int k = 0; k < 3; ++k) p->wk[k] = make_float2((float)W[k][0], (float)W[k][1]);
-        p->post_dt = res <= 1e-6 * l1;
-    }
     std::vector<float2> tw(CS_N);
     for (int m = 0; m < CS_N; ++m) {
         const double a = -2.0 * M_PI * (double)m / (double)CS_N;
@@ -570,14 +455,7 @@ int msd_cstft_psd_fsums_dev(msd_cstft_plan *p, const void *x, int dtype, const i
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
     DeviceGuard g(p->ctx->device);
     const int64_t total = nstreams * max_frames;
-    const bool pd = p->post_dt && p->detrend && p->hop == 4 * 256;  // the PD kernels: C5's hop
-    void *side = nullptr;  // PD: CsSide per frame (64 B), then CsHead per stream
-    if (pd) {
-        if (int rc = ctx_scratch(p->ctx, 5, 64 * (size_t)total + 64 * (size_t)nstreams, &side)) return rc;
-    }
-    auto launch = [&](auto kern, const auto *xp, int pd_kern) {
-        using T = std::remove_cv_t<std::remove_pointer_t<decltype(xp)>>;
-        static_assert(sizeof(CsSide<T>) == 64, "CsSide: 64-B records (side_rsrc)");
+    auto launch = [&](auto kern, const auto *xp) {
         // persistent: as many workgroups as stay resident (registers and the 37 KB of LDS decide;
         // the compiler's register count sets 3 or 4 per CU)
         int per_cu = 0;
@@ -589,42 +467,25 @@ int msd_cstft_psd_fsums_dev(msd_cstft_plan *p, const void *x, int dtype, const i
         int64_t per = (total + wgs - 1) / wgs;
         if (etot) per = (per + 3) / 4 * 4;  // energy groups of 4 frames start at every workgroup's first
         wgs = (total + per - 1) / per;
-        {
-            KernelTimer timer(p->ctx, K_CSTFT);  // the FFT kernel alone: the roofline's
-            hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
-                               max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out, etot,
-                               msd_cstft_energy_stride(nstreams, max_frames), static_cast<CsSide<T> *>(side));
-        }
-        static_assert(sizeof(CsHead<T>) <= 64, "CsHead");
-        if (!pd_kern) return;
-        KernelTimer dc_timer(p->ctx, K_CSTFT_DC);  // the fix-up kernels apart from the FFT's roofline
-        auto *head = reinterpret_cast<CsHead<T> *>(static_cast<char *>(side) + 64 * (size_t)total);
-        const unsigned bps = (unsigned)((max_frames + 255) / 256);
-        const dim3 fg(bps * (unsigned)nstreams);
-        if (pd_kern == 1) {
-            hipLaunchKernelGGL(cs_head_kernel<T>, dim3((unsigned)(3 * nstreams)), dim3(256), 0, p->ctx->stream, xp, off,
-                               len, p->hop, head);
-            hipLaunchKernelGGL((dc_fix_kernel<T, false>), fg, dim3(256), 0, p->ctx->stream,
-                               static_cast<const CsSide<T> *>(side), head, fsum, len, max_frames, bps, p->hop,
-                               p->wk[0], p->wk[1], p->wk[2], out);
-        } else if (pd_kern == 2) {
-            hipLaunchKernelGGL((dc_fix_kernel<T, true>), fg, dim3(256), 0, p->ctx->stream,
-                               static_cast<const CsSide<T> *>(side), head, fsum, len, max_frames, bps, p->hop,
-                               p->wk[0], p->wk[1], p->wk[2], out);
-        }
+        KernelTimer timer(p->ctx, K_CSTFT);  // the FFT kernel alone: the roofline's
+        hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
+                           max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out, etot,
+                           msd_cstft_energy_stride(nstreams, max_frames), fsum);
     };
     const int sh = p->hop % 256 == 0 ? p->hop / 256 : 0;
+    // the given sums (PD 2) at C5's hop: the int16 exact delta step leaves them (frames that start
+    // every 1024 samples); other hops compute their own
+    const bool given = fsum && p->detrend && sh == 4;
     auto by_shift = [&](auto en, const auto *xp) {
         constexpr bool EN = decltype(en)::value;
         using T = std::remove_cv_t<std::remove_pointer_t<decltype(xp)>>;
         if (sh == 4) {  // 75 % overlap (C5)
-            if (pd && fsum) launch(cstft4096_kernel<T, 4, EN, 2>, xp, 2);
-            else if (pd) launch(cstft4096_kernel<T, 4, EN, 1>, xp, 1);
-            else launch(cstft4096_kernel<T, 4, EN, 0>, xp, 0);
+            if (given) launch(cstft4096_kernel<T, 4, EN, 2>, xp);
+            else launch(cstft4096_kernel<T, 4, EN, 0>, xp);
         } else if (sh == 8) {  // 50 %
-            launch(cstft4096_kernel<T, 8, EN, 0>, xp, 0);
+            launch(cstft4096_kernel<T, 8, EN, 0>, xp);
         } else {
-            launch(cstft4096_kernel<T, 0, EN, 0>, xp, 0);
+            launch(cstft4096_kernel<T, 0, EN, 0>, xp);
         }
     };
     auto by_energy = [&](const auto *xp) {

@@ -50,8 +50,8 @@ struct msd_ctx {
     double total_ms[msd::K_COUNT] = {};
     int64_t launches[msd::K_COUNT] = {};
     // scratch device buffers for the host-pointer convenience entry points
-    // (slot 4: msd_iq_delta64_dev's block table, rotations and ranges; slot 5: cstft4096_kernel's
-    // per-frame sums and raw DC-bin values for its post-FFT detrend)
+    // (slot 4: msd_iq_delta64_dev's block table, rotations and ranges; slot 5 unused since the
+    // post-FFT detrend's side records went, round 5)
     void *scratch[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t scratch_bytes[6] = {0, 0, 0, 0, 0, 0};
     // msd_iq_delta64_dev's twiddle table W^m (m < rf_w_n), built once per frame length
@@ -71,6 +71,8 @@ struct msd_ctx {
     int i8_km[16] = {};
     bool refine_goertzel = false;  // MSD_OPT_REFINE_GOERTZEL: int16 refinement on the float64 Goertzel
     int cstft_reserve = 0;         // MSD_OPT_CSTFT_RESERVE: workgroup slots the C5 spectrogram leaves free
+    int num_cu_dev = 0;            // the device's CUs (num_cu: those the stream may use, MSD_OPT_STREAM_CUS)
+    int stream_cus = 0;            // MSD_OPT_STREAM_CUS value in force
 };
 
 namespace msd {

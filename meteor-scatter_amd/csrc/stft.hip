@@ -220,14 +220,18 @@ __global__ __launch_bounds__(NW * 64) void stft_psd_kernel(const T *__restrict__
             float ls = 0.f;
 #pragma unroll
             for (int q = 0; q < SPL; ++q) ls += s[q];
-            // integer samples: per-lane sums are exact in fp32, the wave sum in fp64
-            float mean = static_cast<float>(wave_sum(static_cast<double>(ls)) / static_cast<double>(N));
-            if (!detrend) mean = 0.f;  // matplotlib's detrend_none
+            // integer samples: per-lane sums are exact in fp32, the wave sum in fp64; the mean is
+            // subtracted as hi + lo (hi its float32 rounding, lo the rest), so that the detrended
+            // sample is the float32 rounding of x - mean also where float(mean) is not exact
+            // (|mean| >= 2^24 / N for integer input: a residual DC at bins 0, 1 otherwise)
+            const double md = detrend ? wave_sum(static_cast<double>(ls)) / static_cast<double>(N) : 0.0;  // detrend_none: 0
+            const float mean = static_cast<float>(md), mlo = static_cast<float>(md - static_cast<double>(mean));
             const float *w = win + lane * SPL;
 #pragma unroll
             for (int q = 0; q < SPL / 2; ++q) {
                 const int m = lane * (SPL / 2) + q;
-                scr[phys(m)] = make_float2((s[2 * q] - mean) * w[2 * q], (s[2 * q + 1] - mean) * w[2 * q + 1]);
+                scr[phys(m)] = make_float2(((s[2 * q] - mean) - mlo) * w[2 * q],
+                                           ((s[2 * q + 1] - mean) - mlo) * w[2 * q + 1]);
             }
             wave_sync();
             fft_passes<M, 0, 1>(scr, tw, lane);

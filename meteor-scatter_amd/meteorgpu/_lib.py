@@ -40,6 +40,7 @@ OPT_GENERIC_STFT = 1
 OPT_FRESH_ALL = 2
 OPT_REFINE_GOERTZEL = 3
 OPT_CSTFT_RESERVE = 4
+OPT_STREAM_CUS = 5
 COMM_ID_BYTES = 128
 
 

@@ -123,66 +123,11 @@ def frame_shard(n_samples: int, nperseg: int, hop: int, rank: int, world: int):
     return T, f0, f1, f0 * hop, ((f1 - 1) * hop + nperseg) if f1 > f0 else f0 * hop
 
 
-def _as_iv(iv) -> np.ndarray:
-    if isinstance(iv, np.ndarray):
-        return iv.astype(np.int64, copy=False).reshape(-1, 2)
-    return np.asarray(list(iv), dtype=np.int64).reshape(-1, 2)
+# the refinement's interval bookkeeping lives with the certify-then-refine loop (stream.py)
+from .stream import _NO_IV, _as_iv, _iv_len, _merge, _merge_a, _subtract, _subtract_a  # noqa: E402,F401
 
 
-_NO_IV = np.zeros((0, 2), np.int64)
-
-
-def _merge_a(iv) -> np.ndarray:
-    """sorted, merged [a, b) intervals (touching ones joined), as an (n, 2) int64 array"""
-    a = _as_iv(iv)
-    a = a[a[:, 1] > a[:, 0]]
-    if a.size == 0:
-        return _NO_IV
-    a = a[np.argsort(a[:, 0], kind="stable")]
-    ends = np.maximum.accumulate(a[:, 1])
-    new = np.ones(len(a), bool)
-    new[1:] = a[1:, 0] > ends[:-1]  # a start past every earlier end opens a new interval
-    heads = np.flatnonzero(new)
-    tails = np.r_[heads[1:] - 1, len(a) - 1]
-    return np.stack([a[heads, 0], ends[tails]], 1)
-
-
-def _subtract_a(iv, done) -> np.ndarray:
-    """the (merged) intervals iv minus the (merged) intervals done: the elementary segments between
-    all their boundaries that iv covers and done does not, merged"""
-    a, d = _as_iv(iv), _as_iv(done)
-    if a.size == 0:
-        return _NO_IV
-    if d.size == 0:
-        return a
-    if len(d) == 1 and d[0, 0] <= a[0, 0] and a[-1, 1] <= d[0, 1]:  # all refined already (the exact delta)
-        return _NO_IV
-    pts = np.unique(np.concatenate([a.reshape(-1), d.reshape(-1)]))
-    lo, hi = pts[:-1], pts[1:]
-
-    def covered(x, seg):  # x inside one of the sorted disjoint [start, end)
-        return np.searchsorted(seg[:, 0], x, "right") > np.searchsorted(seg[:, 1], x, "right")
-
-    keep = covered(lo, a) & ~covered(lo, d)
-    return _merge_a(np.stack([lo[keep], hi[keep]], 1))
-
-
-def _merge(iv) -> list:
-    """_merge_a as a list of [a, b]"""
-    return _merge_a(iv).tolist()
-
-
-def _subtract(iv, done) -> list:
-    """_subtract_a as a list of [a, b]"""
-    return _subtract_a(iv, done).tolist()
-
-
-def _iv_len(iv) -> int:
-    a = _as_iv(iv)
-    return int((a[:, 1] - a[:, 0]).sum())
-
-
-class IQShardDetector:
+class IQShardDetector(_stream.CertifyingShard):
     """One rank's time shard of an I/Q stream on the GPU: spectrogram (frame-major, kept in HBM) →
     per-frame band delta written straight into the stream plan → detector over the whole stream.
 
@@ -220,11 +165,13 @@ class IQShardDetector:
         (REFINE_INT8_MFMA: blocks of 1024 samples, <= 10 bins, no band at 0 Hz -- C5), else fp32.
         With the exact delta every frame's error bound is ~1e-13 dB, so certification settles every
         decision in one pass (no energy partials, no refinement, no second detector pass).
-        overlap: run the stream detector on a second context (own HIP stream) and let the
-        spectrogram leave that many workgroup slots free (MSD_OPT_CSTFT_RESERVE): with the exact
-        delta the detector does not need the spectrogram, so its latency-bound kernels and host
-        round trips run beside it (the exact delta first, then the spectrogram and the detector
-        concurrently).  0: one stream, in order."""
+        overlap: n > 0 splits the chip for the detector: the spectrogram runs on a context whose
+        stream may use all but n CUs and the stream detector on one restricted to those n
+        (MSD_OPT_STREAM_CUS, hipExtStreamCreateWithCUMask).  With the exact delta the detector does
+        not need the spectrogram, so after the delta (full chip, the caller's context) the two run
+        side by side -- the detector's latency-bound kernels and host round trips on their own CUs,
+        the spectrogram's persistent grid sized for the rest.  The caller's context is not changed.
+        0: one stream, in order."""
         self.ctx, self.fs, self.N = ctx, fs, int(nperseg)
         self.hop = self.N - int(noverlap)
         self.block_sec = self.hop / fs
@@ -241,7 +188,26 @@ class IQShardDetector:
         nloc = self.f1 - self.f0
         self.chunk = int(chunk_frames) if chunk_frames and 0 < int(chunk_frames) < nloc else None
         nb = (self.chunk - 1) * self.hop + self.N if self.chunk else max(self.s1 - self.s0, 1)
-        self.batch = IQBatch(ctx, 1, nb, fs, self.N, noverlap, dtype)
+        self.overlap = int(overlap)
+        if self.overlap < 0:
+            raise ValueError("overlap must be >= 0 (CUs for the detector)")
+        self.sctx = self.dctx = ctx  # the spectrogram's and the detector's contexts
+        self.plan = None
+        self.batch = None
+        try:
+            if self.overlap > 0:
+                self.sctx, self.dctx = ctx.sibling(), ctx.sibling()
+                self.sctx.set_option(_lib.OPT_STREAM_CUS, -self.overlap)
+                self.dctx.set_option(_lib.OPT_STREAM_CUS, self.overlap)
+            self._init(ctx, fs, noverlap, freq_band, noise_band, threshold_std_factor, nb, dtype, delta,
+                       seg_len, certify, Fa, Fb)
+        except BaseException:
+            self.close()
+            raise
+
+    def _init(self, ctx, fs, noverlap, freq_band, noise_band, threshold_std_factor, nb, dtype, delta, seg_len,
+              certify, Fa, Fb):
+        self.batch = IQBatch(self.sctx, 1, nb, fs, self.N, noverlap, dtype)
         if delta not in ("auto", "fp32", "exact"):
             raise ValueError(f"delta must be 'auto', 'fp32' or 'exact', not {delta!r}")
         try:
@@ -255,29 +221,13 @@ class IQShardDetector:
         self.d_frames = ctx.alloc(8)
         self.d_frames.upload(np.array([self.batch.T if self.s1 > self.s0 else 0], np.int64))
         cfg = _lib.det_cfg(self.adaptive, self.k, self.W, Fb, Fa, self.F0)
-        self.overlap = int(overlap)
-        self.dctx = ctx  # the detector's context
-        self.plan = None
-        # the caller's spectrogram reserve (MSD_OPT_CSTFT_RESERVE is context-wide and ctx may be the
-        # process-wide one): restored by close(), or here if the constructor fails after changing it
-        self._reserve_prev = ctx.options.get(_lib.OPT_CSTFT_RESERVE, 0)
-        try:
-            if self.overlap > 0:
-                self.dctx = ctx.sibling()
-                ctx.set_option(_lib.OPT_CSTFT_RESERVE, self.overlap)
-            self.plan = _lib.StreamPlan(self.dctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
-            self.ops = _stream.DeviceStreamOps(self.plan)
-            self.d_etot = None
-            self.d_fsum = None  # exact delta: the frames' sample sums, shared with the spectrogram's detrend
-            self._fsums_ok = True
-            self.certify = False
-            self.set_certify(certify)
-        except BaseException:
-            self._release_overlap()
-            if self.plan is not None:
-                self.plan.close()
-            self.batch.close()
-            raise
+        self.plan = _lib.StreamPlan(self.dctx, cfg, self.T, self.f0, self.f1 - self.f0, seg_len=seg_len)
+        self.ops = _stream.DeviceStreamOps(self.plan)
+        self.d_etot = None
+        self.d_fsum = None  # exact delta: the frames' sample sums, shared with the spectrogram's detrend
+        self._fsums_ok = True
+        self.certify = False
+        self.set_certify(certify)
         self.fs_ = float(fs)
         self._read = None      # the shard's sample source when chunked (refinement re-reads samples)
         self._refined = _NO_IV  # global frame ranges whose delta is float64 already (merged, (n, 2))
@@ -310,26 +260,36 @@ class IQShardDetector:
     def spectrogram_and_delta(self):
         """async: spectrogram of the shard and its per-frame band delta (into the stream plan)"""
         self._refined = _NO_IV
+        self._step_start()
         if self.f1 > self.f0:
             if self.exact_delta:
-                # the exact delta first: the detector (on dctx) then runs beside the spectrogram
+                # the exact delta first (full chip): the detector (dctx) then runs beside the spectrogram
                 self._delta_exact(self.batch.n, self.f1 - self.f0, 0)
-                self._detector_ready()
+                self._after(self.dctx, self.ctx)
+                self._after(self.sctx, self.ctx)
                 self.batch.run(fsums=self._fsums())
             else:
                 etot = self.d_etot if self.certify else None
+                self._after(self.sctx, self.ctx)
                 self.batch.run(etot)
-                _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
+                _lib.iq_band_delta_dev(self.sctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                        self.noise, self.plan.d_delta, self.batch.T, etot=etot,
                                        ed=self.plan.d_ed if self.certify else None)
-                self._detector_ready()
+                self._after(self.dctx, self.sctx)
         if self.exact_delta:
             self._refined = np.array([[0, self.T]], np.int64)  # every rank's frames are float64 (the ranks agree on this list)
 
-    def _detector_ready(self):
-        """the detector's context waits for the delta enqueued on the spectrogram's"""
-        if self.dctx is not self.ctx:
-            self.dctx.wait_for(self.ctx)
+    @staticmethod
+    def _after(a: _lib.Context, b: _lib.Context):
+        """work enqueued on a from now on waits for b's so far (nothing when they share a stream)"""
+        if a is not b:
+            a.wait_for(b)
+
+    def _step_start(self):
+        """a new step on the caller's context (uploads, the delta) waits for the previous step's
+        spectrogram (it reads the samples and the frame sums) and detector (it reads the delta)"""
+        self._after(self.ctx, self.sctx)
+        self._after(self.ctx, self.dctx)
 
     def _fsums(self):
         return self.d_fsum if self._fsums_ok else None
@@ -373,103 +333,26 @@ class IQShardDetector:
             nf = min(self.chunk, nloc - c0)
             a = c0 * self.hop
             b = a + (nf - 1) * self.hop + self.N
+            self.sctx.synchronize()  # the previous chunk's spectrogram has read the batch buffer
             self.batch.upload(0, np.ascontiguousarray(read(a, b)))
             if self.exact_delta:
+                self._after(self.ctx, self.sctx)
                 self._delta_exact(b - a, nf, c0)
                 # frames past nf read stale samples (and sums); the spectrogram is the product
+                self._after(self.sctx, self.ctx)
                 self.batch.run(fsums=self._fsums())
                 continue
             self.d_frames.upload(np.array([nf], np.int64))
             etot = self.d_etot if self.certify else None
             self.batch.run(etot)  # frames past nf read stale samples; their powers are not used
             ed = _lib.C.c_void_p(self.plan.d_ed.value + 8 * c0) if self.certify else None
-            _lib.iq_band_delta_dev(self.ctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
+            _lib.iq_band_delta_dev(self.sctx, self.batch.d_out, 1, self.batch.T, self.d_frames, self.N, self.band,
                                    self.noise, _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0), self.batch.T,
                                    etot=etot, ed=ed)
-        self._detector_ready()
+        self._after(self.dctx, self.ctx)
+        self._after(self.dctx, self.sctx)
         if self.exact_delta:
             self._refined = np.array([[0, self.T]], np.int64)
-
-    MAX_REFINE = 8  # refinement rounds before giving up (refine_budget_exhausted)
-
-    def detect(self, comm=None, thresholds: bool = True, exact_decisions: bool = True) -> _stream.StreamResult:
-        """The detector over the whole stream (every rank gets the same result).  Certifying, each
-        decision is checked against its error bounds; exact_decisions refines the uncertain ones,
-        then the detections' own frames (class docstring)."""
-        comm = comm or _stream.LocalComm()
-        refined, first, passes, exhausted, db_frames = 0, None, 0, False, 0
-        while True:
-            res = self._detector(comm).run(thresholds)
-            passes += 1
-            if first is None:
-                first = res.uncertain
-            if not self.certify or not exact_decisions:
-                break
-            if res.certified:
-                # the detections' own frames in float64 (the CSV's dB column); with the thresholds
-                # output one more pass, so that the thresholds, the delta and the dB means agree
-                n = self._refine_detections(res)
-                db_frames += n
-                if n and thresholds and passes <= self.MAX_REFINE:
-                    continue
-                if n:
-                    res.detections["db"] = self._detector(comm).db_means(res.detections, refresh_halos=True)
-                break
-            if passes > self.MAX_REFINE:  # refined MAX_REFINE times, still uncertain: reported, not a tie
-                exhausted = True
-                break
-            need = self._dependencies(res.uncertain_frames)
-            if not len(need):  # every uncertain decision already reads float64 values: a float64 near tie
-                break
-            self._refined = _merge_a(np.concatenate([self._refined, need]))
-            refined += _iv_len(need)
-        if self.certify:
-            if exact_decisions and not res.certified:  # a near tie / exhausted budget: the dB still float64
-                n = self._refine_detections(res)
-                if n:
-                    db_frames += n
-                    res.detections["db"] = self._detector(comm).db_means(res.detections, refresh_halos=True)
-            res.refined_delta_frames = refined + db_frames
-            res.db_refined_frames = db_frames
-            res.near_tie = not res.certified and not exhausted
-            res.refine_budget_exhausted = exhausted
-            res.uncertain_initial = first
-            res.detector_passes = passes
-        return res
-
-    def _detector(self, comm) -> _stream.StreamDetector:
-        return _stream.StreamDetector(self.ops, comm, self.adaptive, self.k, self.W, self.F0)
-
-    def _refine_detections(self, res) -> int:
-        """float64 delta for every frame of every detection not refined yet (main.py:501-502 takes
-        np.mean(delta_power[start:stop]) over them); returns the frames refined.  Every rank holds
-        the same detections and refined ranges and refines its own part."""
-        dets = res.detections
-        if dets is None or len(dets) == 0:
-            return 0
-        r = self._refined
-        if len(r) == 1 and r[0, 0] <= dets["start"].min() and dets["stop"].max() <= r[0, 1]:
-            return 0  # every frame float64 already (the exact delta): no interval work per step
-        need = _subtract_a(_merge_a(np.stack([dets["start"], dets["stop"]], 1)), r)
-        if not len(need):
-            return 0
-        self._refine_local(need)
-        self._refined = _merge_a(np.concatenate([self._refined, need]))
-        return _iv_len(need)
-
-    def _dependencies(self, uncertain) -> np.ndarray:
-        """global frame ranges the uncertain decisions (frame, threshold source) depend on, and
-        refines this rank's part of them"""
-        iv = []
-        for f, src in np.asarray(uncertain, np.int64).reshape(-1, 2):
-            if src < 0:  # thr0: the whole stream's mean and std
-                iv.append((0, self.T))
-            else:
-                iv.append((max(0, int(src) - self.W), int(src)))  # the window delta[src - W : src]
-            iv.append((int(f), int(f) + 1))
-        need = _subtract_a(_merge_a(iv), self._refined)
-        self._refine_local(need)
-        return need
 
     def _refine_local(self, ranges):
         """float64 delta (and its bound) of this rank's frames in the global ranges, from the samples"""
@@ -495,28 +378,31 @@ class IQShardDetector:
                                     _lib.C.c_void_p(self.plan.d_ed.value + 8 * c))
 
     def synchronize(self):
-        """both contexts' work (spectrogram and detector) finished"""
+        """every context's work (delta, spectrogram and detector) finished"""
         self.ctx.synchronize()
-        if self.dctx is not self.ctx:
-            self.dctx.synchronize()
+        for c in (self.sctx, self.dctx):
+            if c is not self.ctx:
+                c.synchronize()
 
     def close(self):
+        """frees the plans and buffers and the CU-split sibling contexts (the caller's context is
+        left as it was); safe on a partly constructed detector"""
         self.synchronize()
-        self.plan.close()
-        self.batch.close()
-        if self.d_etot is not None:
-            self.d_etot.free()
-        if self.d_fsum is not None:
-            self.d_fsum.free()
-        self._release_overlap()
-
-    def _release_overlap(self):
-        """the sibling context closed, the caller's reserve value back"""
-        if self.dctx is not self.ctx:
-            self.dctx.close()
-            self.dctx = self.ctx
-        if self.ctx.options.get(_lib.OPT_CSTFT_RESERVE, 0) != self._reserve_prev:
-            self.ctx.set_option(_lib.OPT_CSTFT_RESERVE, self._reserve_prev)
+        if self.plan is not None:
+            self.plan.close()
+            self.plan = None
+        if self.batch is not None:
+            self.batch.close()
+            self.batch = None
+        for name in ("d_etot", "d_fsum"):
+            buf = getattr(self, name, None)
+            if buf is not None:
+                buf.free()
+                setattr(self, name, None)
+        for c in (self.sctx, self.dctx):
+            if c is not self.ctx:
+                c.close()
+        self.sctx = self.dctx = self.ctx
 
 
 def proc_iq_samples(i, q, fs, freq_band, noise_band, nperseg=4096, noverlap=3072, threshold_std_factor=4.0,

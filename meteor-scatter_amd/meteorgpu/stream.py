@@ -335,6 +335,163 @@ class StreamDetector:
         return self._certified(StreamResult(dets, thr0, thr, margin, rounds, refined))
 
 
+# ------------------------------------------------------------ certified decisions (any plan / rank)
+def _as_iv(iv) -> np.ndarray:
+    if isinstance(iv, np.ndarray):
+        return iv.astype(np.int64, copy=False).reshape(-1, 2)
+    return np.asarray(list(iv), dtype=np.int64).reshape(-1, 2)
+
+
+_NO_IV = np.zeros((0, 2), np.int64)
+
+
+def _merge_a(iv) -> np.ndarray:
+    """sorted, merged [a, b) intervals (touching ones joined), as an (n, 2) int64 array"""
+    a = _as_iv(iv)
+    a = a[a[:, 1] > a[:, 0]]
+    if a.size == 0:
+        return _NO_IV
+    a = a[np.argsort(a[:, 0], kind="stable")]
+    ends = np.maximum.accumulate(a[:, 1])
+    new = np.ones(len(a), bool)
+    new[1:] = a[1:, 0] > ends[:-1]  # a start past every earlier end opens a new interval
+    heads = np.flatnonzero(new)
+    tails = np.r_[heads[1:] - 1, len(a) - 1]
+    return np.stack([a[heads, 0], ends[tails]], 1)
+
+
+def _subtract_a(iv, done) -> np.ndarray:
+    """the (merged) intervals iv minus the (merged) intervals done: the elementary segments between
+    all their boundaries that iv covers and done does not, merged"""
+    a, d = _as_iv(iv), _as_iv(done)
+    if a.size == 0:
+        return _NO_IV
+    if d.size == 0:
+        return a
+    if len(d) == 1 and d[0, 0] <= a[0, 0] and a[-1, 1] <= d[0, 1]:  # all refined already (the exact delta)
+        return _NO_IV
+    pts = np.unique(np.concatenate([a.reshape(-1), d.reshape(-1)]))
+    lo, hi = pts[:-1], pts[1:]
+
+    def covered(x, seg):  # x inside one of the sorted disjoint [start, end)
+        return np.searchsorted(seg[:, 0], x, "right") > np.searchsorted(seg[:, 1], x, "right")
+
+    keep = covered(lo, a) & ~covered(lo, d)
+    return _merge_a(np.stack([lo[keep], hi[keep]], 1))
+
+
+def _merge(iv) -> list:
+    """_merge_a as a list of [a, b]"""
+    return _merge_a(iv).tolist()
+
+
+def _subtract(iv, done) -> list:
+    """_subtract_a as a list of [a, b]"""
+    return _subtract_a(iv, done).tolist()
+
+
+def _iv_len(iv) -> int:
+    a = _as_iv(iv)
+    return int((a[:, 1] - a[:, 0]).sum())
+
+
+class CertifyingShard:
+    """The certify-then-refine loop of one rank's shard (meteorgpu.iq.IQShardDetector; the CPU tests'
+    numpy shard in tests/stream_np_ops.py): every pass runs the protocol above with certification on
+    the plan, the uncertain decisions' dependencies (the frame and the window its threshold reads,
+    main.py:475-480; the whole stream for thr0, main.py:464-466) are recomputed in float64 by
+    ``_refine_local`` -- each rank its own part of the global ranges -- and the detector reruns until
+    every decision is certified; then the detections' frames are made float64 for the dB means.
+    Subclasses provide ``_refine_local(ranges)`` and the attributes ``ops`` (the rank's plan or a
+    stand-in), ``adaptive``, ``k``, ``W`` (window), ``F0``, ``certify``, ``T`` (frames of the whole
+    stream) and ``_refined`` (global frame ranges already float64, merged (n, 2)); ``_detector``
+    builds the StreamDetector over ``ops``."""
+
+    MAX_REFINE = 8  # refinement rounds before giving up (refine_budget_exhausted)
+
+    def detect(self, comm=None, thresholds: bool = True, exact_decisions: bool = True) -> StreamResult:
+        """The detector over the whole stream (every rank gets the same result).  Certifying, each
+        decision is checked against its error bounds; exact_decisions refines the uncertain ones,
+        then the detections' own frames (class docstring)."""
+        comm = comm or LocalComm()
+        refined, first, passes, exhausted, db_frames = 0, None, 0, False, 0
+        while True:
+            res = self._detector(comm).run(thresholds)
+            passes += 1
+            if first is None:
+                first = res.uncertain
+            if not self.certify or not exact_decisions:
+                break
+            if res.certified:
+                # the detections' own frames in float64 (the CSV's dB column); with the thresholds
+                # output one more pass, so that the thresholds, the delta and the dB means agree
+                n = self._refine_detections(res)
+                db_frames += n
+                if n and thresholds and passes <= self.MAX_REFINE:
+                    continue
+                if n:
+                    res.detections["db"] = self._detector(comm).db_means(res.detections, refresh_halos=True)
+                break
+            if passes > self.MAX_REFINE:  # refined MAX_REFINE times, still uncertain: reported, not a tie
+                exhausted = True
+                break
+            need = self._dependencies(res.uncertain_frames)
+            if not len(need):  # every uncertain decision already reads float64 values: a float64 near tie
+                break
+            self._refined = _merge_a(np.concatenate([self._refined, need]))
+            refined += _iv_len(need)
+        if self.certify:
+            if exact_decisions and not res.certified:  # a near tie / exhausted budget: the dB still float64
+                n = self._refine_detections(res)
+                if n:
+                    db_frames += n
+                    res.detections["db"] = self._detector(comm).db_means(res.detections, refresh_halos=True)
+            res.refined_delta_frames = refined + db_frames
+            res.db_refined_frames = db_frames
+            res.near_tie = not res.certified and not exhausted
+            res.refine_budget_exhausted = exhausted
+            res.uncertain_initial = first
+            res.detector_passes = passes
+        return res
+
+    def _detector(self, comm) -> StreamDetector:
+        return StreamDetector(self.ops, comm, self.adaptive, self.k, self.W, self.F0)
+
+    def _refine_detections(self, res) -> int:
+        """float64 delta for every frame of every detection not refined yet (main.py:501-502 takes
+        np.mean(delta_power[start:stop]) over them); returns the frames refined.  Every rank holds
+        the same detections and refined ranges and refines its own part."""
+        dets = res.detections
+        if dets is None or len(dets) == 0:
+            return 0
+        r = self._refined
+        if len(r) == 1 and r[0, 0] <= dets["start"].min() and dets["stop"].max() <= r[0, 1]:
+            return 0  # every frame float64 already (the exact delta): no interval work per step
+        need = _subtract_a(_merge_a(np.stack([dets["start"], dets["stop"]], 1)), r)
+        if not len(need):
+            return 0
+        self._refine_local(need)
+        self._refined = _merge_a(np.concatenate([self._refined, need]))
+        return _iv_len(need)
+
+    def _dependencies(self, uncertain) -> np.ndarray:
+        """global frame ranges the uncertain decisions (frame, threshold source) depend on, and
+        refines this rank's part of them"""
+        iv = []
+        for f, src in np.asarray(uncertain, np.int64).reshape(-1, 2):
+            if src < 0:  # thr0: the whole stream's mean and std
+                iv.append((0, self.T))
+            else:
+                iv.append((max(0, int(src) - self.W), int(src)))  # the window delta[src - W : src]
+            iv.append((int(f), int(f) + 1))
+        need = _subtract_a(_merge_a(iv), self._refined)
+        self._refine_local(need)
+        return need
+
+    def _refine_local(self, ranges):
+        raise NotImplementedError
+
+
 class DeviceStreamOps:
     """``_lib.StreamPlan`` with the protocol's method signatures."""
 

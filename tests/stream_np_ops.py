@@ -176,3 +176,145 @@ def shard_bounds(n_total, world, rank, cuts=None):
     base, extra = divmod(n_total, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+class NumpyCertOps(NumpyStreamOps):
+    """``NumpyStreamOps`` with the certification interface of a certifying ``_lib.StreamPlan``
+    (msd_stream_set_certify): the rank's delta is an APPROXIMATION within ``ed`` per frame of the
+    float64 one (the fp32 spectrogram's, on the device), and every decision is checked against its
+    bounds -- |delta - thr| > ed[i] + terr(source) certifies it (NaN never does).  terr: a fresh
+    threshold's window moves it by at most mean(ed) + |k| rms(ed) over the window (mean: 1-Lipschitz
+    in the max norm, population std: in the rms norm); thr0 by stream.terr0_from over the whole
+    stream's sums; a held threshold keeps its source's (stream.hip terr_kernel / scan_kernel,
+    main.py:464-466, :475-480, :485)."""
+
+    certify = True
+    TERR_ROUND = 1e-12  # float64 rounding of the statistics, far below any ed used here
+
+    def __init__(self, delta_local, ed_local, n_total, frame0, adaptive, k, W, Fa, F0, head_frames=CHUNK):
+        super().__init__(delta_local, n_total, frame0, adaptive, k, W, Fa, F0, head_frames)
+        self.e = np.asarray(ed_local, np.float64).copy()
+        self.etail = self.ehead = None
+        self.terr = np.full(self.n_local, np.nan)
+        self.terr0 = 0.0
+        self._unc, self._mslack, self._mzone = [], np.inf, 0.0
+
+    def ed(self, lo=0, hi=None):
+        return self.e[lo:hi].copy()
+
+    def set_ed_halos(self, tail, head):
+        assert tail.shape == (self.n_tail,) and head.shape == (self.n_head,)
+        self.etail, self.ehead = np.asarray(tail, np.float64), np.asarray(head, np.float64)
+
+    def ed_sums(self):
+        return float(np.sum(self.e)), float(np.sum(self.e * self.e))
+
+    def set_terr0(self, s1, s2):
+        from meteorgpu.stream import terr0_from
+        self.terr0 = terr0_from(s1, s2, self.n_total, self.k)
+
+    def fresh(self):
+        super().fresh()
+        ex, x0 = np.concatenate([self.etail, self.e, self.ehead]), self.frame0 - self.n_tail
+        for j in range(self.n_local):
+            i = self.frame0 + j
+            if i < self.F0:
+                continue
+            w = ex[max(0, i - self.W) - x0: i - x0]
+            self.terr[j] = (np.mean(w) + abs(self.k) * np.sqrt(np.mean(w * w))) * (1 + 1e-9) + self.TERR_ROUND \
+                if w.size else np.inf
+
+    def scan(self, thr0, entry, reset):
+        fz, last, thr, src, err = entry
+        runs = []
+        margin = np.inf
+        unc, mslack, mzone = [], np.inf, 0.0
+        for j in range(self.n_local):
+            i = self.frame0 + j
+            if i < self.F0:
+                thr, src, err = thr0, -1, self.terr0
+            elif i > fz:
+                thr, src, err = self.fr[j], i, self.terr[j]
+            self.thr[j] = thr
+            v = self.d[j]
+            margin = min(margin, abs(v - thr)) if not np.isnan(thr) else margin
+            zone = self.e[j] + err
+            slack = abs(v - thr) - zone
+            mzone = max(mzone, zone) if np.isfinite(zone) else mzone
+            if not slack > 0:  # NaN (a NaN threshold or bound) is uncertain too
+                unc.append((i, src))
+            elif slack < mslack:
+                mslack = slack
+            if v > thr:
+                if i > last + 1:
+                    runs.append([i, i])
+                elif runs:
+                    runs[-1][1] = i
+                else:
+                    runs.append([-1, i])
+                last = i
+                fz = max(i + self.Fa, max(0, i))
+        self._runs, self._margin = runs, margin
+        self._unc, self._mslack, self._mzone = unc, mslack, mzone
+        return (fz, last, thr, src, err), 1
+
+    def certificate(self):
+        lst = np.array(self._unc, np.int64).reshape(-1, 2)
+        return len(self._unc), self._mslack, self._mzone, lst
+
+
+def make_cert_shard(exact, approx, ed, rank, world, adaptive, k, W, Fa, F0, cuts=None):
+    """one rank's numpy certifying shard: the CertifyingShard loop of meteorgpu.stream over
+    NumpyCertOps, whose _refine_local puts the float64 values (``exact``) and a float64-grade bound
+    into the rank's own frames of the global ranges -- as IQShardDetector._refine_local recomputes
+    them from the samples with msd_iq_delta64_dev"""
+    from meteorgpu import stream
+
+    n = exact.size
+    lo, hi = shard_bounds(n, world, rank, cuts)
+
+    class Shard(stream.CertifyingShard):
+        certify = True
+
+        def __init__(self):
+            self.T, self.W, self.f0, self.f1 = n, (W if adaptive else 0), lo, hi
+            self.adaptive, self.k, self.F0 = adaptive, k, (F0 if adaptive else 0)
+            self.ops = NumpyCertOps(approx[lo:hi], ed[lo:hi], n, lo, adaptive, k, W, Fa, F0)
+            self._refined = stream._NO_IV
+            self.refined_local = 0  # frames this rank recomputed
+
+        def _refine_local(self, ranges):
+            for a, b in stream._as_iv(ranges):
+                a, b = max(int(a), self.f0), min(int(b), self.f1)
+                if b > a:
+                    self.ops.d[a - self.f0: b - self.f0] = exact[a:b]
+                    self.ops.e[a - self.f0: b - self.f0] = 1e-13
+                    self.refined_local += b - a
+
+    return Shard()
+
+
+def cert_stream(n, seed, ed_scale=2e-3, plants=(), W=600, Fa=100, F0=50, k=4.0, rate=0.01):
+    """(exact, approx, ed): a detector stream (test_stream_protocol.make_delta's shape: noise + bursts),
+    its approximation within a per-frame bound ed, and near ties planted at the frames in ``plants``:
+    each such frame's exact delta is moved to within 0.3 ed of the threshold the exact detector uses
+    there (oracle), so the approximate delta (0.9 ed away, random sign) may decide it either way"""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import dsp_oracle as O
+    rng = np.random.default_rng(seed)
+    d = rng.normal(0.0, 1.0, n)
+    t = 0
+    while True:
+        t += int(rng.exponential(1 / rate))
+        if t >= n:
+            break
+        L = int(rng.integers(1, 40))
+        d[t: t + L] += rng.uniform(3.0, 9.0)
+    ed = ed_scale * rng.uniform(0.5, 1.5, n)
+    for i in sorted(plants):
+        _, thr = O.get_detections_adaptive_ref(d, k, 1.0, W, 0, Fa, F0)
+        if np.isfinite(thr[i]):
+            d[i] = thr[i] + rng.choice([-0.3, 0.3]) * ed[i]
+    approx = d + rng.choice([-0.9, 0.9], n) * ed
+    return d, approx, ed

@@ -229,6 +229,28 @@ def test_spectrogram_vs_scipy(case):
     assert _frame_err(S, Sr) <= SPEC_TOL
 
 
+@pytest.mark.parametrize("dc,sigma", [(700, 600.0), (700, 3.0), (20000, 3.0), (-30000, 30.0)])
+@pytest.mark.parametrize("N,nov", [(1024, 512), (2048, 1024), (256, 128)])
+def test_spectrogram_dc_offset(dc, sigma, N, nov):
+    """a DC offset on the int16 audio (tests/test_iq.py's offset-700 case, and a large offset over quiet
+    noise): the detrend subtracts the frame mean as an exact two-part float32 value (stft1024.hip,
+    stft.hip), so scipy's spectrogram holds per frame and at bins 0, 1 -- where a residual of the mean
+    lands -- against each frame's mean power; 1024 / 512 is stft1024_kernel (C3)"""
+    rng = np.random.default_rng(abs(dc) + N)
+    n = 48000 * 2
+    t = np.arange(n) / 48000
+    x = dc + sigma * rng.standard_normal(n) + 4 * sigma * np.sin(2 * np.pi * 1000.0 * t)
+    x = np.clip(np.round(x), -32768, 32767).astype(np.int16)
+    from scipy.signal import spectrogram as sp_spec
+    _, _, Sr = sp_spec(x, fs=48000, window="hann", nperseg=N, noverlap=nov, nfft=N, scaling="density", mode="psd")
+    _, _, S = dsp.spectrogram(x, fs=48000, window="hann", nperseg=N, noverlap=nov, nfft=N)
+    assert _frame_err(S, Sr) <= SPEC_TOL
+    R = Sr.astype(np.float64)
+    mean = R.mean(axis=0)
+    for k in (0, 1):
+        assert np.max(np.abs(S[k].astype(np.float64) - R[k]) / mean) <= SPEC_TOL, k
+
+
 def test_spectrogram_constant_input_is_zero():
     # constant detrend removes a DC-only signal entirely
     x = np.full(48000, 1234, np.int16)

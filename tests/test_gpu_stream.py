@@ -679,21 +679,23 @@ def test_overlapped_detector_matches_in_order(chunk):
         assert np.array_equal(sa, sb)
 
 
-def test_overlap_restores_the_callers_reserve():
-    """MSD_OPT_CSTFT_RESERVE is context-wide: an overlapped detector puts the caller's value back on
-    close(), and also when its constructor fails after setting it"""
+def test_overlap_leaves_the_callers_context():
+    """the CU split lives on two sibling contexts: the caller's context keeps its options (ADVICE r4:
+    a context-wide option changed by the detector), also when the constructor fails"""
     from meteorgpu import _lib, iq
     ctx = _lib.Context(0)
     try:
         ctx.set_option(_lib.OPT_CSTFT_RESERVE, 3)
+        before = dict(ctx.options)
         det = iq.IQShardDetector(ctx, 192000 * 5, 192000, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
                                  5, 3, 2, 1, overlap=16)
-        assert ctx.options[_lib.OPT_CSTFT_RESERVE] == 16
+        assert det.sctx is not ctx and det.dctx is not ctx
+        assert det.sctx.options[_lib.OPT_STREAM_CUS] == -16 and det.dctx.options[_lib.OPT_STREAM_CUS] == 16
         det.close()
-        assert ctx.options[_lib.OPT_CSTFT_RESERVE] == 3
+        assert ctx.options == before
         with pytest.raises(_lib.MsdError):  # the stream plan refuses seg_len 100 (not a multiple of 64)
             iq.IQShardDetector(ctx, 192000 * 5, 192000, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
                                5, 3, 2, 1, overlap=16, seg_len=100)
-        assert ctx.options[_lib.OPT_CSTFT_RESERVE] == 3
+        assert ctx.options == before
     finally:
         ctx.close()

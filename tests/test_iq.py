@@ -154,7 +154,73 @@ def test_detrend_from_given_frame_sums(dc, kind):
     _, _, rS = Q.spectrogram_iq_ref(i, q, fs, 4096, 3072)
     assert _frame_rel(own.T.astype(np.float64), rS) < SPEC_TOL
     assert _frame_rel(given.T.astype(np.float64), rS) < SPEC_TOL
-    assert _frame_rel(given.T.astype(np.float64), own.T.astype(np.float64)) < 1e-6
+    if kind == "int16":  # exact sums either way: the same two-part mean, the same bits
+        np.testing.assert_array_equal(given, own)
+    else:
+        assert _frame_rel(given.T.astype(np.float64), own.T.astype(np.float64)) < 1e-6
     for buf in (fsum, d, e):
         buf.free()
     b.close()
+
+
+def _dc_bins_rel(S, R):
+    """largest error of bins 0, 1, N-1 (the bins a DC offset lands in), each frame's error relative
+    to that frame's mean power"""
+    mean = R.mean(axis=0)
+    return float(max(np.max(np.abs(S[k] - R[k]) / mean) for k in (0, 1, R.shape[0] - 1)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dc,sigma", [(700, 3.0), (4000, 30.0), (16000, 3.0), (30000, 3.0), (-32000, 30.0)])
+@pytest.mark.parametrize("noverlap", [3072, 2048])
+def test_large_dc_over_quiet_noise(dc, sigma, noverlap):
+    """an SDR's DC offset far above the noise.  The detrend subtracts the frame mean before
+    the window as an exact two-part float32 value (cstft.hip), so the result is scipy's within the
+    float32 rounding of the detrended samples: per frame within SPEC_TOL, and bins 0, 1, N-1 -- where a
+    mis-subtracted mean lands -- checked one by one against the frame's mean power.  With the exact
+    frame sums given (the certified C5 path) and computed in the kernel alike; hop 1024 and 2048.
+    (Round 4's post-FFT detrend gave 2.7e-5 per frame at (700, 3) and 9e-4 at (30000, 3); a
+    single-float mean 1e-4 at (16000, 3): tools/dbg/dc_precision.py.)"""
+    from meteorgpu import _lib, iq
+    from meteorgpu.dsp import context
+    rng = np.random.default_rng(abs(dc) + int(sigma))
+    fs, n = 192000, 40000
+    z = sigma * (rng.standard_normal(n) + 1j * rng.standard_normal(n)) + dc * (1 - 0.5j)
+    i = np.clip(np.round(z.real), -32768, 32767).astype(np.int16)
+    q = np.clip(np.round(z.imag), -32768, 32767).astype(np.int16)
+    x = np.empty(2 * n, np.int16)
+    x[0::2], x[1::2] = i, q
+    ctx = context(0)
+    b = iq.IQBatch(ctx, 1, n, fs, 4096, noverlap)
+    b.upload(0, x)
+    b.run()
+    own = b.frames(0, 0, b.T).T.astype(np.float64)
+    _, _, R = Q.spectrogram_iq_ref(i, q, fs, 4096, noverlap)
+    assert _frame_rel(own, R) < SPEC_TOL
+    assert _dc_bins_rel(own, R) < SPEC_TOL
+    if noverlap == 3072:
+        T = b.T
+        fsum, d, e = ctx.alloc(16 * T), ctx.alloc(8 * T), ctx.alloc(8 * T)
+        band, noise = iq.iq_band_bins(4096, fs, (950.0, 1050.0)), iq.iq_band_bins(4096, fs, (-3050.0, -2950.0))
+        _lib.iq_delta64_dev(ctx, b.d_x, b.code, n, 4096, 1024, float(fs), band, noise,
+                            np.array([[0, T]], np.int64), d, e, frame_sums=fsum)
+        b.run(fsums=fsum)
+        given = b.frames(0, 0, b.T).T.astype(np.float64)
+        np.testing.assert_array_equal(given, own)
+        for buf in (fsum, d, e):
+            buf.free()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_large_dc_float32():
+    """float32 I/Q with a DC offset 1e4 times the noise: the two-part mean from the float sums"""
+    from meteorgpu import iq
+    rng = np.random.default_rng(77)
+    n = 30000
+    z = 1e-4 * (rng.standard_normal(n) + 1j * rng.standard_normal(n)) + (0.6 + 0.3j)
+    i, q = z.real.astype(np.float32), z.imag.astype(np.float32)
+    _, _, S = iq.spectrogram_iq(i, q, 192000, 4096, 3072)
+    _, _, R = Q.spectrogram_iq_ref(i, q, 192000, 4096, 3072)
+    assert _frame_rel(S, R) < SPEC_TOL
+    assert _dc_bins_rel(S, R) < SPEC_TOL

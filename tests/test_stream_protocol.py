@@ -169,3 +169,108 @@ def test_random_configs_and_cuts(seed):
     res = run_protocol(d, world, adaptive, k, W, Fa, F0, cuts)
     check(res, d, adaptive, k, W, Fa, F0)
     assert want is not None
+
+
+# ----------------------------------------------------------------------------------------------
+# The certified C5 protocol (meteorgpu.stream.CertifyingShard, the loop IQShardDetector.detect runs)
+# across ranks: an approximate delta within a per-frame bound, near ties planted at and beside shard
+# edges so that uncertain decisions' threshold windows cross into other ranks' shards; each rank
+# refines its own part of the merged dependencies, the halos (delta and bound) are exchanged again,
+# and every rank ends certified with the float64 oracle's detections and dB means.
+CERT_N, CERT_W, CERT_FA, CERT_F0, CERT_K = 12000, 600, 100, 50, 4.0
+
+
+def _cert_plants(n, world):
+    edges = [n * r // world for r in range(1, world)]
+    return sorted({p for e in edges for p in (e - 7, e, e + 3, e + 250)} | {n // 2 + 11, n - 20})
+
+
+def _cert_case(world, seed):
+    from stream_np_ops import cert_stream
+    return cert_stream(CERT_N, seed, plants=_cert_plants(CERT_N, world), W=CERT_W, Fa=CERT_FA, F0=CERT_F0,
+                       k=CERT_K)
+
+
+def _cert_body(exact, approx, ed, world, exact_decisions=True):
+    from stream_np_ops import make_cert_shard
+
+    def body(r, comm):
+        sh = make_cert_shard(exact, approx, ed, r, world, True, CERT_K, CERT_W, CERT_FA, CERT_F0)
+        res = sh.detect(comm, thresholds=False, exact_decisions=exact_decisions)
+        return res, sh.refined_local
+    return body
+
+
+def _check_cert(results, exact):
+    want, _ = oracle(exact, True, CERT_K, CERT_W, CERT_FA, CERT_F0)
+    assert len(want) > 20
+    for res, _ in results:
+        assert res.certified and not res.near_tie and not res.refine_budget_exhausted
+        assert res.uncertain_initial > 0 and res.detector_passes >= 2  # the planted ties were caught
+        got = [(int(a), int(b)) for a, b, _ in res.detections]
+        assert got == [(a, b) for a, b, _ in want]
+        np.testing.assert_allclose(res.detections["db"], [w[2] for w in want], rtol=0, atol=1e-9)
+    # every rank refined its own part of the merged ranges, and the same total
+    assert len({int(res.refined_delta_frames) for res, _ in results}) == 1
+    assert sum(n for _, n in results) == int(results[0][0].refined_delta_frames)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_certified_protocol_threads(world):
+    exact, approx, ed = _cert_case(world, 40 + world)
+    res = run_threads(world, _cert_body(exact, approx, ed, world))
+    _check_cert(res, exact)
+    if world > 1:  # the windows of the ties beside the edges reach into the previous shard
+        assert all(n > 0 for _, n in res)
+
+
+def test_certified_flag_only_reports_the_ties():
+    """certification without refinement: the planted ties are listed, nothing is claimed certified"""
+    exact, approx, ed = _cert_case(2, 42)
+    res = run_threads(2, _cert_body(exact, approx, ed, 2, exact_decisions=False))
+    for r, n in res:
+        assert not r.certified and r.uncertain > 0 and n == 0
+        frames = set(int(f) for f in r.uncertain_frames[:, 0])
+        assert frames & set(_cert_plants(CERT_N, 2))
+    assert np.array_equal(res[0][0].uncertain_frames, res[1][0].uncertain_frames)  # merged on every rank
+
+
+def _gloo_cert_rank(rank, world, port, out):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "meteor-scatter_amd"), os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from torch_comm import TorchComm
+    import test_stream_protocol as T
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        exact, approx, ed = T._cert_case(world, 60 + world)
+        res, n = T._cert_body(exact, approx, ed, world)(rank, TorchComm())
+        np.savez(os.path.join(out, f"c{rank}.npz"), start=res.detections["start"], stop=res.detections["stop"],
+                 db=res.detections["db"], info=np.array([res.certified, res.uncertain_initial, res.detector_passes,
+                                                         res.refined_delta_frames, n, res.near_tie], np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_certified_protocol_gloo(world, tmp_path):
+    """the same across real processes (gloo allgathers): the certificate merge, the refinement of
+    windows that cross shard edges by their owners, and the halo refresh before the dB means"""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_gloo_cert_rank, args=(world, port, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    exact, approx, _ = _cert_case(world, 60 + world)
+    want, _ = oracle(exact, True, CERT_K, CERT_W, CERT_FA, CERT_F0)
+    # the uncertified approximate delta would give other detections: the refinement is what fixes them
+    assert [w[:2] for w in oracle(approx, True, CERT_K, CERT_W, CERT_FA, CERT_F0)[0]] != [w[:2] for w in want]
+    tot = []
+    for r in range(world):
+        z = np.load(tmp_path / f"c{r}.npz")
+        cert, unc0, passes, refined, n, tie = (int(v) for v in z["info"])
+        assert cert == 1 and tie == 0 and unc0 > 0 and passes >= 2 and n > 0
+        assert [(int(a), int(b)) for a, b in zip(z["start"], z["stop"])] == [(a, b) for a, b, _ in want]
+        np.testing.assert_allclose(z["db"], [w[2] for w in want], rtol=0, atol=1e-9)
+        tot.append((refined, n))
+    assert len({t[0] for t in tot}) == 1 and sum(t[1] for t in tot) == tot[0][0]

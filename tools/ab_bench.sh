@@ -1,6 +1,7 @@
 #!/bin/bash
 # Alternate bench runs between in-tree library variants (GPU box).
-# Usage: [WL=c3|live|c5] tools/ab_bench.sh ROUNDS TAG...   ("cur" = meteorgpu/libmsdsp.so)
+# Usage: [WL=c3|live|c5] [AB_ARGS="more bench.py args"] tools/ab_bench.sh ROUNDS TAG...
+# ("cur" = meteorgpu/libmsdsp.so, TAG = tools/ubench/bin/libmsdsp_TAG.so)
 # Logs to gpurun_out/ab_<wl>_<tag>_<i>.log; prints ms/step, the roofline kernel's ms and the
 # per-kernel ms of every run.
 set -u
@@ -13,7 +14,7 @@ for i in $(seq 1 "$N"); do
     [ "$t" = cur ] && lib=$ROOT/meteor-scatter_amd/meteorgpu/libmsdsp.so
     extra=""; [ "$WL" = c3 ] && extra="--no-c5"
     MSD_LIB_PATH=$lib timeout -k 10 200 python3 "$ROOT/bench.py" --workload "$WL" --steps 10 --warmup 2 \
-        --no-cpu-baseline $extra > "$ROOT/gpurun_out/ab_${WL}_${t}_$i.log" 2>&1 || exit 1
+        --no-cpu-baseline $extra ${AB_ARGS:-} > "$ROOT/gpurun_out/ab_${WL}_${t}_$i.log" 2>&1 || exit 1
   done
 done
 for t in "$@"; do

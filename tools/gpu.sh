@@ -10,7 +10,7 @@
 #   tools/gpu.sh trace  NAME [bench.py args]    rocprofv3 --kernel-trace --stats of a bench run +
 #                                               tools/trace_gaps.py step timeline
 #   tools/gpu.sh ab     WL ROUNDS TAG...        tools/ab_bench.sh (variants in tools/ubench/bin)
-#   tools/gpu.sh stft_ab MODE ROUNDS LIB...     tools/stft_ab (MODE c3 | c5), variant libraries
+#   tools/gpu.sh stft_ab NAME MODE ROUNDS LIB... tools/stft_ab (MODE c3 | c5; STFT_AB_* env passed on)
 #   tools/gpu.sh pmc    TAG REGEX [bench args]  tools/pmc_stft.sh's four PMC passes
 #   tools/gpu.sh round  TAG                     tools/profile_round.sh (bench + traces + PMC)
 #   tools/gpu.sh py     NAME SECONDS SCRIPT [args]  a python script under a time limit
@@ -64,11 +64,11 @@ step() {
       head -14 "gpurun_out/${name}_gaps.txt" ;;
     ab)
       local wl=$1; shift
-      WL=$wl timeout -k 10 900 bash tools/ab_bench.sh "$@" ;;
+      WL=$wl timeout -k 10 1100 bash tools/ab_bench.sh "$@" ;;
     stft_ab)
-      local mode=$1 rounds=$2; shift 2
-      STFT_AB_MODE=$mode timeout -k 10 400 tools/stft_ab "$rounds" "$@" > "gpurun_out/stft_ab_$mode.txt" 2>&1; local rc=$?
-      tail -8 "gpurun_out/stft_ab_$mode.txt"; return $rc ;;
+      local name=$1 mode=$2 rounds=$3; shift 3
+      STFT_AB_MODE=$mode timeout -k 10 400 tools/stft_ab "$rounds" "$@" > "gpurun_out/$name.txt" 2>&1; local rc=$?
+      tail -8 "gpurun_out/$name.txt"; return $rc ;;
     pmc)
       local tag=$1 regex=$2; shift 2
       REGEX=$regex timeout -k 10 900 bash tools/pmc_stft.sh "$tag" "$@" || return 1
