@@ -217,14 +217,17 @@ __global__ __launch_bounds__(NW * 64) void stft_psd_kernel(const T *__restrict__
         if (t < nfr) {
             float s[SPL];
             load_samples<T, SPL>(xf + t * hop + lane * SPL, s);
+            // the per-lane sums accumulate x - xref, xref the frame's first sample: exact for integer
+            // samples, and for float ones a DC offset does not enter their float rounding; the wave
+            // sum in fp64.  The mean is subtracted as hi + lo (hi its float32 rounding, lo the rest),
+            // so that the detrended sample is the float32 rounding of x - mean also where float(mean)
+            // is not exact (|mean| >= 2^24 / N for integer input: a residual DC at bins 0, 1 otherwise)
+            const float xref = __shfl(s[0], 0, 64);
             float ls = 0.f;
 #pragma unroll
-            for (int q = 0; q < SPL; ++q) ls += s[q];
-            // integer samples: per-lane sums are exact in fp32, the wave sum in fp64; the mean is
-            // subtracted as hi + lo (hi its float32 rounding, lo the rest), so that the detrended
-            // sample is the float32 rounding of x - mean also where float(mean) is not exact
-            // (|mean| >= 2^24 / N for integer input: a residual DC at bins 0, 1 otherwise)
-            const double md = detrend ? wave_sum(static_cast<double>(ls)) / static_cast<double>(N) : 0.0;  // detrend_none: 0
+            for (int q = 0; q < SPL; ++q) ls += s[q] - xref;
+            const double md = detrend ? (double)xref + wave_sum(static_cast<double>(ls)) / static_cast<double>(N)
+                                      : 0.0;  // detrend_none: 0
             const float mean = static_cast<float>(md), mlo = static_cast<float>(md - static_cast<double>(mean));
             const float *w = win + lane * SPL;
 #pragma unroll

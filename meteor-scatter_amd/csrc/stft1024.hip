@@ -333,7 +333,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         float2 v[2][8], wv[8];
         // ---- detrend (consumes raw); the window is applied inside pass 1
         {
-            float mean[2], mlo[2] = {0.f, 0.f};
+            float mean[2], mlo[2] = {0.f, 0.f}, xr[2] = {0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 if constexpr (IO::kInt) {
@@ -358,21 +358,31 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                     mean[q] = detrend ? ft * (1.0f / 1024.0f) : 0.f;
                     mlo[q] = detrend ? (float)(tot - (int)ft) * (1.0f / 1024.0f) : 0.f;
                 } else {
-                    float s = 0.f;
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) s += IO::lo(raw[RB * q + r]) + IO::hi(raw[RB * q + r]);
-                    s = row_sum_f(s);
+                    // float samples: the frame's first sample (lane 0's first value) comes off before
+                    // the float sums, so that they accumulate the variation and not a DC offset (a
+                    // float sum of 1024 values near m is off by ~10 u |m|: a residual DC otherwise);
+                    // the mean is xref + the mean of x - xref
                     auto rl = [](float a, int lane) {
                         return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), lane));
                     };
+                    const float xref = detrend ? rl(IO::lo(raw[RB * q]), 0) : 0.f;
+                    float s = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) s += (IO::lo(raw[RB * q + r]) - xref) + (IO::hi(raw[RB * q + r]) - xref);
+                    s = row_sum_f(s);
                     const float tot = (rl(s, 0) + rl(s, 16)) + (rl(s, 32) + rl(s, 48));
                     mean[q] = detrend ? tot * (1.0f / 1024.0f) : 0.f;
+                    xr[q] = xref;
                 }
             }
-            // each sample register converted once (SH: the shared half serves both frames)
+            // each sample register converted once (SH: the shared half serves both frames); float
+            // samples relative to their frame's xref
             float2 fr[NR];
 #pragma unroll
-            for (int i = 0; i < NR; ++i) fr[i] = make_float2(IO::lo(raw[i]), IO::hi(raw[i]));
+            for (int i = 0; i < NR; ++i) {
+                if constexpr (IO::kInt) fr[i] = make_float2(IO::lo(raw[i]), IO::hi(raw[i]));
+                else fr[i] = make_float2(IO::lo(raw[i]) - xr[i / RB], IO::hi(raw[i]) - xr[i / RB]);
+            }
 #pragma unroll
             for (int r = 0; r < 8; r += 2) {
                 const float4 w4 = tab4(r);

@@ -251,6 +251,24 @@ def test_spectrogram_dc_offset(dc, sigma, N, nov):
         assert np.max(np.abs(S[k].astype(np.float64) - R[k]) / mean) <= SPEC_TOL, k
 
 
+@pytest.mark.parametrize("N,nov", [(1024, 512), (2048, 1024), (256, 128)])
+def test_spectrogram_float32_dc_offset(N, nov):
+    """float32 samples with a DC offset 6000 x the noise: the kernels' float sums run relative to each
+    frame's first sample and the mean comes off as hi + lo, so the result is the float64 spectrogram
+    of the same float32 samples within SPEC_TOL.  (scipy on the float32 array itself detrends in
+    float32 with numpy's float32 pairwise mean and is 5e-4 away from that here -- shown below --
+    so no float32 pipeline with another summation order can reproduce it to 1e-5.)"""
+    rng = np.random.default_rng(N)
+    x = (0.6 + 1e-4 * rng.standard_normal(48000)).astype(np.float32)
+    from scipy.signal import spectrogram as sp_spec
+    _, _, R64 = sp_spec(x.astype(np.float64), fs=48000, window="hann", nperseg=N, noverlap=nov, nfft=N,
+                        scaling="density", mode="psd")
+    _, _, R32 = sp_spec(x, fs=48000, window="hann", nperseg=N, noverlap=nov, nfft=N, scaling="density", mode="psd")
+    _, _, S = dsp.spectrogram(x, fs=48000, window="hann", nperseg=N, noverlap=nov, nfft=N)
+    assert _frame_err(S, R64) <= SPEC_TOL
+    assert _frame_err(R32, R64) > 10 * SPEC_TOL  # scipy's own float32 detrend
+
+
 def test_spectrogram_constant_input_is_zero():
     # constant detrend removes a DC-only signal entirely
     x = np.full(48000, 1234, np.int16)

@@ -2,7 +2,7 @@ L=tools/ubench/bin/libmsdsp_pdold.so; C=meteor-scatter_amd/meteorgpu/libmsdsp.so
 tools/gpu.sh multi 'test t_c5 tests/test_iq.py tests/test_gpu_certify.py tests/test_gpu_stream.py tests/test_gpu_parity.py' 'py dcprec2 400 tools/dbg/dc_precision.py' "stft_ab ab_pd0 c5 8 $L $C" || exit 1
 STFT_AB_FSUMS=1,1 tools/gpu.sh stft_ab ab_pd2 c5 8 $L $C || exit 1
 tools/gpu.sh stft_ab ab_c3 c3 8 $L $C $N || exit 1
-for ov in 0 8 16 32; do echo "== overlap $ov"; tools/gpu.sh c5 c5ov$ov 1 --c5-overlap $ov || exit 1; done
+for ov in 0 4 8 16 32; do echo "== overlap $ov"; tools/gpu.sh c5 c5ov$ov 1 --c5-overlap $ov || exit 1; done
 AB_ARGS='--c5-mode exact' tools/gpu.sh ab c5 2 pdold cur
 tools/gpu.sh py mall 300 tools/dbg/mall_interleave.py
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
