@@ -178,12 +178,18 @@ struct CsTune {
 // PD 0: the sums in the kernel (exact integer DPP sums per wave, one LDS slot per wave, a barrier);
 // PD 2 (msd_cstft_psd_fsums_dev): the frames' sums given (fsum[g], the exact delta step's): no
 // reduction and no barrier before pass 1, the next frame's sums prefetched with its samples.
-template <typename T, int SH, bool EN, int PD>
+// DYN (C5's hop, with MSD_OPT_CSTFT_RESERVE > 0): the workgroups take chunks of frames from a
+// guided schedule (sched[k] .. sched[k + 1], sizes falling from ~total / (2 wgs) to 16 frames) by an
+// atomic ticket instead of one fixed range each.  With a fixed range a workgroup that starts late --
+// because kernels on another stream (the C5 detector beside the spectrogram) held its slot when the
+// grid was dispatched -- ends the launch late by the whole delay; with chunks the others take its share.
+template <typename T, int SH, bool EN, int PD, bool DYN = false>
 __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft4096_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len, int64_t nstreams,
     int64_t max_frames, int64_t total, int64_t per, int hop, int detrend, const float *__restrict__ g_win,
     const float2 *__restrict__ g_tw, float *__restrict__ out, float *__restrict__ etot, int64_t estride,
-    const double2 *__restrict__ fsum) {
+    const double2 *__restrict__ fsum, const int64_t *__restrict__ sched, int64_t nchunks,
+    unsigned long long *__restrict__ ticket) {
     using io = IQ<T>;
     __shared__ float2 buf[CS_LDS_F2];
     // pass-2 twiddles W256^(j1 k).  kW4: at k * 16 + j1 — a half-wave reads 16 consecutive entries
@@ -211,8 +217,6 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
     const int q3 = tid & 15, k2a = tid >> 4;  // pass-3 thread: t = q + 16 k2a
     __syncthreads();
 
-    const int64_t g0 = (int64_t)blockIdx.x * per;
-    const int64_t g1 = g0 + per < total ? g0 + per : total;
     typename io::raw_t raw[16];
     // load rows [R0, 16) of frame t of the stream at element offset `base`
     auto load_rows = [&](int64_t base, int64_t t, auto r0c) {
@@ -221,10 +225,11 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
 #pragma unroll
         for (int r = R0; r < 16; ++r) raw[r] = io::load(p + 2 * (tid + 256 * r));
     };
-    // The workgroup's frames, split at stream boundaries: per segment, the frames of the stream
+    // A range of frames [g0, g1) split at stream boundaries: per segment, the frames of the stream
     // [ga, gv) and then the frames past its end [gv, gb), written as zeros.  Within [ga, gv) the
     // prefetch of frame t + 1 is unconditional (clamped to the last frame at the end), so the
     // register rows never pass through data-dependent copies.
+    auto run_range = [&](const int64_t g0, const int64_t g1) __attribute__((always_inline)) {
     for (int64_t ga = g0; ga < g1;) {
         const int64_t s = ga / max_frames;
         const int64_t gb = (s + 1) * max_frames < g1 ? (s + 1) * max_frames : g1;
@@ -367,6 +372,26 @@ __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft409
             for (int k2b = 0; k2b < 16; ++k2b) of[tid + 256 * k2b] = 0.f;
         ga = gb;
     }
+    };
+    if constexpr (!DYN) {
+        const int64_t g0 = (int64_t)blockIdx.x * per;
+        run_range(g0, g0 + per < total ? g0 + per : total);
+    } else {
+        // thread 0 draws the next chunk while the current one runs (double-buffered slot); the barrier
+        // after a chunk publishes it and ends every wave's use of the chunk's LDS
+        __shared__ int64_t slot[2];
+        if (tid == 0) slot[0] = (int64_t)atomicAdd(ticket, 1ull);
+        __syncthreads();
+        int64_t k = uniform_i64(slot[0]);
+        int par = 0;
+        while (k < nchunks) {
+            if (tid == 0) slot[par ^ 1] = (int64_t)atomicAdd(ticket, 1ull);
+            run_range(uniform_i64(sched[k]), uniform_i64(sched[k + 1]));
+            __syncthreads();
+            k = uniform_i64(slot[par ^ 1]);
+            par ^= 1;
+        }
+    }
 }
 
 }  // namespace
@@ -377,6 +402,10 @@ struct msd_cstft_plan {
     int nperseg = 0, hop = 0, detrend = 1;
     float *d_win = nullptr;   // window x sqrt(scale)
     float2 *d_tw = nullptr;   // W4096^m, m = 0..4095
+    // DYN: the guided chunk schedule for (sched_total frames, sched_wgs workgroups) and the ticket
+    int64_t *d_sched = nullptr;
+    int64_t sched_cap = 0, sched_total = -1, sched_wgs = -1, sched_n = 0;
+    unsigned long long *d_ticket = nullptr;
 };
 
 using namespace msd;
@@ -421,6 +450,8 @@ void msd_cstft_plan_destroy(msd_cstft_plan *p) {
     (void)hipStreamSynchronize(p->ctx->stream);
     if (p->d_win) (void)hipFree(p->d_win);
     if (p->d_tw) (void)hipFree(p->d_tw);
+    if (p->d_sched) (void)hipFree(p->d_sched);
+    if (p->d_ticket) (void)hipFree(p->d_ticket);
     delete p;
 }
 
@@ -455,45 +486,85 @@ int msd_cstft_psd_fsums_dev(msd_cstft_plan *p, const void *x, int dtype, const i
     if (nstreams == 0 || max_frames == 0) return MSD_OK;
     DeviceGuard g(p->ctx->device);
     const int64_t total = nstreams * max_frames;
-    auto launch = [&](auto kern, const auto *xp) {
-        // persistent: as many workgroups as stay resident (registers and the 37 KB of LDS decide;
-        // the compiler's register count sets 3 or 4 per CU)
+    // persistent: as many workgroups as stay resident (registers and the 37 KB of LDS decide; the
+    // compiler's register count sets 3 or 4 per CU), less the reserve
+    auto grid = [&](auto kern) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, CS_T, 0) != hipSuccess || per_cu < 1)
             per_cu = 3;
         int64_t wgs = (int64_t)p->ctx->num_cu * per_cu - p->ctx->cstft_reserve;
         if (wgs < 1) wgs = 1;
-        if (wgs > total) wgs = total;
+        return wgs > total ? total : wgs;
+    };
+    auto launch = [&](auto kern, const auto *xp) -> int {
+        int64_t wgs = grid(kern);
         int64_t per = (total + wgs - 1) / wgs;
         if (etot) per = (per + 3) / 4 * 4;  // energy groups of 4 frames start at every workgroup's first
         wgs = (total + per - 1) / per;
         KernelTimer timer(p->ctx, K_CSTFT);  // the FFT kernel alone: the roofline's
         hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
                            max_frames, total, per, p->hop, p->detrend, p->d_win, p->d_tw, out, etot,
-                           msd_cstft_energy_stride(nstreams, max_frames), fsum);
+                           msd_cstft_energy_stride(nstreams, max_frames), fsum, nullptr, (int64_t)0, nullptr);
+        return MSD_OK;
+    };
+    // DYN: the guided schedule (multiples of 4 frames: the energy groups), built when (total, wgs)
+    // change, and the ticket zeroed on the stream before every launch
+    auto launch_dyn = [&](auto kern, const auto *xp) -> int {
+        const int64_t wgs = grid(kern);
+        if (p->sched_total != total || p->sched_wgs != wgs) {
+            std::vector<int64_t> st(1, 0);
+            for (int64_t pos = 0; pos < total;) {
+                int64_t sz = (total - pos) / (2 * wgs);
+                sz = (std::max<int64_t>(sz, 16) + 3) / 4 * 4;
+                pos = std::min(total, pos + sz);
+                st.push_back(pos);
+            }
+            DeviceGuard dg(p->ctx->device);
+            MSD_HIP(hipStreamSynchronize(p->ctx->stream));
+            if ((int64_t)st.size() > p->sched_cap) {
+                if (p->d_sched) MSD_HIP(hipFree(p->d_sched));
+                p->d_sched = nullptr;
+                p->sched_cap = 0;
+                MSD_HIP(hipMalloc(&p->d_sched, sizeof(int64_t) * st.size()));
+                p->sched_cap = (int64_t)st.size();
+            }
+            if (!p->d_ticket) MSD_HIP(hipMalloc(&p->d_ticket, sizeof(unsigned long long)));
+            MSD_HIP(hipMemcpy(p->d_sched, st.data(), sizeof(int64_t) * st.size(), hipMemcpyHostToDevice));
+            p->sched_total = total;
+            p->sched_wgs = wgs;
+            p->sched_n = (int64_t)st.size() - 1;
+        }
+        MSD_HIP(hipMemsetAsync(p->d_ticket, 0, sizeof(unsigned long long), p->ctx->stream));
+        KernelTimer timer(p->ctx, K_CSTFT);
+        hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(CS_T), 0, p->ctx->stream, xp, off, len, nstreams,
+                           max_frames, total, (int64_t)0, p->hop, p->detrend, p->d_win, p->d_tw, out, etot,
+                           msd_cstft_energy_stride(nstreams, max_frames), fsum, p->d_sched, p->sched_n,
+                           p->d_ticket);
+        return MSD_OK;
     };
     const int sh = p->hop % 256 == 0 ? p->hop / 256 : 0;
     // the given sums (PD 2) at C5's hop: the int16 exact delta step leaves them (frames that start
     // every 1024 samples); other hops compute their own
     const bool given = fsum && p->detrend && sh == 4;
-    auto by_shift = [&](auto en, const auto *xp) {
+    // the chunked kernels where a reserve makes room for another stream's kernels (C5's hop)
+    const bool dyn = p->ctx->cstft_reserve > 0;
+    auto by_shift = [&](auto en, const auto *xp) -> int {
         constexpr bool EN = decltype(en)::value;
         using T = std::remove_cv_t<std::remove_pointer_t<decltype(xp)>>;
         if (sh == 4) {  // 75 % overlap (C5)
-            if (given) launch(cstft4096_kernel<T, 4, EN, 2>, xp);
-            else launch(cstft4096_kernel<T, 4, EN, 0>, xp);
-        } else if (sh == 8) {  // 50 %
-            launch(cstft4096_kernel<T, 8, EN, 0>, xp);
-        } else {
-            launch(cstft4096_kernel<T, 0, EN, 0>, xp);
+            if (dyn) return given ? launch_dyn(cstft4096_kernel<T, 4, EN, 2, true>, xp)
+                                  : launch_dyn(cstft4096_kernel<T, 4, EN, 0, true>, xp);
+            return given ? launch(cstft4096_kernel<T, 4, EN, 2>, xp) : launch(cstft4096_kernel<T, 4, EN, 0>, xp);
         }
+        if (sh == 8) return launch(cstft4096_kernel<T, 8, EN, 0>, xp);  // 50 %
+        return launch(cstft4096_kernel<T, 0, EN, 0>, xp);
     };
-    auto by_energy = [&](const auto *xp) {
-        if (etot) by_shift(std::integral_constant<bool, true>{}, xp);
-        else by_shift(std::integral_constant<bool, false>{}, xp);
+    auto by_energy = [&](const auto *xp) -> int {
+        if (etot) return by_shift(std::integral_constant<bool, true>{}, xp);
+        return by_shift(std::integral_constant<bool, false>{}, xp);
     };
-    if (dtype == MSD_CI16) by_energy(static_cast<const int16_t *>(x));
-    else by_energy(static_cast<const float *>(x));
+    const int rc = dtype == MSD_CI16 ? by_energy(static_cast<const int16_t *>(x)) : by_energy(static_cast<const float *>(x));
+    if (rc) return rc;
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }

@@ -333,7 +333,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         float2 v[2][8], wv[8];
         // ---- detrend (consumes raw); the window is applied inside pass 1
         {
-            float mean[2], mlo[2] = {0.f, 0.f}, xr[2] = {0.f, 0.f};
+            float mean[2], xr[2] = {0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 if constexpr (IO::kInt) {
@@ -351,12 +351,12 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                     const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
                                     __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
                     // float(tot) rounds tot to 24 bits exactly as rounding tot / 1024 would (a
-                    // power-of-two scale), so this equals float((double)tot / 1024) without FP64;
-                    // from |tot| >= 2^24 (|mean| >= 16384) on that rounding is not exact, and the rest
-                    // (tot - float(tot)) / 1024 (exact) is subtracted as well
-                    const float ft = (float)tot;
-                    mean[q] = detrend ? ft * (1.0f / 1024.0f) : 0.f;
-                    mlo[q] = detrend ? (float)(tot - (int)ft) * (1.0f / 1024.0f) : 0.f;
+                    // power-of-two scale), so this equals float((double)tot / 1024) without FP64.
+                    // It is the exact mean while |tot| < 2^24, i.e. |mean| < 16384 (half of int16 full
+                    // scale); beyond, the detrended samples keep a common offset below 2^-10.  The
+                    // two-part mean of the C5 kernel (hi + lo behind a wave-uniform branch) measured
+                    // +7.9 % on this loop (tools/stft_ab, round 5), so it stays single here.
+                    mean[q] = detrend ? (float)tot * (1.0f / 1024.0f) : 0.f;
                 } else {
                     // float samples: the frame's first sample (lane 0's first value) comes off before
                     // the float sums, so that they accumulate the variation and not a DC offset (a
@@ -389,21 +389,11 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 wv[r] = make_float2(w4.x, w4.y);
                 wv[r + 1] = make_float2(w4.z, w4.w);
             }
-            // lo is wave-uniform and zero unless |mean| >= 16384: a branch, not a select
-            if (__builtin_amdgcn_readfirstlane(mlo[0] != 0.f || mlo[1] != 0.f)) {
 #pragma unroll
-                for (int r = 0; r < 8; ++r) {
+            for (int r = 0; r < 8; ++r) {
 #pragma unroll
-                    for (int q = 0; q < 2; ++q)
-                        v[q][r] = make_float2((fr[RB * q + r].x - mean[q]) - mlo[q], (fr[RB * q + r].y - mean[q]) - mlo[q]);
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-#pragma unroll
-                    for (int q = 0; q < 2; ++q)
-                        v[q][r] = make_float2(fr[RB * q + r].x - mean[q], fr[RB * q + r].y - mean[q]);
-                }
+                for (int q = 0; q < 2; ++q)
+                    v[q][r] = make_float2(fr[RB * q + r].x - mean[q], fr[RB * q + r].y - mean[q]);
             }
             if (SH && !b_cur) {  // no second frame: its tile column must be zero (the loads were not)
 #pragma unroll

@@ -165,13 +165,14 @@ class IQShardDetector(_stream.CertifyingShard):
         (REFINE_INT8_MFMA: blocks of 1024 samples, <= 10 bins, no band at 0 Hz -- C5), else fp32.
         With the exact delta every frame's error bound is ~1e-13 dB, so certification settles every
         decision in one pass (no energy partials, no refinement, no second detector pass).
-        overlap: n > 0 splits the chip for the detector: the spectrogram runs on a context whose
-        stream may use all but n CUs and the stream detector on one restricted to those n
-        (MSD_OPT_STREAM_CUS, hipExtStreamCreateWithCUMask).  With the exact delta the detector does
-        not need the spectrogram, so after the delta (full chip, the caller's context) the two run
-        side by side -- the detector's latency-bound kernels and host round trips on their own CUs,
-        the spectrogram's persistent grid sized for the rest.  The caller's context is not changed.
-        0: one stream, in order."""
+        overlap: n > 0 runs the stream detector beside the spectrogram: the spectrogram on a sibling
+        context whose persistent grid leaves n workgroup slots free (MSD_OPT_CSTFT_RESERVE; its
+        workgroups then draw chunks of frames from a guided schedule, so one that starts late because
+        a detector kernel held its slot does not end the launch late), the detector on another sibling.
+        With the exact delta the detector does not need the spectrogram, so after the delta (the
+        caller's context) the two run side by side: the detector's latency-bound kernels and host
+        round trips under the spectrogram.  The caller's context is not changed.  0: one stream,
+        in order."""
         self.ctx, self.fs, self.N = ctx, fs, int(nperseg)
         self.hop = self.N - int(noverlap)
         self.block_sec = self.hop / fs
@@ -190,15 +191,14 @@ class IQShardDetector(_stream.CertifyingShard):
         nb = (self.chunk - 1) * self.hop + self.N if self.chunk else max(self.s1 - self.s0, 1)
         self.overlap = int(overlap)
         if self.overlap < 0:
-            raise ValueError("overlap must be >= 0 (CUs for the detector)")
+            raise ValueError("overlap must be >= 0 (workgroup slots left to the detector)")
         self.sctx = self.dctx = ctx  # the spectrogram's and the detector's contexts
         self.plan = None
         self.batch = None
         try:
             if self.overlap > 0:
                 self.sctx, self.dctx = ctx.sibling(), ctx.sibling()
-                self.sctx.set_option(_lib.OPT_STREAM_CUS, -self.overlap)
-                self.dctx.set_option(_lib.OPT_STREAM_CUS, self.overlap)
+                self.sctx.set_option(_lib.OPT_CSTFT_RESERVE, self.overlap)
             self._init(ctx, fs, noverlap, freq_band, noise_band, threshold_std_factor, nb, dtype, delta,
                        seg_len, certify, Fa, Fb)
         except BaseException:

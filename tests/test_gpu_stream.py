@@ -680,8 +680,8 @@ def test_overlapped_detector_matches_in_order(chunk):
 
 
 def test_overlap_leaves_the_callers_context():
-    """the CU split lives on two sibling contexts: the caller's context keeps its options (ADVICE r4:
-    a context-wide option changed by the detector), also when the constructor fails"""
+    """the overlap's spectrogram reserve lives on a sibling context: the caller's context keeps its
+    options (a context-wide option changed by the detector), also when the constructor fails"""
     from meteorgpu import _lib, iq
     ctx = _lib.Context(0)
     try:
@@ -690,7 +690,7 @@ def test_overlap_leaves_the_callers_context():
         det = iq.IQShardDetector(ctx, 192000 * 5, 192000, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
                                  5, 3, 2, 1, overlap=16)
         assert det.sctx is not ctx and det.dctx is not ctx
-        assert det.sctx.options[_lib.OPT_STREAM_CUS] == -16 and det.dctx.options[_lib.OPT_STREAM_CUS] == 16
+        assert det.sctx.options[_lib.OPT_CSTFT_RESERVE] == 16
         det.close()
         assert ctx.options == before
         with pytest.raises(_lib.MsdError):  # the stream plan refuses seg_len 100 (not a multiple of 64)
@@ -699,3 +699,43 @@ def test_overlap_leaves_the_callers_context():
         assert ctx.options == before
     finally:
         ctx.close()
+
+
+def test_overlapped_certified_ranks_match_one_process():
+    """the overlap at world > 1: 3 rank-threads, each with its detector beside its spectrogram (8
+    workgroup slots reserved, the chunked spectrogram) and the exact delta, exchange halos, chunk sums,
+    states, runs and the certificate through the thread allgather -- the detections, dB values and
+    certificate of one in-order process over the whole stream"""
+    from meteorgpu import _lib, iq, synth
+    fs = 192000
+    i, q, _ = synth.synth_iq(31, fs, 40.0, 1000.0, rate_per_min=20)
+    buf, _ = iq.interleave(i, q)
+    kw = dict(threshold_estimation_window_sec=5, threshold_freeze_after_detection_sec=2,
+              threshold_fixed_init_duration_sec=1)
+
+    def run(world, ov):
+        def body(r, comm):
+            ctx = _lib.Context(0)
+            try:
+                det = iq.IQShardDetector(ctx, i.size, fs, 4096, 3072, (950, 1050), (-3050, -2950), 4.0, True,
+                                         rank=r, world=world, overlap=ov, **kw)
+                try:
+                    assert det.exact_delta
+                    det.upload(buf[2 * det.s0: 2 * det.s1])
+                    res = None
+                    for _ in range(2):  # a second step on the same buffers (the step-to-step ordering)
+                        det.spectrogram_and_delta()
+                        res = det.detect(comm, thresholds=False)
+                    return res
+                finally:
+                    det.close()
+            finally:
+                ctx.close()
+        return run_threads(world, body)
+
+    one = run(1, 0)[0]
+    assert one.certified and len(one.detections) > 5
+    for r in run(3, 8):
+        assert r.certified
+        assert np.array_equal(r.detections, one.detections)
+        assert r.thr0 == one.thr0

@@ -224,3 +224,46 @@ def test_large_dc_float32():
     _, _, R = Q.spectrogram_iq_ref(i, q, 192000, 4096, 3072)
     assert _frame_rel(S, R) < SPEC_TOL
     assert _dc_bins_rel(S, R) < SPEC_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["int16", "float32"])
+def test_chunked_schedule_matches_static(kind):
+    """MSD_OPT_CSTFT_RESERVE > 0: the C5 kernel's workgroups draw chunks of frames from the guided
+    schedule (cstft.hip DYN) -- the spectrogram, the energy partials and the given-sums variant are
+    bit-identical to the fixed-range launch, over several streams of different lengths"""
+    from meteorgpu import _lib, iq
+    from meteorgpu.dsp import context
+    rng = np.random.default_rng(5)
+    n = 700_000
+    dt = np.int16 if kind == "int16" else np.float32
+    xs = []
+    for s in range(3):
+        z = rng.integers(-3000, 3000, 2 * n) + (500 if s == 1 else 0)
+        xs.append(z.astype(np.int16) if kind == "int16" else (z / 32768).astype(np.float32))
+    lens = [n, n - 123_457, 300_000]
+    out = {}
+    base = context(0)
+    for reserve in (0, 8):
+        ctx = base.sibling()
+        try:
+            if reserve:
+                ctx.set_option(_lib.OPT_CSTFT_RESERVE, reserve)
+            b = iq.IQBatch(ctx, 3, n, 192000, 4096, 3072, dtype=dt)
+            for s in range(3):
+                b.upload(s, xs[s])
+            b.d_len.upload(np.array(lens, np.int64))
+            T = b.T
+            etot = ctx.alloc(16 * 4 * ctx.lib.msd_cstft_energy_stride(3, T))
+            b.run(etot)
+            spec = np.empty((3, T, 4096), np.float32)
+            b.d_out.download(spec)
+            e = np.empty(16 * ctx.lib.msd_cstft_energy_stride(3, T), np.float32)
+            etot.download(e)
+            out[reserve] = (spec, e)
+            etot.free()
+            b.close()
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(out[0][0], out[8][0])
+    np.testing.assert_array_equal(out[0][1], out[8][1])
