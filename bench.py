@@ -74,11 +74,11 @@ def parse():
                          "flag = the same certified, uncertain decisions reported; refine = flag + the uncertain "
                          "ones and every detection's frames recomputed in float64 (round 3's certified path); "
                          "all = the line on 'exact', plus the other modes timed under \"modes\"")
-    ap.add_argument("--c5-overlap", type=int, default=0,
+    ap.add_argument("--c5-overlap", type=int, default=32,
                     help="C5: run the stream detector beside the spectrogram after the delta step, the "
                          "spectrogram leaving this many workgroup slots free (its workgroups then take chunks of "
                          "frames from a guided schedule; exact delta only: the detector does not read the "
-                         "spectrogram); 0 = one stream, in order")
+                         "spectrogram; default 32 of ~1000); 0 = one stream, in order")
     ap.add_argument("--shard-day", action="store_true",
                     help="C4 as strong scaling: ONE day of --files files sharded over the ranks (contiguous "
                          "shard_range slices; the per-hour counts all-reduce into that day's 24 buckets) instead "

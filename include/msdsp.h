@@ -81,12 +81,20 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
  * MSD_OPT_STREAM_CUS = n → the context's stream is re-created on a subset of the device's CUs
  * (hipExtStreamCreateWithCUMask): n > 0 the first n CUs, n < 0 all but those |n| -- two contexts
  * set to n and -n split the chip into disjoint parts --, 0 all CUs again; persistent grids are
- * sized for the CUs the stream may use.  Synchronises the context's stream first. */
+ * sized for the CUs the stream may use.  Synchronises the context's stream first.
+ * MSD_OPT_CSTFT_SCHED = 0 / 1 / 2 → how the persistent C5 spectrogram kernel (hop 1024) splits the
+ * frames over its workgroups: 0 (default) and 2 chunks drawn from a guided schedule by an atomic
+ * ticket; 1 one fixed range per workgroup (round-4 behaviour, A/B).  Same output either way.
+ * (MSD_CSTFT_SCHED=static|chunked in the environment sets the default of new contexts, for A/B.)
+ * MSD_OPT_STFT_SCHED = 0 / 1 / 2 → the same choice for stft1024_kernel's 32-frame tiles (the C3
+ * spectrogram): 0 (default) and 1 fixed ranges, 2 chunks (MSD_STFT_SCHED=static|chunked). */
 #define MSD_OPT_GENERIC_STFT 1
 #define MSD_OPT_FRESH_ALL 2
 #define MSD_OPT_REFINE_GOERTZEL 3
 #define MSD_OPT_CSTFT_RESERVE 4
 #define MSD_OPT_STREAM_CUS 5
+#define MSD_OPT_CSTFT_SCHED 6
+#define MSD_OPT_STFT_SCHED 7
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <map>
@@ -161,6 +162,10 @@ int msd_create(int device, msd_ctx **out) {
         c->num_cu <= 0)
         c->num_cu = 256;  // grid sizing only: a wrong count costs balance, not correctness
     c->num_cu_dev = c->num_cu;
+    if (const char *e = getenv("MSD_CSTFT_SCHED"))  // A/B runs: static | chunked (MSD_OPT_CSTFT_SCHED)
+        c->cstft_sched = !strcmp(e, "static") ? 1 : !strcmp(e, "chunked") ? 2 : 0;
+    if (const char *e = getenv("MSD_STFT_SCHED"))  // the same for stft1024_kernel (MSD_OPT_STFT_SCHED)
+        c->stft_sched = !strcmp(e, "static") ? 1 : !strcmp(e, "chunked") ? 2 : 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -254,6 +259,14 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
         case MSD_OPT_CSTFT_RESERVE:
             if (value < 0) return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_CSTFT_RESERVE must be >= 0");
             ctx->cstft_reserve = value;
+            return MSD_OK;
+        case MSD_OPT_CSTFT_SCHED:
+            if (value < 0 || value > 2) return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_CSTFT_SCHED is 0, 1 or 2");
+            ctx->cstft_sched = value;
+            return MSD_OK;
+        case MSD_OPT_STFT_SCHED:
+            if (value < 0 || value > 2) return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_STFT_SCHED is 0, 1 or 2");
+            ctx->stft_sched = value;
             return MSD_OK;
         case MSD_OPT_STREAM_CUS: {
             // the context's stream re-created on a CU subset: n > 0 the first n CUs of the mask, n < 0
@@ -451,6 +464,8 @@ void msd_stft_plan_destroy(msd_stft_plan *p) {
     hipFree(p->d_window64);
     hipFree(p->d_tw64);
     hipFree(p->d_post64);
+    if (p->d_sched) hipFree(p->d_sched);
+    if (p->d_ticket) hipFree(p->d_ticket);
     delete p;
 }
 

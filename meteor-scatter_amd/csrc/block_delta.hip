@@ -305,7 +305,7 @@ int launch_bd2(msd_block_plan *p, const void *x, const int64_t *off, const int64
         p->energy_cap = (size_t)blocks;
     }
     // persistent grid: a few workgroups per CU, each walking groups of 16 blocks (4 resident per CU;
-    // C3 A/B over two boxes, tools/gpu_r4s.sh: 4 per CU 0.409 ms, 8 0.381-0.393, 16 0.372-0.383,
+    // C3 A/B over two boxes, profiles/r4_bd2_grid_ab.txt: 4 per CU 0.409 ms, 8 0.381-0.393, 16 0.372-0.383,
     // 32 0.382, one per group 0.398)
     const int64_t grid = std::min<int64_t>((blocks + BD2_GROUPS - 1) / BD2_GROUPS, (int64_t)p->ctx->num_cu * 16);
     const size_t lds = sizeof(double) * (16 * bd2_pitch(SPL) + BD2_GROUPS * (size_t)(p->nbins > 0 ? p->nbins : 1));

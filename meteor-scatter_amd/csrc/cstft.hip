@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "msd_internal.h"
@@ -178,11 +180,13 @@ struct CsTune {
 // PD 0: the sums in the kernel (exact integer DPP sums per wave, one LDS slot per wave, a barrier);
 // PD 2 (msd_cstft_psd_fsums_dev): the frames' sums given (fsum[g], the exact delta step's): no
 // reduction and no barrier before pass 1, the next frame's sums prefetched with its samples.
-// DYN (C5's hop, with MSD_OPT_CSTFT_RESERVE > 0): the workgroups take chunks of frames from a
-// guided schedule (sched[k] .. sched[k + 1], sizes falling from ~total / (2 wgs) to 16 frames) by an
-// atomic ticket instead of one fixed range each.  With a fixed range a workgroup that starts late --
-// because kernels on another stream (the C5 detector beside the spectrogram) held its slot when the
-// grid was dispatched -- ends the launch late by the whole delay; with chunks the others take its share.
+// DYN (C5's hop, the default): the workgroups take chunks of frames from a guided schedule (sched[k] ..
+// sched[k + 1], sizes falling from ~total / (4 wgs) to 16 frames) by an atomic ticket instead of one
+// fixed range each.  With fixed ranges the slowest workgroup sets the launch's end -- one on a slower
+// CU, or one that started late because kernels on another stream (the C5 detector beside the
+// spectrogram) held its slot when the grid was dispatched; with chunks the others take its share.
+// Measured: 11.79 -> 10.62 ms alone, 10.35 ms beside the detector (bench C5, one box; chunks of 1 / (2
+// wgs) of the rest), 9.73-9.81 ms with 1 / (4 wgs).
 template <typename T, int SH, bool EN, int PD, bool DYN = false>
 __global__ __launch_bounds__(CS_T, (CsTune<T, SH>::kWavesPerSimd)) void cstft4096_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len, int64_t nstreams,
@@ -513,9 +517,19 @@ int msd_cstft_psd_fsums_dev(msd_cstft_plan *p, const void *x, int dtype, const i
         const int64_t wgs = grid(kern);
         if (p->sched_total != total || p->sched_wgs != wgs) {
             std::vector<int64_t> st(1, 0);
+            // guided: each chunk 1 / (div * wgs) of what is left, at least cmin frames (A/B knobs:
+            // MSD_CSTFT_GUIDE="cmin,div"; bench C5 on one box, profiles/r5_c5_sched_overlap.txt: div 1
+            // 13.06 ms, 2 10.19, 4 9.73-9.81, 8 9.81, 16 9.88; fixed 16 / 32 / 64 / 128-frame chunks
+            // 9.95 / 9.91 / 9.94 / 10.02 -- the workgroups working on nearby frames, not only the
+            // balance, pays)
+            int64_t cmin = 16, div = 4;
+            if (const char *e = getenv("MSD_CSTFT_GUIDE")) {
+                long a = 0, b = 0;
+                if (sscanf(e, "%ld,%ld", &a, &b) == 2 && a >= 4 && b >= 1) cmin = a, div = b;
+            }
             for (int64_t pos = 0; pos < total;) {
-                int64_t sz = (total - pos) / (2 * wgs);
-                sz = (std::max<int64_t>(sz, 16) + 3) / 4 * 4;
+                int64_t sz = (total - pos) / (div * wgs);
+                sz = (std::max<int64_t>(sz, cmin) + 3) / 4 * 4;
                 pos = std::min(total, pos + sz);
                 st.push_back(pos);
             }
@@ -546,8 +560,10 @@ int msd_cstft_psd_fsums_dev(msd_cstft_plan *p, const void *x, int dtype, const i
     // the given sums (PD 2) at C5's hop: the int16 exact delta step leaves them (frames that start
     // every 1024 samples); other hops compute their own
     const bool given = fsum && p->detrend && sh == 4;
-    // the chunked kernels where a reserve makes room for another stream's kernels (C5's hop)
-    const bool dyn = p->ctx->cstft_reserve > 0;
+    // the chunked kernels at C5's hop unless MSD_OPT_CSTFT_SCHED asks for fixed ranges: they balance
+    // the workgroups' unequal speeds as well as late starts (A/B on one box, bench C5 exact mode:
+    // 11.79 -> 10.62 ms for the kernel alone, profiles/r5_c5_sched_overlap.txt)
+    const bool dyn = p->ctx->cstft_sched != 1;
     auto by_shift = [&](auto en, const auto *xp) -> int {
         constexpr bool EN = decltype(en)::value;
         using T = std::remove_cv_t<std::remove_pointer_t<decltype(xp)>>;

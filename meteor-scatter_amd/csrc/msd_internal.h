@@ -71,6 +71,8 @@ struct msd_ctx {
     int i8_km[16] = {};
     bool refine_goertzel = false;  // MSD_OPT_REFINE_GOERTZEL: int16 refinement on the float64 Goertzel
     int cstft_reserve = 0;         // MSD_OPT_CSTFT_RESERVE: workgroup slots the C5 spectrogram leaves free
+    int cstft_sched = 0;           // MSD_OPT_CSTFT_SCHED: 0 / 2 chunks from a guided schedule, 1 fixed ranges
+    int stft_sched = 0;            // MSD_OPT_STFT_SCHED: the same for stft1024_kernel (tiles)
     int num_cu_dev = 0;            // the device's CUs (num_cu: those the stream may use, MSD_OPT_STREAM_CUS)
     int stream_cus = 0;            // MSD_OPT_STREAM_CUS value in force
 };
@@ -102,6 +104,10 @@ struct msd_stft_plan {
     double *d_window64 = nullptr;  // the same three in float64 (MSD_F64 plans)
     double2 *d_tw64 = nullptr;
     double2 *d_post64 = nullptr;
+    // stft1024_kernel's guided tile schedule (chunked, MSD_OPT_STFT_SCHED) and its ticket
+    int64_t *d_sched = nullptr;
+    int64_t sched_cap = 0, sched_total = -1, sched_wgs = -1, sched_n = 0;
+    unsigned long long *d_ticket = nullptr;
 };
 
 struct msd_block_plan {

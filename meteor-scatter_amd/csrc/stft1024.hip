@@ -21,6 +21,10 @@
 // persistent and walk a contiguous range of tiles (the half frame shared by
 // neighbouring tiles is re-read from L2); each wave loads its next tile's frame pair
 // into the sample registers as soon as the current pair is windowed.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "msd_internal.h"
 
 #include <cmath>
@@ -226,12 +230,17 @@ __device__ __forceinline__ void lane01_fix(float &m0, float &m1, float &m2, floa
 }
 
 // WIDE: 64-bit output offsets (files of 2^20 frames and more); SH: hop 512 with integer samples
-template <typename T, int WIDE, bool SH>
+// DYN: the workgroups take chunks of consecutive tiles from a guided schedule (sched[k] .. sched[k+1],
+// at least 2 tiles) by an atomic ticket instead of one fixed range each (as cstft4096_kernel, where it
+// balances the workgroups' unequal speeds); the next chunk's ticket is drawn when a chunk starts and
+// read at its last tile, at least one tile barrier later.
+template <typename T, int WIDE, bool SH, bool DYN = false>
 __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const T *__restrict__ x, const int64_t *__restrict__ off, const int64_t *__restrict__ len,
     int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float wscale, int detrend,
     const float *__restrict__ g_win, const float2 *__restrict__ g_tw, const float2 *__restrict__ g_post,
-    float *__restrict__ out, int64_t ld) {
+    float *__restrict__ out, int64_t ld, const int64_t *__restrict__ sched, int64_t nchunks,
+    unsigned long long *__restrict__ ticket) {
     using IO = PairIO<T>;
     using raw_t = typename IO::raw_t;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -263,9 +272,23 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     const int pi = pi_of(l);
     __syncthreads();
 
-    const int64_t tb = (int64_t)blockIdx.x * tiles_per_wg;
-    const int64_t te = tb + tiles_per_wg < ntiles ? tb + tiles_per_wg : ntiles;
-    if (tb >= te) return;
+    __shared__ int64_t slot[2];  // DYN: drawn chunk tickets
+    int64_t tb, te;              // the current range of tiles
+    int par = 0;
+    if constexpr (DYN) {
+        if (tid == 0) slot[0] = (int64_t)atomicAdd(ticket, 1ull);
+        __syncthreads();
+        const int64_t k = uniform_i64(slot[0]);
+        if (k >= nchunks) return;
+        tb = uniform_i64(sched[k]);
+        te = uniform_i64(sched[k + 1]);
+        if (tid == 0) slot[1] = (int64_t)atomicAdd(ticket, 1ull);  // the chunk after
+        par = 1;
+    } else {
+        tb = (int64_t)blockIdx.x * tiles_per_wg;
+        te = tb + tiles_per_wg < ntiles ? tb + tiles_per_wg : ntiles;
+        if (tb >= te) return;
+    }
     auto file_at = [&](int64_t f, int64_t ti) {
         FileCur c;
         c.f = f;
@@ -326,9 +349,21 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     bool have_prev = false;
     const float hs = vgpr_f(0.70710678118654752440f);  // sqrt(1/2) of the DFT8s, in a VGPR
 
-    for (int64_t tl = tb; tl < te; ++tl) {
-        const bool has_next = tl + 1 < te;
-        const FileCur nxt = has_next ? advance(cur) : cur;
+    for (int64_t tl = tb;;) {
+        // the next tile: the next of this range, else (DYN) the first of the next drawn chunk
+        bool has_next = tl + 1 < te, jump = false;
+        int64_t ntl = tl + 1, nte = te;
+        if constexpr (DYN) {
+            if (!has_next) {
+                const int64_t k2 = uniform_i64(slot[par]);
+                if (k2 < nchunks) {
+                    has_next = jump = true;
+                    ntl = uniform_i64(sched[k2]);
+                    nte = uniform_i64(sched[k2 + 1]);
+                }
+            }
+        }
+        const FileCur nxt = !has_next ? cur : jump ? file_at(ntl / tiles_per_file, ntl % tiles_per_file) : advance(cur);
         const bool b_cur = b_ok;
         float2 v[2][8], wv[8];
         // ---- detrend (consumes raw); the window is applied inside pass 1
@@ -538,6 +573,15 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         prev = cur;
         have_prev = true;
         cur = nxt;
+        if (!has_next) break;
+        if constexpr (DYN) {
+            if (jump) {  // into the next chunk: draw the one after it
+                par ^= 1;
+                if (tid == 0) slot[par] = (int64_t)atomicAdd(ticket, 1ull);
+            }
+        }
+        tl = ntl;
+        te = nte;
     }
     write_out(prev, std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});  // the last tile (complete since the loop's final barrier)
 }
@@ -555,11 +599,51 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
     const int64_t ntiles = tiles_per_file * nfiles;
     int64_t wgs = cus;  // one 16-wave workgroup per CU (LDS-bound residency)
     if (wgs > ntiles) wgs = ntiles;
+    const float ws = static_cast<float>(std::sqrt(p->scale * 0.5));
+    if (p->ctx->stft_sched == 2) {
+        // guided schedule of tile chunks (>= 2 tiles), rebuilt when (ntiles, wgs) change
+        auto dkern = wide ? (sh ? stft1024_kernel<T, 1, PairIO<T>::kInt, true> : stft1024_kernel<T, 1, false, true>)
+                          : (sh ? stft1024_kernel<T, 0, PairIO<T>::kInt, true> : stft1024_kernel<T, 0, false, true>);
+        if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(dkern), F_LDS)) return rc;
+        if (p->sched_total != ntiles || p->sched_wgs != wgs) {
+            int64_t cmin = 2, div = 2;  // A/B knobs: MSD_STFT_GUIDE="cmin,div" (tiles)
+            if (const char *e = getenv("MSD_STFT_GUIDE")) {
+                long a = 0, b = 0;
+                if (sscanf(e, "%ld,%ld", &a, &b) == 2 && a >= 2 && b >= 1) cmin = a, div = b;
+            }
+            std::vector<int64_t> st(1, 0);
+            for (int64_t pos = 0; pos < ntiles;) {
+                const int64_t sz = std::max<int64_t>((ntiles - pos) / (div * wgs), cmin);
+                pos = std::min(ntiles, pos + sz);
+                if (ntiles - pos > 0 && ntiles - pos < cmin) pos = ntiles;  // no chunk below cmin at the end
+                st.push_back(pos);
+            }
+            MSD_HIP(hipStreamSynchronize(p->ctx->stream));
+            if ((int64_t)st.size() > p->sched_cap) {
+                if (p->d_sched) MSD_HIP(hipFree(p->d_sched));
+                p->d_sched = nullptr;
+                p->sched_cap = 0;
+                MSD_HIP(hipMalloc(&p->d_sched, sizeof(int64_t) * st.size()));
+                p->sched_cap = (int64_t)st.size();
+            }
+            if (!p->d_ticket) MSD_HIP(hipMalloc(&p->d_ticket, sizeof(unsigned long long)));
+            MSD_HIP(hipMemcpy(p->d_sched, st.data(), sizeof(int64_t) * st.size(), hipMemcpyHostToDevice));
+            p->sched_total = ntiles;
+            p->sched_wgs = wgs;
+            p->sched_n = (int64_t)st.size() - 1;
+        }
+        MSD_HIP(hipMemsetAsync(p->d_ticket, 0, sizeof(unsigned long long), p->ctx->stream));
+        hipLaunchKernelGGL(dkern, dim3((unsigned)wgs), dim3(F_NW * 64), F_LDS, p->ctx->stream, static_cast<const T *>(x),
+                           off, len, tiles_per_file, ntiles, (int64_t)0, p->hop, ws, p->detrend, p->d_window, p->d_tw,
+                           p->d_post, out, ld, p->d_sched, p->sched_n, p->d_ticket);
+        MSD_HIP(hipGetLastError());
+        return MSD_OK;
+    }
     const int64_t per = (ntiles + wgs - 1) / wgs;
     wgs = (ntiles + per - 1) / per;
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(F_NW * 64), F_LDS, p->ctx->stream, static_cast<const T *>(x),
-                       off, len, tiles_per_file, ntiles, per, p->hop, static_cast<float>(std::sqrt(p->scale * 0.5)), p->detrend,
-                       p->d_window, p->d_tw, p->d_post, out, ld);
+                       off, len, tiles_per_file, ntiles, per, p->hop, ws, p->detrend, p->d_window, p->d_tw, p->d_post,
+                       out, ld, nullptr, (int64_t)0, nullptr);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }

@@ -41,6 +41,8 @@ OPT_FRESH_ALL = 2
 OPT_REFINE_GOERTZEL = 3
 OPT_CSTFT_RESERVE = 4
 OPT_STREAM_CUS = 5
+OPT_CSTFT_SCHED = 6
+OPT_STFT_SCHED = 7
 COMM_ID_BYTES = 128
 
 

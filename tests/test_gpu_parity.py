@@ -612,3 +612,45 @@ def test_stft_fast_path_wide_row_stride():
     tail = np.empty(64, np.float32)
     d_spec.download(tail, byte_offset=(512 * ld + ld - 64) * 4)
     assert not tail.any()
+
+
+@pytest.mark.parametrize("hop_case", ["c3", "h768"])
+def test_stft1024_chunked_schedule_identical(hop_case):
+    """MSD_OPT_STFT_SCHED = 2: stft1024_kernel's workgroups draw chunks of consecutive tiles from a
+    guided schedule (ticket) instead of one fixed range each -- the spectrogram is bit-identical over a
+    batch of 40 files of different lengths, repeated launches (the ticket is reset per launch)"""
+    from meteorgpu import _lib
+    base = dsp.context(0)
+    rng = np.random.default_rng(8)
+    fs, n, F = 48000, 48000 * 20, 40
+    hop = 512 if hop_case == "c3" else 768  # the shared-half pair (SH) and the plain one
+    xs = [rng.integers(-6000, 6000, n).astype(np.int16) for _ in range(F)]
+    lens = [n - (i * 7919) % 200_000 for i in range(F)]
+    out = {}
+    for sched in (1, 2):
+        ctx = base.sibling()
+        try:
+            ctx.set_option(_lib.OPT_STFT_SCHED, sched)
+            w = dsp.hann_periodic(1024).astype(np.float32)
+            plan = _lib.StftPlan(ctx, 1024, hop, w, float(1.0 / (fs * (w.astype(np.float64) ** 2).sum())))
+            T = (n - 1024) // hop + 1
+            ld = (T + 31) // 32 * 32
+            d_x, d_off, d_len = ctx.alloc(2 * F * n), ctx.alloc(8 * F), ctx.alloc(8 * F)
+            d_x.upload(np.concatenate(xs))
+            d_off.upload(np.arange(F, dtype=np.int64) * n)
+            d_len.upload(np.array(lens, np.int64))
+            d_out = ctx.alloc(4 * F * 513 * ld)
+            res = []
+            for _ in range(2):
+                plan.run_dev(d_x, np.int16, d_off, d_len, F, T, d_out, ld)
+                S = np.empty((F, 513, ld), np.float32)
+                d_out.download(S)
+                res.append(S)
+            np.testing.assert_array_equal(res[0], res[1])
+            out[sched] = res[0]
+            for b in (d_x, d_off, d_len, d_out):
+                b.free()
+            plan.close()
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(out[1], out[2])
