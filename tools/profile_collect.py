@@ -26,8 +26,8 @@ for wl, suffix in (("", ""), ("_live", "_live"), ("_c5", "_c5"), ("_c5x", "_c5_e
         continue
     shutil.copy(f"{src}/kt{wl}/kt_kernel_stats.csv", f"{dst}/{tag}_kernel_stats{suffix}.csv")
     json.dump(last_json(f"{src}/kt{wl}.log"), open(f"{dst}/{tag}_bench{suffix}_under_rocprof.json", "w"))
-for sub, name, kernel, match in ((tag, "stft", "stft1024_kernel<short, 0, true>", {"files": 1440, "nperseg": 1024}),
-                                 (f"{tag}_c5", "cstft", "cstft4096_kernel<short, 4, false, 2>", None),
+for sub, name, kernel, match in ((tag, "stft", "stft1024_kernel<short, 0, true, false>", {"files": 1440, "nperseg": 1024}),
+                                 (f"{tag}_c5", "cstft", "cstft4096_kernel<short, 4, false, 2, true>", None),
                                  (f"{tag}_c5det", None, None, None), (f"{tag}_c5i8", None, None, None)):
     if not os.path.isdir(f"{pmc}/{sub}"):
         continue
