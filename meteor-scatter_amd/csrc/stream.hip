@@ -1122,7 +1122,10 @@ __global__ void propagate_kernel(SState *__restrict__ in_state, const SState *__
 
 // compaction: runs of segment s go to out[pos_s ..]; a continued first run of s >= 1 extends the
 // last run of s-1 (or the run that one continues) instead.  One workgroup.
-__global__ __launch_bounds__(1024) void runs_kernel(const msd_det *__restrict__ runs,
+// 256 threads (was 1024): beside the persistent spectrogram (IQShardDetector overlap) a 16-wave
+// workgroup found no CU with room until the spectrogram's last workgroups left (1.3 ms in the trace)
+constexpr int RK_T = 256;
+__global__ __launch_bounds__(RK_T) void runs_kernel(const msd_det *__restrict__ runs,
                                                     const int32_t *__restrict__ nruns, int64_t nseg, int64_t cap,
                                                     msd_det *__restrict__ out, int64_t *__restrict__ count,
                                                     int64_t *__restrict__ seg_pos) {
@@ -1130,7 +1133,7 @@ __global__ __launch_bounds__(1024) void runs_kernel(const msd_det *__restrict__ 
     const int tid = threadIdx.x;
     if (tid == 0) s_base = 0;
     __syncthreads();
-    for (int64_t c0 = 0; c0 < nseg; c0 += 1024) {
+    for (int64_t c0 = 0; c0 < nseg; c0 += RK_T) {
         const int64_t s = c0 + tid;
         int64_t e = 0;
         bool cont = false;
@@ -1140,10 +1143,10 @@ __global__ __launch_bounds__(1024) void runs_kernel(const msd_det *__restrict__ 
             e = n - (cont ? 1 : 0);
         }
         // block-wide inclusive scan of e (Hillis-Steele in LDS)
-        __shared__ int64_t sc[1024];
+        __shared__ int64_t sc[RK_T];
         sc[tid] = e;
         __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
+        for (int o = 1; o < RK_T; o <<= 1) {
             const int64_t v = tid >= o ? sc[tid - o] : 0;
             __syncthreads();
             sc[tid] += v;
@@ -1156,13 +1159,13 @@ __global__ __launch_bounds__(1024) void runs_kernel(const msd_det *__restrict__ 
             for (int64_t r = cont ? 1 : 0; r < n; ++r) out[pos + r - (cont ? 1 : 0)] = runs[s * cap + r];
         }
         __syncthreads();
-        if (tid == 1023) s_base += sc[1023];
+        if (tid == RK_T - 1) s_base += sc[RK_T - 1];
         __syncthreads();
     }
     if (tid == 0) *count = s_base;
     __syncthreads();
     // continued runs: the owner is the last emitted run before this segment
-    for (int64_t s = 1 + tid; s < nseg; s += 1024) {
+    for (int64_t s = 1 + tid; s < nseg; s += RK_T) {
         const int64_t n = nruns[s];
         if (n == 0 || runs[s * cap].start >= 0) continue;
         const int64_t before = seg_pos[s];  // runs emitted by the segments before s
@@ -1711,7 +1714,7 @@ int msd_stream_runs(msd_stream_plan *p, msd_det *runs, int64_t cap, int64_t *cou
     if (!p->scanned) return fail(MSD_ERR_INVALID, "msd_stream_runs: call msd_stream_scan first");
     DeviceGuard g(p->ctx->device);
     hipStream_t st = p->ctx->stream;
-    hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(1024), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
+    hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(RK_T), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
                        p->d_count, p->d_pos);
     MSD_HIP(hipGetLastError());
     MSD_HIP(hipMemcpyAsync(&pin_hdr(p)->count, p->d_count, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -1820,7 +1823,7 @@ int msd_stream_detect_local(msd_stream_plan *p, int32_t exact_thresholds, msd_de
     // runs of the shard, compacted on the device
     DeviceGuard g(p->ctx->device);
     hipStream_t st = p->ctx->stream;
-    hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(1024), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
+    hipLaunchKernelGGL(runs_kernel, dim3(1), dim3(RK_T), 0, st, p->d_runs, p->d_nruns, p->nseg, p->cap, p->d_out,
                        p->d_count, p->d_pos);
     MSD_HIP(hipGetLastError());
     MSD_HIP(hipMemcpyAsync(&pin_hdr(p)->count, p->d_count, sizeof(int64_t), hipMemcpyDeviceToHost, st));
