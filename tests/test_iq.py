@@ -266,4 +266,12 @@ def test_chunked_schedule_matches_static(kind):
         finally:
             ctx.close()
     np.testing.assert_array_equal(out[0][0], out[8][0])
-    np.testing.assert_array_equal(out[0][1], out[8][1])
+    # the energy partials are written for each stream's frames (not for the zero frames past a shorter
+    # stream's end): compare those
+    T = out[0][0].shape[1]
+    valid = np.zeros(out[0][1].size // 16, bool)
+    for s_, ln in enumerate(lens):
+        nf = (ln - 4096) // 1024 + 1 if ln >= 4096 else 0
+        valid[s_ * T: s_ * T + nf] = True
+    e0, e8 = out[0][1].reshape(16, -1), out[8][1].reshape(16, -1)
+    np.testing.assert_array_equal(e0[:, valid], e8[:, valid])
