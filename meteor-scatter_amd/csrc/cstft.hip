@@ -85,7 +85,10 @@ struct IQ;
 template <>
 struct IQ<int16_t> {  // interleaved int16 I, Q
     using raw_t = uint32_t;
-    __device__ static raw_t load(const int16_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+    // non-temporal: 9.78 vs 9.86 ms for the C5 step's spectrogram (profiles/r5_cstft_nt_ab.txt)
+    __device__ static raw_t load(const int16_t *p) {
+        return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p));
+    }
     __device__ static int re_i(raw_t r) { return (int)(int16_t)(r & 0xffffu); }
     __device__ static int im_i(raw_t r) { return (int)(int16_t)(r >> 16); }
     __device__ static float2 f(raw_t r) { return make_float2(cvt_i16_lo(r), cvt_i16_hi(r)); }
