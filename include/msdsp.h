@@ -87,7 +87,12 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
  * ticket; 1 one fixed range per workgroup (round-4 behaviour, A/B).  Same output either way.
  * (MSD_CSTFT_SCHED=static|chunked in the environment sets the default of new contexts, for A/B.)
  * MSD_OPT_STFT_SCHED = 0 / 1 / 2 → the same choice for stft1024_kernel's 32-frame tiles (the C3
- * spectrogram): 0 (default) and 1 fixed ranges, 2 chunks (MSD_STFT_SCHED=static|chunked). */
+ * spectrogram): 0 (default) and 1 fixed ranges, 2 chunks (MSD_STFT_SCHED=static|chunked).
+ * MSD_OPT_BLOCK_GOERTZEL = 1 → msd_block_delta[_dev] computes int16 blocks with the float64
+ * Goertzel kernel instead of the exact int8-MFMA one (plans with min(block_size, n_fft) = 256,
+ * 512 or 1024 and at most 8 band + noise bins take the latter by default; A/B, both within the
+ * near-tie bound of meteorgpu/margin.py; MSD_BLOCK_GOERTZEL=1 in the environment sets it for new
+ * contexts). */
 #define MSD_OPT_GENERIC_STFT 1
 #define MSD_OPT_FRESH_ALL 2
 #define MSD_OPT_REFINE_GOERTZEL 3
@@ -95,6 +100,7 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
 #define MSD_OPT_STREAM_CUS 5
 #define MSD_OPT_CSTFT_SCHED 6
 #define MSD_OPT_STFT_SCHED 7
+#define MSD_OPT_BLOCK_GOERTZEL 8
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.

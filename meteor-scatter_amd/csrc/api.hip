@@ -166,6 +166,8 @@ int msd_create(int device, msd_ctx **out) {
         c->cstft_sched = !strcmp(e, "static") ? 1 : !strcmp(e, "chunked") ? 2 : 0;
     if (const char *e = getenv("MSD_STFT_SCHED"))  // the same for stft1024_kernel (MSD_OPT_STFT_SCHED)
         c->stft_sched = !strcmp(e, "static") ? 1 : !strcmp(e, "chunked") ? 2 : 0;
+    if (const char *e = getenv("MSD_BLOCK_GOERTZEL"))  // A/B runs: MSD_OPT_BLOCK_GOERTZEL
+        c->block_goertzel = atoi(e) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -256,6 +258,7 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
         case MSD_OPT_GENERIC_STFT: ctx->force_generic = value != 0; return MSD_OK;
         case MSD_OPT_FRESH_ALL: ctx->fresh_all = value != 0; return MSD_OK;
         case MSD_OPT_REFINE_GOERTZEL: ctx->refine_goertzel = value != 0; return MSD_OK;
+        case MSD_OPT_BLOCK_GOERTZEL: ctx->block_goertzel = value != 0; return MSD_OK;
         case MSD_OPT_CSTFT_RESERVE:
             if (value < 0) return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_CSTFT_RESERVE must be >= 0");
             ctx->cstft_reserve = value;
@@ -583,6 +586,12 @@ int msd_block_plan_create(msd_ctx *ctx, int64_t block_size, int32_t nfft, const 
         msd_block_plan_destroy(p);
         return hip_fail(e, "block plan upload");
     }
+    if (block_i8_shape(L, p->nbins)) {  // int16 blocks on the matrix cores (block_i8.hip)
+        if (int rc = block_i8_build(p, window, bins.data(), p->nbins)) {
+            msd_block_plan_destroy(p);
+            return rc;
+        }
+    }
     *out = p;
     return MSD_OK;
 }
@@ -596,6 +605,7 @@ void msd_block_plan_destroy(msd_block_plan *p) {
     hipFree(p->d_bins);
     hipFree(p->d_bconst);
     hipFree(p->d_energy);
+    hipFree(p->d_i8);
     delete p;
 }
 

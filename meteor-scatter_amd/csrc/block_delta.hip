@@ -296,19 +296,27 @@ template <typename T, int SPL>
 int launch_bd2(msd_block_plan *p, const void *x, const int64_t *off, const int64_t *len, int64_t nfiles,
                int64_t max_blocks, double *band_db, double *noise_db, double *delta, int64_t ld) {
     const int64_t blocks = nfiles * max_blocks;
-    if ((size_t)blocks > p->energy_cap) {  // grown once per plan (the stream is drained first)
-        MSD_HIP(hipStreamSynchronize(p->ctx->stream));
+    if ((size_t)blocks + 1 > p->energy_cap) {  // grown once per plan (the stream is drained first);
+        MSD_HIP(hipStreamSynchronize(p->ctx->stream));  // + 1: block_i8_kernel's spare slot
         MSD_HIP(hipFree(p->d_energy));
         p->d_energy = nullptr;
         p->energy_cap = 0;
-        MSD_HIP(hipMalloc(&p->d_energy, sizeof(double2) * (size_t)blocks));
-        p->energy_cap = (size_t)blocks;
+        MSD_HIP(hipMalloc(&p->d_energy, sizeof(double2) * ((size_t)blocks + 1)));
+        p->energy_cap = (size_t)blocks + 1;
     }
     // persistent grid: a few workgroups per CU, each walking groups of 16 blocks (4 resident per CU;
     // C3 A/B over two boxes, profiles/r4_bd2_grid_ab.txt: 4 per CU 0.409 ms, 8 0.381-0.393, 16 0.372-0.383,
     // 32 0.382, one per group 0.398)
     const int64_t grid = std::min<int64_t>((blocks + BD2_GROUPS - 1) / BD2_GROUPS, (int64_t)p->ctx->num_cu * 16);
     const size_t lds = sizeof(double) * (16 * bd2_pitch(SPL) + BD2_GROUPS * (size_t)(p->nbins > 0 ? p->nbins : 1));
+    bool done = false;
+    if constexpr (std::is_same_v<T, int16_t>) {
+        if (p->d_i8 && !p->ctx->block_goertzel) {  // the exact integer DFT on the matrix cores
+            if (int rc = launch_block_i8(p, static_cast<const int16_t *>(x), off, len, nfiles, max_blocks)) return rc;
+            done = true;
+        }
+    }
+    if (!done)
     hipLaunchKernelGGL((block_delta2_kernel<T, SPL>), dim3((unsigned)grid), dim3(256), lds, p->ctx->stream,
                        static_cast<const T *>(x), off, len, nfiles, max_blocks, p->block_size, p->L, p->d_window,
                        p->d_bconst, p->band_hi - p->band_lo + 1 > 0 ? p->band_hi - p->band_lo + 1 : 0,

@@ -70,6 +70,7 @@ struct msd_ctx {
     int i8_n = 0, i8_nk = 0;
     int i8_km[16] = {};
     bool refine_goertzel = false;  // MSD_OPT_REFINE_GOERTZEL: int16 refinement on the float64 Goertzel
+    bool block_goertzel = false;   // MSD_OPT_BLOCK_GOERTZEL: int16 block energies on the float64 Goertzel
     int cstft_reserve = 0;         // MSD_OPT_CSTFT_RESERVE: workgroup slots the C5 spectrogram leaves free
     int cstft_sched = 0;           // MSD_OPT_CSTFT_SCHED: 0 / 2 chunks from a guided schedule, 1 fixed ranges
     int stft_sched = 0;            // MSD_OPT_STFT_SCHED: the same for stft1024_kernel (tiles)
@@ -125,6 +126,8 @@ struct msd_block_plan {
     int spl = 0;                          // samples per lane segment of the fast path
     double2 *d_energy = nullptr;          // fast path: per block (band, noise) energy + 1e-12, grown
     size_t energy_cap = 0;                // blocks d_energy holds
+    void *d_i8 = nullptr;                 // int16 blocks on the matrix cores (block_i8.hip): B fragments
+                                          // + column constants, when block_i8_shape(L, nbins)
 };
 
 struct msd_welch_plan {
@@ -255,6 +258,10 @@ int launch_stft_any(msd_stft_plan *plan, const void *x, int dtype, const int64_t
                     int64_t nfiles, void *out, int64_t ld);
 int launch_stft1024(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                     int64_t nfiles, float *out, int64_t ld);
+bool block_i8_shape(int64_t L, int nbins);
+int block_i8_build(msd_block_plan *p, const double *window, const int *bins, int nbins);
+int launch_block_i8(msd_block_plan *p, const int16_t *x, const int64_t *off, const int64_t *len, int64_t nfiles,
+                    int64_t max_blocks);
 int launch_block_delta(msd_block_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                        int64_t nfiles, int64_t max_blocks, double *band_db, double *noise_db, double *delta,
                        int64_t ld);

@@ -43,6 +43,7 @@ OPT_CSTFT_RESERVE = 4
 OPT_STREAM_CUS = 5
 OPT_CSTFT_SCHED = 6
 OPT_STFT_SCHED = 7
+OPT_BLOCK_GOERTZEL = 8
 COMM_ID_BYTES = 128
 
 

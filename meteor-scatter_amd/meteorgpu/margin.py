@@ -16,7 +16,10 @@ The bound (standard floating-point error model, u = 2^-53):
   ``S = sum_j |x_j w_j| <= max|x| * sum(w)`` over the L samples used and ``c`` the longest chain
   of roundings an input term passes through: pocketfft's real FFT ``4 log2(Nf) + 8``; the
   Goertzel segments ``3 L_seg G + 24`` (L_seg samples per lane, G = min(1/|sin theta|, L_seg)
-  the recurrence's error gain at bin angle theta, 24 for the rotations and the 16-lane sum);
+  the recurrence's error gain at bin angle theta, 24 for the rotations and the 16-lane sum), or,
+  for int16 blocks on the exact integer path (csrc/block_i8.hip), ``10.25 L / sum(w)`` (its
+  coefficients' 2^-55 quantisation is absolute, not relative to the window) -- the larger of
+  the two;
 * a band energy E = sum |X_k|^2 + 1e-12 over n bins then moves by at most
   ``dE = 2 sqrt(n E) dX + n dX^2 + (n + 2) u E``;
 * its dB value by at most ``10/ln 10 * r / (1 - r) + 2 u`` with r = dE / E (unbounded when
@@ -73,10 +76,23 @@ def _goertzel_chain(l_seg: int, bins, nfft: int) -> float:
     return 3.0 * l_seg * g + 24.0
 
 
-def _chain(nfft: int, L: int, bins: np.ndarray) -> float:
-    """c: longest rounding chain of a bin (pocketfft + the device's Goertzel segments)."""
+def _i8_chain(L: int, nbins: int, wsum: float) -> float:
+    """The int16 blocks' exact integer DFT (csrc/block_i8.hip), where it applies (L = 256, 512 or
+    1024, 1-8 bins): each coefficient w_n cos / sin is quantised to 2^-55 = u / 4 absolute and the
+    float64 digit combination (7 digit terms) adds < 10 u of sum |x|, so |dX| <= 10.25 u sum|x| <=
+    10.25 u L max|x| = (10.25 L / sum w) u S.  0 where the path does not apply."""
+    if int(L) not in (256, 512, 1024) or not 1 <= int(nbins) <= 8:
+        return 0.0
+    return 10.25 * float(L) / wsum if wsum > 0 else 0.0  # sum w = 0: every coefficient is 0, X = 0
+
+
+def _chain(nfft: int, L: int, bins: np.ndarray, wsum: float) -> float:
+    """c: longest rounding chain of a bin (pocketfft + the device's transform: the Goertzel
+    segments or, for int16 blocks of the int8 path's shapes, its quantisation -- the larger, so
+    the bound holds whichever path ran)."""
     l_seg = max(1, -(-int(L) // 16))  # samples per lane: the block_delta kernel's 16 lanes
-    return 4.0 * math.log2(nfft) + 8.0 + _goertzel_chain(l_seg, bins, nfft)
+    dev = max(_goertzel_chain(l_seg, bins, nfft), _i8_chain(L, len(bins), wsum))
+    return 4.0 * math.log2(nfft) + 8.0 + dev
 
 
 def band_db_error(e_db: np.ndarray, nbins: int, dx: float) -> np.ndarray:
@@ -95,11 +111,12 @@ def delta_error_bound(band_db: np.ndarray, noise_db: np.ndarray, *, nfft: int, L
                       xmax: float, band: tuple[int, int], noise: tuple[int, int]) -> np.ndarray:
     """Per-block bound on |delta_gpu - delta_numpy| (dB).  ``band`` / ``noise``: inclusive bin
     ranges ((0, -1) when empty); ``window``: the L window values used; ``xmax``: max |x|."""
-    s = float(xmax) * float(np.abs(np.asarray(window, dtype=np.float64)[:L]).sum())
+    wsum = float(np.abs(np.asarray(window, dtype=np.float64)[:L]).sum())
+    s = float(xmax) * wsum
     nb = max(0, band[1] - band[0] + 1)
     nn = max(0, noise[1] - noise[0] + 1)
     bins = np.concatenate([np.arange(band[0], band[1] + 1), np.arange(noise[0], noise[1] + 1)])
-    dx = _chain(nfft, L, bins) * U * s
+    dx = _chain(nfft, L, bins, wsum) * U * s
     return band_db_error(band_db, nb, dx) + band_db_error(noise_db, nn, dx)
 
 
@@ -112,7 +129,7 @@ def delta_error_bounds(band_db: np.ndarray, noise_db: np.ndarray, *, nfft: int, 
     nn = max(0, noise[1] - noise[0] + 1)
     bins = np.concatenate([np.arange(band[0], band[1] + 1), np.arange(noise[0], noise[1] + 1)])
     s = np.asarray(xmax, dtype=np.float64).reshape(-1, 1) * wsum
-    dx = _chain(nfft, L, bins) * U * s
+    dx = _chain(nfft, L, bins, wsum) * U * s
     return band_db_error(band_db, nb, dx) + band_db_error(noise_db, nn, dx)
 
 

@@ -35,7 +35,7 @@ def test_pocketfft_within_bin_bound(seed, offset, scale):
     bins = np.array([0, 1, 2, 170, 171, 172, 300, 511, 512])
     exact = _exact_bins(xw, nfft, bins)
     S = float(np.abs(x).max()) * float(w[:nfft].sum())
-    bound = M._chain(nfft, nfft, bins) * M.U * S
+    bound = M._chain(nfft, nfft, bins, float(w[:nfft].sum())) * M.U * S
     err = np.abs(X[bins].astype(np.clongdouble) - exact).astype(np.float64)
     assert (err <= bound).all() and err.max() > 0
 

@@ -15,7 +15,7 @@ for grp in \
   "FETCH_SIZE" \
   "WRITE_SIZE" ; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${REGEX:-stft|block_delta|detect}" -d "$OUT/p$i" -o pmc \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${REGEX:-stft|block_delta|block_band_i8|detect}" -d "$OUT/p$i" -o pmc \
       --output-format csv -- python3 "$ROOT/bench.py" $ARGS > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
