@@ -75,6 +75,7 @@ int ctx_scratch(msd_ctx *ctx, int slot, size_t bytes, void **out) {
             ctx->scratch_bytes[slot] = 0;
         }
         size_t want = bytes < 4096 ? 4096 : bytes;
+        ctx->rf_last_dev = nullptr;  // a new block (perhaps at the old address) holds no uploaded tables
         MSD_HIP(hipMalloc(&ctx->scratch[slot], want));
         ctx->scratch_bytes[slot] = want;
     }

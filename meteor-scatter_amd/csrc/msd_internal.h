@@ -61,6 +61,10 @@ struct msd_ctx {
     void *rf_pin = nullptr;
     size_t rf_pin_bytes = 0;
     hipEvent_t rf_ev = nullptr;
+    // the tables of the last call as uploaded to scratch slot 4 (rf_last_dev): a call with the same
+    // tables (every step of a stream of the same length) skips the two copies
+    std::vector<char> rf_last;
+    const void *rf_last_dev = nullptr;
     // the int8-MFMA block step's tables (refine_i8.hip): B fragments, column starts, lane twiddles,
     // built once per (frame length, bins)
     void *i8_tab = nullptr;

@@ -407,24 +407,37 @@ int msd_iq_delta64_sums_dev(msd_ctx *ctx, const void *x, int32_t dtype, int64_t 
     const int64_t *d_fstart = meta, *d_fcs = meta + nranges, *d_bstart = meta + 2 * nranges + 1,
                   *d_bcs = meta + 3 * nranges + 1;
     // both tables through a pinned staging block (the copies are truly async, so the call returns
-    // while the kernels run); the previous call's copies have left it once its event has passed
+    // while the kernels run); the previous call's copies have left it once its event has passed.
+    // The same tables as the last call's, still in the same scratch block, are not copied again:
+    // in the C5 step the two copies sat between the spectrogram's end and the delta's start.
     const size_t b_rt = sizeof(double2) * rt.size(), b_hm = sizeof(int64_t) * hm.size();
-    if (!ctx->rf_ev) MSD_HIP(hipEventCreateWithFlags(&ctx->rf_ev, hipEventDisableTiming));
-    else MSD_HIP(hipEventSynchronize(ctx->rf_ev));
-    if (ctx->rf_pin_bytes < b_rt + b_hm) {
-        if (ctx->rf_pin) MSD_HIP(hipHostFree(ctx->rf_pin));
-        ctx->rf_pin = nullptr;
-        ctx->rf_pin_bytes = 0;
-        const size_t want = std::max<size_t>(b_rt + b_hm, 4096);
-        MSD_HIP(hipHostMalloc(&ctx->rf_pin, want, hipHostMallocDefault));
-        ctx->rf_pin_bytes = want;
+    const bool same = ctx->rf_last_dev == d && ctx->rf_last.size() == b_rt + b_hm &&
+                      !std::memcmp(ctx->rf_last.data(), rt.data(), b_rt) &&
+                      !std::memcmp(ctx->rf_last.data() + b_rt, hm.data(), b_hm);
+    hipError_t e = hipSuccess;
+    if (!same) {
+        ctx->rf_last_dev = nullptr;  // set again once both copies are enqueued
+        if (!ctx->rf_ev) MSD_HIP(hipEventCreateWithFlags(&ctx->rf_ev, hipEventDisableTiming));
+        else MSD_HIP(hipEventSynchronize(ctx->rf_ev));
+        if (ctx->rf_pin_bytes < b_rt + b_hm) {
+            if (ctx->rf_pin) MSD_HIP(hipHostFree(ctx->rf_pin));
+            ctx->rf_pin = nullptr;
+            ctx->rf_pin_bytes = 0;
+            const size_t want = std::max<size_t>(b_rt + b_hm, 4096);
+            MSD_HIP(hipHostMalloc(&ctx->rf_pin, want, hipHostMallocDefault));
+            ctx->rf_pin_bytes = want;
+        }
+        char *pin = static_cast<char *>(ctx->rf_pin);
+        std::memcpy(pin, rt.data(), b_rt);
+        std::memcpy(pin + b_rt, hm.data(), b_hm);
+        e = hipMemcpyAsync(rot, pin, b_rt, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(meta, pin + b_rt, b_hm, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(ctx->rf_ev, st);
+        if (e == hipSuccess) {
+            ctx->rf_last.assign(pin, pin + b_rt + b_hm);
+            ctx->rf_last_dev = d;
+        }
     }
-    char *pin = static_cast<char *>(ctx->rf_pin);
-    std::memcpy(pin, rt.data(), b_rt);
-    std::memcpy(pin + b_rt, hm.data(), b_hm);
-    hipError_t e = hipMemcpyAsync(rot, pin, b_rt, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(meta, pin + b_rt, b_hm, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipEventRecord(ctx->rf_ev, st);
     // int16 blocks of 1024 samples: the exact integer DFT on the matrix cores (refine_i8.hip), its
     // own (smaller) rounding chain in the bound
     RefineGeom GF = G;

@@ -264,6 +264,9 @@ class IQShardDetector(_stream.CertifyingShard):
         if self.f1 > self.f0:
             if self.exact_delta:
                 # the exact delta first (full chip): the detector (dctx) then runs beside the spectrogram
+                # (the delta on the spectrogram's own stream instead, in order behind the previous
+                # step's spectrogram, measured 12.55-12.71 against 11.77-11.80 ms per step:
+                # profiles/r5_c5_delta_stream_ab.txt)
                 self._delta_exact(self.batch.n, self.f1 - self.f0, 0)
                 self._after(self.dctx, self.ctx)
                 self._after(self.sctx, self.ctx)
@@ -294,11 +297,12 @@ class IQShardDetector(_stream.CertifyingShard):
     def _fsums(self):
         return self.d_fsum if self._fsums_ok else None
 
-    def _delta_exact(self, n_samples: int, nframes: int, c0: int):
+    def _delta_exact(self, n_samples: int, nframes: int, c0: int, ctx: _lib.Context | None = None):
         """float64 delta and bound of the local frames [c0, c0 + nframes), whose samples start at the
         batch buffer's first sample (frame c0 + j at sample j * hop); with them the frames' sample sums
-        (batch-local frame j) for the spectrogram's detrend, where the block step carries them"""
-        args = (self.ctx, self.batch.d_x, self.batch.code, n_samples, self.N, self.hop, self.fs_, self.band,
+        (batch-local frame j) for the spectrogram's detrend, where the block step carries them.  On
+        ctx's stream (default: the caller's context)"""
+        args = (ctx or self.ctx, self.batch.d_x, self.batch.code, n_samples, self.N, self.hop, self.fs_, self.band,
                 self.noise, np.array([[0, nframes]], np.int64), _lib.C.c_void_p(self.plan.d_delta.value + 8 * c0),
                 _lib.C.c_void_p(self.plan.d_ed.value + 8 * c0))
         if self._fsums_ok:
