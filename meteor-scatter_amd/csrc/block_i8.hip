@@ -42,6 +42,7 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 constexpr int BI_ND = 7;       // coefficient digits (= column tiles)
 constexpr int BI_ROWS = 16;    // blocks per tile
 constexpr int BI_MAXBINS = 8;  // components 2 * bins <= 16 columns
+constexpr int BI_PP = 9;       // powers row pitch (doubles): 16 rows on 16 disjoint bank pairs for the band sums
 constexpr int BI_WAVES = 8;    // waves per workgroup (2 per SIMD) sharing one copy of the B fragments
 
 template <int CTRL>
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(64 * BI_WAVES, 1) void block_band_i8_kernel(const i
                                                           double2 *__restrict__ energy) {
     __shared__ v4i sB[BI_ND * KS * 64];
     __shared__ int sInit[BI_ND * 16];
-    __shared__ double sP[BI_WAVES][BI_ROWS * BI_MAXBINS];  // per wave: the tile's powers [row][bin]
+    __shared__ double sP[BI_WAVES][BI_ROWS * BI_PP];  // per wave: the tile's powers [row][bin]
     for (int i = threadIdx.x; i < BI_ND * KS * 64; i += 64 * BI_WAVES) sB[i] = bfrag[i];
     for (int i = threadIdx.x; i < BI_ND * 16; i += 64 * BI_WAVES) sInit[i] = colinit[i];
     __syncthreads();
@@ -173,14 +174,14 @@ __global__ __launch_bounds__(64 * BI_WAVES, 1) void block_band_i8_kernel(const i
             p *= 0x1p-6;
             const double q = dpp64<0xB1>(p);  // the partner component (c ^ 1)
             // |X|^2 = re^2 + im^2: within 2 ulp of np.abs(X)**2 (the bar is 1e-9 dB)
-            if (!(c & 1) && (c >> 1) < nbins) pw[(4 * grp + i) * BI_MAXBINS + (c >> 1)] = p * p + q * q;
+            if (!(c & 1) && (c >> 1) < nbins) pw[(4 * grp + i) * BI_PP + (c >> 1)] = p * p + q * q;
         }
         __builtin_amdgcn_wave_barrier();
         {  // every lane stores (lanes past the tile's 16 rows and missing blocks into the spare slot
            // energy[nblocks]): a store behind a branch would leave the memory counter in two states
            // at the loop head, and the wait for the prefetched samples would become a wait for all
-            const double eb = np_sum_small(ArrRef{pw}, row * BI_MAXBINS, nband) + 1e-12;
-            const double en = np_sum_small(ArrRef{pw}, row * BI_MAXBINS + nband, nnoise) + 1e-12;
+            const double eb = np_sum_small(ArrRef{pw}, row * BI_PP, nband) + 1e-12;
+            const double en = np_sum_small(ArrRef{pw}, row * BI_PP + nband, nnoise) + 1e-12;
             energy[l < BI_ROWS && cur.valid ? cur.g : nblocks] = make_double2(eb, en);
         }
         __builtin_amdgcn_wave_barrier();  // pw is rewritten by the next tile

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(DT_THREADS, 4) void detect_kernel(const double *__r
     for (int64_t c = tid; c < nd; c += DT_THREADS) {
         const int64_t a = df[c].start, b = df[c].stop;
         const int64_t n = b - a;
-        df[c].db = np_sum(ArrRef{d}, a, n) / (double)n;
+        df[c].db = np_sum(ArrRef{src}, a, n) / (double)n;  // the staged file (LDS) when it fits one chunk
         if (P.has_hist) {
             const double t_start = (double)a * P.block_sec;
             const int64_t us = llrint(t_start * 1e6);
