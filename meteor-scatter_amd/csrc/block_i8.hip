@@ -20,7 +20,7 @@
 // K steps of 64 (a lane's A fragment = 16 samples of its row: 8 at 8 g and 8 at 32 + 8 g of the
 // step, g = lane >> 4, one 64-B piece per row per load instruction), columns = the components
 // (bin j's real part 2 j, imaginary part 2 j + 1; <= 8 bins) in one 16-column tile per digit.  A
-// lane of the result (column c = lane & 15, rows 4 (lane >> 4) + i) holds all six digits of its
+// lane of the result (column c = lane & 15, rows 4 (lane >> 4) + i) holds all seven digits of its
 // component for 4 blocks: the digits combine by a float64 Horner sum in registers, the real and
 // imaginary parts by one DPP swap, and the band sums (numpy's order) run on 16 lanes from LDS.
 // The output is block_delta2_kernel's: per block (band energy + 1e-12, noise energy + 1e-12),
