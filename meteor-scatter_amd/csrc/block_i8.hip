@@ -162,6 +162,9 @@ __global__ __launch_bounds__(64 * BI_WAVES, 1) void block_band_i8_kernel(const i
                 Ah[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bk[d], Ah[d], 0, 0, 0);
                 Al[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bk[d], Al[d], 0, 0, 0);
             }
+            // keep each K step's refills in K order: with the prologue store below, every K step
+            // then waits for its own two loads only (vmcnt 31-32), a tile of samples in flight
+            __builtin_amdgcn_sched_barrier(0);
         }
         // component c of blocks 4 grp + i: sum_b A_b 256^(6 - b) 2^-54 = sum_b A_b 2^(-6 - 8 b),
         // A_b = 256 h_b + l_b (exact in float64)
@@ -193,6 +196,9 @@ __global__ __launch_bounds__(64 * BI_WAVES, 1) void block_band_i8_kernel(const i
         R[2 * ks] = fetch(cur, ks, 0);
         R[2 * ks + 1] = fetch(cur, ks, 1);
     }
+    // a store after the first loads, as every tile ends with one: the memory counter enters the loop
+    // in the state the loop leaves it, so the first K step waits for its own samples only
+    energy[nblocks] = make_double2(0.0, 0.0);
     for (int64_t t = wave; t < ntiles; t += nwaves) {
         const Row nxt = t + nwaves < ntiles ? row_of(t + nwaves) : cur;  // wave-uniform choice
         tile(R, cur, nxt);
