@@ -199,3 +199,65 @@ def test_block_i8_misaligned_files_and_partial_tile():
         b1, n1, d1, _ = dsp.block_powers(f, fs, bs, band, noise, n_fft)
         for j, one in enumerate((b1, n1, d1)):
             np.testing.assert_array_equal(out[0][j][i, :nbk], one)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fs,bs,n_fft,band,noise", [(6000, 0.1, 128, (990, 1010), (2990, 3010)),
+                                                     (48000, 0.2, 512, (950, 1050), (2950, 3050))])
+def test_block_i8_ragged_batch(fs, bs, n_fft, band, noise):
+    """a ragged batch as the file loader hands it over: 41 files of 0 to 37 blocks (shorter than one
+    block, exactly one, one sample short of / past a whole count), odd and even offsets, so that a
+    16-block tile spans up to 16 files and many rows of a tile do not exist; ld > max_blocks, with
+    every entry the path must not write checked untouched"""
+    from meteorgpu import _lib, dsp
+    B, nfft = int(fs * bs), 2 * n_fft
+    L = min(B, nfft)
+    bb, nb = dsp.band_bins(nfft, fs, band), dsp.band_bins(nfft, fs, noise)
+    assert L in (256, 512, 1024) and 1 <= max(0, bb[1] - bb[0] + 1) + max(0, nb[1] - nb[0] + 1) <= 8
+    rng = np.random.default_rng(77 + n_fft)
+    nblk = [0, 1, 1, 2, 0, 3, 37, 1, 5, 0, 16, 15, 17, 1, 2] + [int(v) for v in rng.integers(0, 12, 26)]
+    lens = []
+    for i, k in enumerate(nblk):
+        extra = [0, B - 1, 1, int(rng.integers(0, B))][i % 4]
+        lens.append(k * B + extra)  # k = 0: shorter than one block
+    files, offs, pos = [], [], 5
+    for i, n in enumerate(lens):
+        t = np.arange(n) / fs
+        f = 900.0 * rng.standard_normal(n) + 4000.0 * np.sin(2 * np.pi * 1000.0 * t + i) + float(rng.integers(-500, 500))
+        files.append(np.clip(np.round(f), -32768, 32767).astype(np.int16))
+        offs.append(pos)
+        pos += n + int(rng.integers(0, 3))  # odd and even gaps
+    nf = len(files)
+    buf = np.zeros(pos + 8, np.int16)
+    for o, f in zip(offs, files):
+        buf[o: o + f.size] = f
+    lens = np.array(lens, np.int64)
+    max_blocks = int(lens.max() // B)
+    ld = max_blocks + 3
+    ctx = dsp.context(0)
+    plan = _lib.BlockPlan(ctx, B, nfft, dsp.hanning_sym(B)[:L], bb, nb)
+    d_x, d_off, d_len = ctx.alloc(2 * buf.size), ctx.alloc(8 * nf), ctx.alloc(8 * nf)
+    d_out = [ctx.alloc(8 * nf * ld) for _ in range(3)]
+    sentinel = np.full((nf, ld), -777.0)
+    try:
+        d_x.upload(buf)
+        d_off.upload(np.array(offs, np.int64))
+        d_len.upload(lens)
+        for d in d_out:
+            d.upload(sentinel)
+        plan.run_dev(d_x, np.int16, d_off, d_len, nf, max_blocks, *d_out, ld)
+        ctx.synchronize()
+        got = [d.download(np.empty((nf, ld), np.float64)) for d in d_out]
+    finally:
+        plan.close()
+        for d in (d_x, d_off, d_len, *d_out):
+            d.free()
+    for i, f in enumerate(files):
+        k = f.size // B
+        for j in range(3):
+            assert (got[j][i, k:] == -777.0).all(), (i, j)  # past the file's blocks: untouched
+        if k == 0:
+            continue
+        ref = O.block_powers_ref(f, fs, bs, band, noise, n_fft)
+        for j in range(3):
+            np.testing.assert_allclose(got[j][i, :k], ref[j], rtol=0, atol=1e-9)
