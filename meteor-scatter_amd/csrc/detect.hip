@@ -140,17 +140,26 @@ __global__ __launch_bounds__(DT_THREADS, 4) void detect_kernel(const double *__r
     double *tf = thr + f * P.ld;
     if (cfg.adaptive) {
         const int64_t W = cfg.window_blocks;
-        for (int64_t i = tid; i < nb; i += DT_THREADS) {
-            if (i < cfg.fixed_init_blocks) {
-                tf[i] = thr0;
-            } else {
+        // windows of <= 1928 blocks (tree depth <= 4; 120 s at 0.1 s is 1200) by the iterative walk, all
+        // lanes in one leaf loop (A/B on C3's 1440 files: the recursive form's inlined copy per tree
+        // shape made this phase 0.08 of the kernel's 0.13 ms); the LDS-staged file as its own branch
+        // so that the walk's loads are LDS loads, not flat ones
+        // the fixed-init blocks first, then one thread per fresh window from the first one on (a
+        // 60 s file: 250 windows on 256 threads, one round)
+        const int64_t f0 = cfg.fixed_init_blocks < nb ? (cfg.fixed_init_blocks > 0 ? cfg.fixed_init_blocks : 0) : nb;
+        for (int64_t i = tid; i < f0; i += DT_THREADS) tf[i] = thr0;
+        auto fresh = [&](const double *p) {
+            for (int64_t i = f0 + tid; i < nb; i += DT_THREADS) {
                 const int64_t ws = i - W > 0 ? i - W : 0;
                 const int64_t wn = i - ws;
                 double m, s;
-                np_mean_std(src, ws, wn, m, s);
+                if (wn <= NP_ITER_MAX[4]) np_mean_std_iter<4>(p, ws, (int)wn, m, s);
+                else np_mean_std(p, ws, wn, m, s);
                 tf[i] = m + cfg.k_std * s;
             }
-        }
+        };
+        if (whole) fresh(c_delta);
+        else fresh(d);
     }
     __syncthreads();
 

@@ -120,6 +120,64 @@ struct SqDevRef {
     }
 };
 
+// numpy's pairwise sum of one buffer chunk walked iteratively, for n <= NP_ITER_MAX[DMAX] (tree depth
+// <= DMAX): the leaves in order, the pending right subtrees and the finished left sums on register
+// stacks that are shifted, never indexed (no scratch).  Every lane runs the same loop and one copy
+// of the leaf loop, so a wave whose lanes sum windows of different lengths (the detector's fresh
+// thresholds) runs the leaves in lockstep instead of the recursion's inlined copy per tree shape,
+// one after another.  Same association as np_pairwise: each internal node is left + right.
+constexpr int NP_ITER_MAX[8] = {128, 248, 488, 968, 1928, 3848, 7688, 8192};  // largest n of depth <= D
+
+template <int DMAX, typename A>
+__device__ __forceinline__ double np_pairwise_iter(const A &a, int64_t base, int n) {
+#pragma clang fp contract(off)
+    int pb[DMAX], ps[DMAX];  // pending right subtrees (offset, size), top = [0]
+    double pv[DMAX];         // left-subtree sums waiting for their right sibling, top = [0]
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) pb[k] = ps[k] = 0, pv[k] = 0.0;
+    int b = 0, s = n, d = 0;
+    unsigned right = 0;  // bit d: the node at depth d is a right child
+    for (;;) {
+        while (s > 128) {  // descend to the leftmost leaf, the right halves pending
+            int s2 = s / 2;
+            s2 -= s2 % 8;
+#pragma unroll
+            for (int k = DMAX - 1; k > 0; --k) pb[k] = pb[k - 1], ps[k] = ps[k - 1];
+            pb[0] = b + s2;
+            ps[0] = s - s2;
+            s = s2;
+            ++d;
+            right &= ~(1u << d);
+        }
+        double v = np_pairwise_leaf(a, base + b, s);
+        while (d > 0 && ((right >> d) & 1u)) {  // a right subtree done: its parent = left + right
+            v = pv[0] + v;
+#pragma unroll
+            for (int k = 0; k < DMAX - 1; ++k) pv[k] = pv[k + 1];
+            --d;
+        }
+        if (d == 0) return v;
+#pragma unroll
+        for (int k = DMAX - 1; k > 0; --k) pv[k] = pv[k - 1];
+        pv[0] = v;  // a left subtree done: on to its right sibling
+        b = pb[0];
+        s = ps[0];
+#pragma unroll
+        for (int k = 0; k < DMAX - 1; ++k) pb[k] = pb[k + 1], ps[k] = ps[k + 1];
+        right |= 1u << d;
+    }
+}
+
+// numpy mean/std of p[base .. base+n), n <= NP_ITER_MAX[DMAX], by np_pairwise_iter
+template <int DMAX>
+__device__ __forceinline__ void np_mean_std_iter(const double *p, int64_t base, int n, double &mean, double &std) {
+#pragma clang fp contract(off)
+    const double s = 0.0 + np_pairwise_iter<DMAX>(ArrRef{p}, base, n);
+    mean = s / (double)n;
+    const double v = 0.0 + np_pairwise_iter<DMAX>(SqDevRef{p, mean}, base, n);
+    std = sqrt(v / (double)n);
+}
+
 // numpy mean/std of p[base .. base+n).  n <= 128 (one pairwise leaf) stays inline: the general
 // np_sum is a large out-of-line function whose call and instruction-cache misses cost more
 // than the sum itself in the event handlers of the live scan (live.hip)
