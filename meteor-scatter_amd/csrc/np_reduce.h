@@ -45,31 +45,72 @@ __device__ __forceinline__ double np_pairwise_leaf(const A &a, int64_t base, int
     return res;
 }
 
-// Walk of numpy's recursion tree over [base, base+n), n <= 8192 (one ufunc buffer chunk), in
-// numpy's order (left subtree first).  leaf(b, m) returns the sum of a leaf (m <= 128); the walk
-// combines the leaves exactly as numpy's recursion does.  Compile-time recursion over the depth
-// (7 splits cover 8192): no stack array, so nothing lives in scratch (the iterative walk's
-// stack did: detect.hip's leaf-table builder, 1.2 KB of scratch per lane)
-template <int D, typename LeafFn>
-__device__ __forceinline__ double np_tree_rec(int64_t base, int64_t n, const LeafFn &leaf) {
+// numpy's recursion tree over [base, base+n) walked iteratively, for n <= NP_ITER_MAX[DMAX] (tree
+// depth <= DMAX): the leaves in order (leaf(b, m) returns a leaf's sum, m <= 128), the pending right
+// subtrees and the finished left sums on register stacks that are shifted, never indexed (no
+// scratch), each internal node combined as left + right (numpy's association).  Every lane runs the
+// same loop and one copy of the leaf code, so a wave whose lanes sum ranges of different lengths runs
+// the leaves in lockstep; the recursion inlined one leaf copy per tree shape (128 at depth 7: the
+// 100-180 KB np_pairwise functions), which the lanes of such a wave ran one after another.
+constexpr int NP_ITER_MAX[8] = {128, 248, 488, 968, 1928, 3848, 7688, 8192};  // largest n of depth <= D
+
+template <int DMAX, typename LeafFn>
+__device__ __forceinline__ double np_walk_iter(int64_t base, int n, const LeafFn &leaf) {
 #pragma clang fp contract(off)
-    if constexpr (D == 0) {
-        return leaf(base, n);
-    } else {
-        if (n <= 128) return leaf(base, n);
-        int64_t n2 = n / 2;
-        n2 -= n2 % 8;
-        const double l = np_tree_rec<D - 1>(base, n2, leaf);
-        return l + np_tree_rec<D - 1>(base + n2, n - n2, leaf);
+    int pb[DMAX], ps[DMAX];  // pending right subtrees (offset, size), top = [0]
+    double pv[DMAX];         // left-subtree sums waiting for their right sibling, top = [0]
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) pb[k] = ps[k] = 0, pv[k] = 0.0;
+    int b = 0, s = n, d = 0;
+    unsigned right = 0;  // bit d: the node at depth d is a right child
+    for (;;) {
+        while (s > 128) {  // down to the leftmost leaf, the right halves pending
+            int s2 = s / 2;
+            s2 -= s2 % 8;
+#pragma unroll
+            for (int k = DMAX - 1; k > 0; --k) pb[k] = pb[k - 1], ps[k] = ps[k - 1];
+            pb[0] = b + s2;
+            ps[0] = s - s2;
+            s = s2;
+            ++d;
+            right &= ~(1u << d);
+        }
+        double v = leaf(base + b, (int64_t)s);
+        while (d > 0 && ((right >> d) & 1u)) {  // a right subtree done: its parent = left + right
+            v = pv[0] + v;
+#pragma unroll
+            for (int k = 0; k < DMAX - 1; ++k) pv[k] = pv[k + 1];
+            --d;
+        }
+        if (d == 0) return v;
+#pragma unroll
+        for (int k = DMAX - 1; k > 0; --k) pv[k] = pv[k - 1];
+        pv[0] = v;  // a left subtree done: on to its right sibling
+        b = pb[0];
+        s = ps[0];
+#pragma unroll
+        for (int k = 0; k < DMAX - 1; ++k) pb[k] = pb[k + 1], ps[k] = ps[k + 1];
+        right |= 1u << d;
     }
 }
-template <typename LeafFn>
-__device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
-    return np_tree_rec<7>(base, n, leaf);
+
+template <int DMAX, typename A>
+__device__ __forceinline__ double np_pairwise_iter(const A &a, int64_t base, int n) {
+    return np_walk_iter<DMAX>(base, n, [&](int64_t b, int64_t m) { return np_pairwise_leaf(a, b, m); });
 }
 
-// numpy's recursion written as compile-time recursion over the depth (n <= 8192 needs at
-// most 7 splits): no stack array, so nothing is promoted to (or spilled from) registers
+// numpy's recursion tree over one ufunc buffer chunk (n <= 8192), leaves in order (left subtree
+// first), combined as numpy's recursion does.  An earlier iterative form kept its stack in an
+// indexed array, i.e. in scratch (1.2 KB per lane in detect.hip's leaf-table builder); the
+// compile-time recursion that replaced it inlined one leaf copy per tree shape.  np_walk_iter has
+// neither problem.
+template <typename LeafFn>
+__device__ double np_tree_walk(int64_t base, int64_t n, const LeafFn &leaf) {
+    return np_walk_iter<7>(base, (int)n, leaf);
+}
+
+// numpy's recursion written as compile-time recursion over the depth (n <= 8192 needs at most 7
+// splits): for a shallow, known depth (stream.hip's canonical blocks, D = 2)
 template <int D, typename A>
 __device__ __forceinline__ double np_pairwise_rec(const A &a, int64_t base, int64_t n) {
 #pragma clang fp contract(off)
@@ -86,7 +127,7 @@ __device__ __forceinline__ double np_pairwise_rec(const A &a, int64_t base, int6
 
 template <typename A>
 __device__ double np_pairwise(const A &a, int64_t base, int64_t n) {  // n <= NP_BUFSIZE
-    return np_pairwise_rec<7>(a, base, n);
+    return np_pairwise_iter<7>(a, base, (int)n);
 }
 
 constexpr int64_t NP_BUFSIZE = 8192;
@@ -119,54 +160,6 @@ struct SqDevRef {
         return d * d;
     }
 };
-
-// numpy's pairwise sum of one buffer chunk walked iteratively, for n <= NP_ITER_MAX[DMAX] (tree depth
-// <= DMAX): the leaves in order, the pending right subtrees and the finished left sums on register
-// stacks that are shifted, never indexed (no scratch).  Every lane runs the same loop and one copy
-// of the leaf loop, so a wave whose lanes sum windows of different lengths (the detector's fresh
-// thresholds) runs the leaves in lockstep instead of the recursion's inlined copy per tree shape,
-// one after another.  Same association as np_pairwise: each internal node is left + right.
-constexpr int NP_ITER_MAX[8] = {128, 248, 488, 968, 1928, 3848, 7688, 8192};  // largest n of depth <= D
-
-template <int DMAX, typename A>
-__device__ __forceinline__ double np_pairwise_iter(const A &a, int64_t base, int n) {
-#pragma clang fp contract(off)
-    int pb[DMAX], ps[DMAX];  // pending right subtrees (offset, size), top = [0]
-    double pv[DMAX];         // left-subtree sums waiting for their right sibling, top = [0]
-#pragma unroll
-    for (int k = 0; k < DMAX; ++k) pb[k] = ps[k] = 0, pv[k] = 0.0;
-    int b = 0, s = n, d = 0;
-    unsigned right = 0;  // bit d: the node at depth d is a right child
-    for (;;) {
-        while (s > 128) {  // descend to the leftmost leaf, the right halves pending
-            int s2 = s / 2;
-            s2 -= s2 % 8;
-#pragma unroll
-            for (int k = DMAX - 1; k > 0; --k) pb[k] = pb[k - 1], ps[k] = ps[k - 1];
-            pb[0] = b + s2;
-            ps[0] = s - s2;
-            s = s2;
-            ++d;
-            right &= ~(1u << d);
-        }
-        double v = np_pairwise_leaf(a, base + b, s);
-        while (d > 0 && ((right >> d) & 1u)) {  // a right subtree done: its parent = left + right
-            v = pv[0] + v;
-#pragma unroll
-            for (int k = 0; k < DMAX - 1; ++k) pv[k] = pv[k + 1];
-            --d;
-        }
-        if (d == 0) return v;
-#pragma unroll
-        for (int k = DMAX - 1; k > 0; --k) pv[k] = pv[k - 1];
-        pv[0] = v;  // a left subtree done: on to its right sibling
-        b = pb[0];
-        s = ps[0];
-#pragma unroll
-        for (int k = 0; k < DMAX - 1; ++k) pb[k] = pb[k + 1], ps[k] = ps[k + 1];
-        right |= 1u << d;
-    }
-}
 
 // numpy mean/std of p[base .. base+n), n <= NP_ITER_MAX[DMAX], by np_pairwise_iter
 template <int DMAX>
