@@ -200,7 +200,9 @@ __global__ __launch_bounds__(64 * BI_WAVES, 1) void block_band_i8_kernel(const i
     // in the state the loop leaves it, so the first K step waits for its own samples only
     energy[nblocks] = make_double2(0.0, 0.0);
     for (int64_t t = wave; t < ntiles; t += nwaves) {
-        const Row nxt = t + nwaves < ntiles ? row_of(t + nwaves) : cur;  // wave-uniform choice
+        // the last tile re-reads itself (unused); a select between two Row values went through
+        // scratch at KS = 4, and its loads waited for the prefetched samples
+        const Row nxt = row_of(t + nwaves < ntiles ? t + nwaves : t);
         tile(R, cur, nxt);
         cur = nxt;
     }
