@@ -140,12 +140,13 @@ __global__ __launch_bounds__(DT_THREADS, 4) void detect_kernel(const double *__r
     double *tf = thr + f * P.ld;
     if (cfg.adaptive) {
         const int64_t W = cfg.window_blocks;
-        // windows of <= 1928 blocks (tree depth <= 4; 120 s at 0.1 s is 1200) by the iterative walk, all
-        // lanes in one leaf loop (A/B on C3's 1440 files: the recursive form's inlined copy per tree
-        // shape made this phase 0.08 of the kernel's 0.13 ms); the LDS-staged file as its own branch
-        // so that the walk's loads are LDS loads, not flat ones
-        // the fixed-init blocks first, then one thread per fresh window from the first one on (a
-        // 60 s file: 250 windows on 256 threads, one round)
+        // The fixed-init blocks first, then one thread per fresh window from the first one on (a 60 s
+        // file: 250 windows on 256 threads, one round).  Every window goes through numpy's tree walked
+        // iteratively (np_reduce.h), all lanes in one leaf loop; windows of <= 1928 blocks (depth <= 4;
+        // 120 s at 0.1 s is 1200) with four-entry stacks, longer ones through np_sum (seven entries,
+        // 8192-block chunks).  The LDS-staged file is its own branch, so that the walk's loads are
+        // LDS loads, not flat ones.  (The recursive walk's inlined copy per tree shape, run one shape
+        // after another by the lanes of a wave, made this phase 0.08 of the kernel's 0.13 ms on C3.)
         const int64_t f0 = cfg.fixed_init_blocks < nb ? (cfg.fixed_init_blocks > 0 ? cfg.fixed_init_blocks : 0) : nb;
         for (int64_t i = tid; i < f0; i += DT_THREADS) tf[i] = thr0;
         auto fresh = [&](const double *p) {
