@@ -126,6 +126,17 @@ def test_adaptive_detector_bit_exact(nb, bs):
         assert a.dB == r[3]
 
 
+@pytest.mark.parametrize("nb,bs", [(6000, 0.05), (15000, 0.01)])
+def test_adaptive_detector_long_windows_bit_exact(nb, bs):
+    """windows past the four-level walk (120 s at 0.05 s: 2 400 blocks > 1 928) and past one numpy
+    buffer chunk (120 s at 0.01 s: 12 000 blocks > 8 192: two chunks summed in turn), np_reduce.h"""
+    d = _random_delta(nb + 7, nb, bursts=max(1, nb // 100))
+    dets, thr = dsp.get_detections_adaptive(d, 4, bs, 120, 3, 20, 10)
+    rdets, rthr = O.get_detections_adaptive_ref(d, 4, bs, 120, 3, 20, 10)
+    np.testing.assert_array_equal(np.array(thr, float), np.array(rthr, float))
+    assert [(a.t_start, a.t_stop, a.dB) for a in dets] == [(r[0], r[1], r[3]) for r in rdets]
+
+
 @pytest.mark.parametrize("nb", [2, 300, 9000, 300000])
 @pytest.mark.parametrize("k", [1.0, 3.5])
 def test_global_detector_bit_exact(nb, k):
