@@ -43,7 +43,59 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 # C5 decision modes: (certify, delta source, exact decisions) -- meteorgpu.iq.IQShardDetector
 C5_MODES = {"exact": (True, "auto", True), "off": (False, "fp32", False), "flag": (True, "fp32", False),
             "refine": (True, "fp32", True)}
-POOL = 16              # distinct synthetic recordings, replicated over the batch
+SYNTH_PROCS = 16       # worker processes that make the synthetic inputs (the GPU box's CPU share)
+
+
+# ------------------------------------------------------------------ synthetic inputs
+# Every file / minute of every workload is distinct, seeded by SURVEY §8(d)'s rule (seed =
+# 1000 * config + file index): C3 file i of day d is synth_real(3000 + 1440 d + i), C5 minute m of
+# the stream synth_iq(5000 + m).  They are made by worker processes forked before any GPU call,
+# straight into one shared anonymous mapping (no pickling of gigabytes), so the bench's full-size
+# correctness guard (near_tie, certification) covers a day of distinct inputs.
+_SYN = None
+
+
+def _syn_real_row(i):
+    from meteorgpu import synth
+    mm, seeds, n, kw = _SYN
+    np.frombuffer(mm, np.int16).reshape(len(seeds), n)[i] = synth.synth_real(seed=int(seeds[i]), **kw)[0][:n]
+    return 0
+
+
+def _syn_iq_row(i):
+    from meteorgpu import synth
+    mm, seeds, n, kw = _SYN
+    i_, q_, _ = synth.synth_iq(int(seeds[i]), **kw)
+    row = np.frombuffer(mm, np.int16).reshape(len(seeds), 2 * n)[i]
+    row[0::2], row[1::2] = i_[:n], q_[:n]
+    return 0
+
+
+def synth_rows(kind, seeds, n, procs=SYNTH_PROCS, **kw):
+    """[len(seeds)][n] int16 (kind "real") or [len(seeds)][2n] interleaved I/Q (kind "iq") in a
+    shared anonymous mapping, one seeded recording per row, made on `procs` forked workers"""
+    import mmap
+    import multiprocessing as mp
+    global _SYN
+    width = n if kind == "real" else 2 * n
+    mm = mmap.mmap(-1, max(1, len(seeds) * width * 2))  # MAP_SHARED | MAP_ANONYMOUS
+    _SYN = (mm, list(seeds), n, kw)
+    fn = _syn_real_row if kind == "real" else _syn_iq_row
+    try:
+        if procs > 1 and len(seeds) > 1:
+            with mp.get_context("fork").Pool(min(procs, len(seeds))) as workers:
+                workers.map(fn, range(len(seeds)), chunksize=max(1, len(seeds) // (8 * procs)))
+        else:
+            for i in range(len(seeds)):
+                fn(i)
+    finally:
+        _SYN = None
+    return np.frombuffer(mm, np.int16).reshape(len(seeds), width)
+
+
+def day_seeds(day, lo, hi):
+    """C3 seeds of files [lo, hi) of day `day`: 1000 * 3 + 1440 * day + file index"""
+    return [3000 + 1440 * day + i for i in range(lo, hi)]
 
 
 def parse():
@@ -260,48 +312,65 @@ def main_live(a, world, rank, local, job_of):
 C5_BAND, C5_NOISE = (950.0, 1050.0), (-3050.0, -2950.0)  # Hz from the SDR centre (two-sided spectrum)
 
 
+def c5_geometry(a, rank, world):
+    """(n_total, s0, s1): the stream of N shards and the samples rank's frames read"""
+    from meteorgpu.iq import frame_shard
+    shard = int(C5_FS * a.c5_seconds)
+    n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
+    _, _, _, s0, s1 = frame_shard(n_total, C5_N, C5_HOP, rank, world)
+    return n_total, s0, s1
+
+
+def c5_rows(a, rank, world):
+    """the distinct seeded minutes of the stream that rank's samples lie in (minute m: synth_iq(5000 + m),
+    so the shards are pieces of one continuous stream), and the first one's sample offset"""
+    _, s0, s1 = c5_geometry(a, rank, world)
+    chunk = C5_FS * 60
+    m0, m1 = s0 // chunk, -(-s1 // chunk)
+    rows = synth_rows("iq", [5000 + m for m in range(m0, m1)], chunk, fs=C5_FS, duration_s=60.0, f0=1000.0,
+                      sigma=1000.0, rate_per_min=6, snr_db=(10.0, 30.0))
+    return rows, m0 * chunk
+
+
 def main_c5(a, world, rank, local, job_of):
     """--workload c5: the C5 line alone."""
     from meteorgpu import _lib
+    rows = c5_rows(a, rank, world)  # before any GPU call (forked workers)
     ctx = _lib.Context(local)
     job = job_of(ctx)
-    out = run_c5(a, ctx, job, rank, world)
+    out = run_c5(a, ctx, job, rank, world, rows)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if job is not None:
         job.close()
 
 
-def run_c5(a, ctx, job, rank, world):
+def run_c5(a, ctx, job, rank, world, rows):
     """BASELINE config C5: a 24 h 192 kHz I/Q stream time-sharded over the GPUs (3 h of it per
     GPU; weak scaling: the stream is 3 h x N long).  A step = the whole path on every rank:
     two-sided 4096-point power spectrogram at 75 % overlap (frame-major float32, kept in HBM),
     the per-frame band / noise dB delta, and the reference's adaptive detector over the WHOLE
     stream (meteorgpu.stream: halo, chunk-sum and shard-edge state exchanges over RCCL).
     Returns the bench line (identical on every rank but cpu_baseline, rank 0 only)."""
-    from meteorgpu import _lib, iq, stream, synth
+    from meteorgpu import _lib, iq, stream
     shard = int(C5_FS * a.c5_seconds)
-    n_total = shard * world + (C5_N - C5_HOP)  # the stream: N shards + the last frame's tail
+    n_total = c5_geometry(a, rank, world)[0]
     head_mode = "exact" if a.c5_mode == "all" else a.c5_mode
     cert_on, delta_src, _ = C5_MODES[head_mode]
     det = iq.IQShardDetector(ctx, n_total, C5_FS, C5_N, C5_N - C5_HOP, C5_BAND, C5_NOISE, 4.0, True,
                              rank=rank, world=world, seg_len=int(os.environ.get("MSD_BENCH_SEG_LEN", "8192")),
                              certify=cert_on, delta=delta_src, overlap=a.c5_overlap)
     chunk = C5_FS * 60
-    pool = []
-    for j in range(4):  # seeded 1-minute chunks: noise + meteor pings at +1 kHz, int16 I/Q interleaved
-        i_, q_, _ = synth.synth_iq(5000 + 10 * rank + j, C5_FS, 60.0, 1000.0, sigma=1000.0, rate_per_min=6,
-                                   snr_db=(10.0, 30.0))
-        z = np.empty(2 * chunk, np.int16)
-        z[0::2], z[1::2] = i_, q_
-        pool.append(z)
+    pool, first = rows  # distinct seeded minutes: noise + meteor pings at +1 kHz, int16 I/Q interleaved
+    assert first <= det.s0 and first + pool.shape[0] * chunk >= det.s1
     n = det.s1 - det.s0
-    pos, k = 0, 0
-    while pos < n:
-        m = min(chunk, n - pos)
-        det.upload(pool[k % len(pool)][: 2 * m], sample_offset=pos)
+    pos = 0
+    while pos < n:  # the rank's samples [s0, s1) minute by minute
+        g = det.s0 + pos
+        k, o = divmod(g - first, chunk)
+        m = min(chunk - o, n - pos)
+        det.upload(pool[k][2 * o: 2 * (o + m)], sample_offset=pos)
         pos += m
-        k += 1
     comm = job.comm if job is not None else stream.LocalComm()
 
     mode = [head_mode]
@@ -400,7 +469,8 @@ def run_c5(a, ctx, job, rank, world):
         "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32 spectrogram / f64 detector",
-        "data": f"synthetic: 4 seeded 1-minute 192 kHz int16 I/Q chunks (noise + pings) tiled into {hrs} per GPU",
+        "data": f"synthetic: {hrs} per GPU of one continuous 192 kHz int16 I/Q stream (noise + pings), every minute "
+                f"distinct (minute m seeded 5000 + m, SURVEY §8(d))",
         "config": {"workload": f"C5: 192 kHz I/Q stream time-sharded {hrs} per GPU ({hrs} x N long), spectrogram "
                                "4096/1024 float32 [T][4096] frame-major + per-frame band dB (950..1050 Hz vs "
                                "-3050..-2950 Hz) + adaptive detector over the whole stream (k 4, window 120 s = "
@@ -580,8 +650,20 @@ def _main():
         {"live": main_live, "c5": main_c5, "files": main_files}[a.workload](a, world, rank, local, job_of)
         return
 
-    from meteorgpu import synth
-    pool = [synth.synth_real(seed=2000 + j, fs=FS, duration_s=SECONDS, f0=1000.0)[0] for j in range(POOL)]
+    from meteorgpu.shard import shard_range
+    if a.shard_day:  # C4 strong scaling as the headline: files [lo, hi) of one day
+        lo, hi = shard_range(a.files, rank, world)
+    else:  # rank r holds day r (weak scaling)
+        lo, hi = 0, a.files
+    day = 0 if a.shard_day else rank
+    pool = synth_rows("real", day_seeds(day, lo, hi), FS * SECONDS, fs=FS, duration_s=SECONDS, f0=1000.0)
+    spool = None  # C4 after the weak-scaling line: this rank's share of day 0, made before any GPU call
+    if not a.shard_day and (world > 1 or launch.launched()):
+        slo, shi = shard_range(a.files, rank, world)
+        spool = pool[slo:shi] if day == 0 else synth_rows("real", day_seeds(0, slo, shi), FS * SECONDS, fs=FS,
+                                                          duration_s=SECONDS, f0=1000.0)
+    # the C5 line's stream, made before any GPU call as well
+    rows5 = c5_rows(a, rank, world) if not a.no_c5 and not a.shard_day else None
     mp_base = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
         # before any GPU call: the workers are forked from this process
@@ -592,12 +674,7 @@ def _main():
                              f"same path as cpu_baseline; CPU: {cpu_model()}"}
     ctx = _lib.Context(local)
     job = job_of(ctx)
-    from meteorgpu.shard import shard_range
     n = FS * SECONDS
-    if a.shard_day:  # C4 strong scaling as the headline: files [lo, hi) of one day
-        lo, hi = shard_range(a.files, rank, world)
-    else:  # rank r holds day r (weak scaling)
-        lo, hi = 0, a.files
     r = run_c3(a, ctx, job, rank, world, pool, lo, hi, a.shard_day, detail=True)
     F = hi - lo
     samples = (a.files if a.shard_day else world * F) * n
@@ -613,7 +690,8 @@ def _main():
         "scaling": "strong" if a.shard_day else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": f"synthetic: {POOL} seeded 60 s 48 kHz int16 noise+ping recordings replicated over {F} files/GPU",
+        "data": f"synthetic: {F} distinct seeded 60 s 48 kHz int16 noise+ping recordings per GPU (seed 3000 + "
+                f"1440 day + file index, SURVEY §8(d))",
         "config": {
             "workload": "C3 day batch: 1440 x 60 s 48 kHz mono int16 per GPU; STFT 1024/512 density PSD "
                         "(float32 [513][T]) + block band dB (0.2 s, n_fft 512 -> 1024-pt rFFT crop, bands 950-1050/2950-3050 Hz) + "
@@ -638,7 +716,7 @@ def _main():
         # measured after the weak-scaling line so that the driver's 1/2/4/8 runs carry both curves
         if world > 1 or job is not None:
             slo, shi = shard_range(a.files, rank, world)
-            rs = run_c3(a, ctx, job, rank, world, pool, slo, shi, True, detail=False)
+            rs = run_c3(a, ctx, job, rank, world, spool, slo, shi, True, detail=False)
             strong = {"value": round(a.files * n * a.steps / rs["elapsed"] / 1e6, 1),
                       "ms_per_step": round(rs["elapsed"] / a.steps * 1e3, 4), "files_total": a.files,
                       "files_per_gpu_max": -(-a.files // world), "detections_per_step": rs["detections"],
@@ -668,7 +746,7 @@ def _main():
         # BASELINE configs[4] (C5) in the same run, after the C3 timed region: the driver's record
         # then carries a C5 number of its own (the full line under "c5")
         try:
-            c5 = run_c5(a, ctx, job, rank, world)
+            c5 = run_c5(a, ctx, job, rank, world, rows5)
             out["c5"] = {k: c5[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "scaling",
                                             "dtype", "roofline", "kernel_ms_per_step", "detections_per_step",
                                             "state_rounds", "exact_threshold_frames", "config", "cpu_baseline",
@@ -696,8 +774,8 @@ def run_c3(a, ctx, job, rank, world, pool, lo, hi, one_day, detail):
     F = hi - lo
     bp = BatchPipeline(ctx, F, n, FS, nperseg=NPERSEG, noverlap=NOVERLAP, freq_band=BAND, noise_band=NOISE,
                        with_spectrogram=not a.no_spectrogram, concurrent=a.concurrent_stages)
-    for i in range(F):
-        bp.upload_file(i, pool[(lo + i + (0 if one_day else rank)) % POOL])
+    for i in range(F):  # pool: this rank's files [lo, hi), one row each
+        bp.upload_file(i, pool[i])
     # file i starts at minute lo + i of the day: 2025-06-01 (one day sharded) or 2025-06-(1+r) (a day per rank)
     epoch = datetime.datetime(1970, 1, 1)
     day0 = datetime.datetime(2025, 6, 1) + datetime.timedelta(days=0 if one_day else rank)

@@ -388,6 +388,26 @@ int stft_plan_make(msd_ctx *ctx, int32_t nperseg, int32_t nfft, int32_t hop, con
         for (int k = 0; k <= M; ++k) post32[k] = make_float2((float)post[k].x, (float)post[k].y);
         std::vector<float> win(nperseg);
         for (int i = 0; i < nperseg; ++i) win[i] = w32 ? w32[i] : (float)w64[i];
+        if (nperseg == nfft) {  // the window's DFT at bins 0 .. M (stft1024_kernel's mean residual)
+            double wmax = 0.0;
+            std::vector<long double> cs(nfft), sn(nfft);  // exp(-2 pi i j / N), the argument reduced exactly
+            for (int j = 0; j < nfft; ++j) {
+                const long double a = -2.0L * 3.141592653589793238462643383279502884L * j / nfft;
+                cs[j] = cosl(a);
+                sn[j] = sinl(a);
+            }
+            for (int k = 0; k <= M; ++k) {
+                long double re = 0.0L, im = 0.0L;
+                for (int i = 0, j = 0; i < nperseg; ++i, j = (j + k) & (nfft - 1)) {
+                    re += (long double)win[i] * cs[j];
+                    im += (long double)win[i] * sn[j];
+                }
+                if (k < 2) p->win_dft01[k] = make_double2((double)re, (double)im);
+                else wmax = std::max(wmax, (double)std::sqrt(re * re + im * im));
+            }
+            const double w0 = std::hypot(p->win_dft01[0].x, p->win_dft01[0].y);
+            p->win_dft_compact = w0 > 0.0 && wmax <= 1e-6 * w0;
+        }
         e = hipMalloc(&p->d_window, sizeof(float) * nperseg);
         if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(float2) * M);
         if (e == hipSuccess) e = hipMalloc(&p->d_post, sizeof(float2) * (M + 1));
@@ -587,7 +607,7 @@ int msd_block_plan_create(msd_ctx *ctx, int64_t block_size, int32_t nfft, const 
         msd_block_plan_destroy(p);
         return hip_fail(e, "block plan upload");
     }
-    if (block_i8_shape(L, p->nbins)) {  // int16 blocks on the matrix cores (block_i8.hip)
+    if (block_i8_shape(L, p->nbins) && block_i8_window(window, L)) {  // int16 blocks on the matrix cores (block_i8.hip)
         if (int rc = block_i8_build(p, window, bins.data(), p->nbins)) {
             msd_block_plan_destroy(p);
             return rc;

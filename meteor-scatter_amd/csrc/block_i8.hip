@@ -208,19 +208,29 @@ __global__ __launch_bounds__(64 * BI_WAVES, 1) void block_band_i8_kernel(const i
     }
 }
 
-// one balanced base-256 digit expansion of T (|T| <= 2^54): T = sum_b d[b] 256^(6 - b)
-void balanced_digits(int64_t T, int8_t (&d)[BI_ND]) {
+// one balanced base-256 digit expansion of T (|T| <= 2^54): T = sum_b d[b] 256^(6 - b); false if T
+// does not fit the seven digits (a carry left over)
+bool balanced_digits(int64_t T, int8_t (&d)[BI_ND]) {
     for (int b = BI_ND - 1; b >= 0; --b) {
         int64_t r = ((T % 256) + 256) % 256;
         if (r >= 128) r -= 256;
         d[b] = (int8_t)r;
         T = (T - r) / 256;
     }
+    return T == 0;
 }
 
 }  // namespace
 
 bool block_i8_shape(int64_t L, int nbins) { return (L == 256 || L == 512 || L == 1024) && nbins >= 1 && nbins <= BI_MAXBINS; }
+
+// the quantisation round(w cos * 2^54) fits seven balanced digits and margin._i8_chain's 2^-55 bound
+// holds for |w_n| <= 1 (every window scipy / numpy make); other windows keep the Goertzel kernel
+bool block_i8_window(const double *window, int64_t L) {
+    for (int64_t n = 0; n < L; ++n)
+        if (!std::isfinite(window[n]) || std::fabs(window[n]) > 1.0) return false;
+    return true;
+}
 
 // the B fragments and column constants of block_band_i8_kernel for the plan's window and bins
 int block_i8_build(msd_block_plan *p, const double *window, const int *bins, int nbins) {
@@ -237,7 +247,7 @@ int block_i8_build(msd_block_plan *p, const double *window, const int *bins, int
             const long double v = (long double)window[n] * ((cp & 1) ? -sinl(a) : cosl(a));
             const int64_t T = llroundl(v * 0x1p54L);
             int8_t d[BI_ND];
-            balanced_digits(T, d);
+            if (!balanced_digits(T, d)) return fail(MSD_ERR_INVALID, "block_i8: coefficient beyond 7 digits");
             for (int b = 0; b < BI_ND; ++b) {
                 dig[((size_t)b * 16 + cp) * L + n] = d[b];
                 init[b * 16 + cp] += 128 * d[b];

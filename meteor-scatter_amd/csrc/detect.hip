@@ -127,14 +127,20 @@ __global__ __launch_bounds__(DT_THREADS, 4) void detect_kernel(const double *__r
         for (int64_t i = tid; i < nb; i += DT_THREADS) c_delta[i] = d[i];
         __syncthreads();
     }
-    const double *src = whole ? c_delta : d;
 
     // ---- 1. global threshold (main.py:399-400, :464-466) ----
-    const double s1 = wg_np_sum(ArrRef{src}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
-    const double gmean = s1 / (double)nb;
-    const double s2 = wg_np_sum(SqDevRef{src, gmean}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
-    const double gstd = sqrt(s2 / (double)nb);
-    const double thr0 = gmean + cfg.k_std * gstd;
+    // Instantiated once on the LDS copy and once on global memory, never on a pointer that may be
+    // either: a generic pointer is read with flat instructions, which pick LDS or global from the
+    // address register alone, and a loop pointer the compiler displaces below an LDS object then
+    // leaves the LDS aperture (the round-5 fault; tests/test_build_check.py).
+    auto global_thr = [&](const double *src) {
+        const double s1 = wg_np_sum(ArrRef{src}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
+        const double gmean = s1 / (double)nb;
+        const double s2 = wg_np_sum(SqDevRef{src, gmean}, nb, leaf_off, leaf_sum, &s_nleaf, P.leaf_cap);
+        const double gstd = sqrt(s2 / (double)nb);
+        return gmean + cfg.k_std * gstd;
+    };
+    const double thr0 = whole ? global_thr(c_delta) : global_thr(d);
 
     // ---- 2. fresh adaptive thresholds (main.py:475-480), all blocks in parallel ----
     double *tf = thr + f * P.ld;
@@ -271,7 +277,9 @@ __global__ __launch_bounds__(DT_THREADS, 4) void detect_kernel(const double *__r
     for (int64_t c = tid; c < nd; c += DT_THREADS) {
         const int64_t a = df[c].start, b = df[c].stop;
         const int64_t n = b - a;
-        df[c].db = np_sum(ArrRef{src}, a, n) / (double)n;  // the staged file (LDS) when it fits one chunk
+        // the staged file (LDS) when it fits one chunk; each branch on its own address space (§1 above)
+        const double sum = whole ? np_sum(ArrRef{c_delta}, a, n) : np_sum(ArrRef{d}, a, n);
+        df[c].db = sum / (double)n;
         if (P.has_hist) {
             const double t_start = (double)a * P.block_sec;
             const int64_t us = llrint(t_start * 1e6);

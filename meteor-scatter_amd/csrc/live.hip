@@ -207,7 +207,7 @@ struct LiveArgs {
 
 // Python's builtin min/max over a list (first element kept unless a later one compares
 // strictly less / greater — NaN behaves as CPython's does)
-__device__ __forceinline__ void py_minmax(const double *v, int64_t a, int64_t e, double &mn, double &mx) {
+__device__ __forceinline__ void py_minmax(gdouble_t *v, int64_t a, int64_t e, double &mn, double &mx) {
     mn = v[a];
     mx = v[a];
     for (int64_t i = a + 1; i < e; ++i) {
@@ -222,54 +222,59 @@ struct LiveScan {
     int64_t trig = 0, cnt = 0;
 };
 
-// numpy mean/std of over[b, b+n): from the staged chunk when the run lies inside it (offsets,
-// not a shifted LDS pointer: that would leave the LDS aperture once made generic)
-__device__ __forceinline__ void hist_stats(const double *ov, const double *s_ov, int64_t c0, int64_t b, int64_t n,
-                                           double &mean, double &sd, double *mn, double *mx) {
-    const bool in = b >= c0;
-    const double *src = in ? s_ov : ov;
-    const int64_t sb = in ? b - c0 : b;
-    np_mean_std(src, sb, n, mean, sd);
-    if (mn) py_minmax(src, sb, sb + n, *mn, *mx);
+// numpy mean/std of over[b, b+n), read from global memory as such (global loads: the event handlers
+// are out of line, and a generic pointer there would be read with flat instructions, np_reduce.h)
+__device__ __forceinline__ void hist_stats(const double *ov, int64_t b, int64_t n, double &mean, double &sd,
+                                           double *mn, double *mx) {
+    np_mean_std_global(ov, b, n, mean, sd);
+    if (mn) py_minmax(as_global(ov), b, b + n, *mn, *mx);
 }
 
+// The two event handlers are out of line (they run once per meteor; inlined, their numpy sums
+// would be copied into every scan).  The scan state travels by value and the history is read
+// through global loads: no generic pointer -- to the caller's scratch, to LDS or to global memory --
+// reaches them, so they hold no flat instruction (np_reduce.h, tests/test_build_check.py).
+
 // Detection → Tracking (processor.py:462-472): locked_threshold = thr + 0 * history_std
-__device__ __noinline__ void live_trigger(LiveScan &sc, const double *ov, const double *s_ov, int64_t c0, int64_t i,
-                                          double t, double t0, const msd_live_cfg &C) {
-    const int64_t W = C.avg_win_blocks;
+__device__ __noinline__ LiveScan live_trigger(LiveScan sc, const double *ov, int64_t i, double t, double t0,
+                                              int64_t W) {
     const int64_t h0 = W > 0 ? (i - W > 0 ? i - W : 0) : 0;
     double hm = NAN, hs = NAN;
-    if (i - h0 > 0) hist_stats(ov, s_ov, c0, h0, i - h0, hm, hs, nullptr, nullptr);
+    if (i - h0 > 0) hist_stats(ov, h0, i - h0, hm, hs, nullptr, nullptr);
     sc.lock = t + 0.0 * hs;
     sc.t_start = t0;
     sc.trig = i;
     sc.state = 2;
+    return sc;
 }
 
 // Tracking ends (processor.py:474-504): history = over[trig+1 .. i]
-__device__ __noinline__ void live_close(LiveScan &sc, const double *ov, const double *s_ov, int64_t c0, int64_t i,
-                                        double t0, const msd_live_cfg &C, msd_meteor *out, int64_t cap, bool writer) {
+__device__ __noinline__ LiveScan live_close(LiveScan sc, const double *ov, int64_t i, double t0, double min_db_mean,
+                                            double min_dur_sec, double wait_sec, msd_meteor *out, int64_t cap,
+                                            bool writer) {
     const double dur = t0 - sc.t_start;
     double hm, hs, mn, mx;
-    hist_stats(ov, s_ov, c0, sc.trig + 1, i - sc.trig, hm, hs, &mn, &mx);
-    if (hm >= C.min_db_mean && dur >= C.min_dur_sec) {
+    hist_stats(ov, sc.trig + 1, i - sc.trig, hm, hs, &mn, &mx);
+    if (hm >= min_db_mean && dur >= min_dur_sec) {
         if (writer && sc.cnt < cap) {
-            msd_meteor m;
-            m.start_block = sc.trig;
-            m.stop_block = i;
-            m.time_start = sc.t_start;
-            m.time_stop = t0;
-            m.duration = dur;
-            m.db_min = mn;
-            m.db_max = mx;
-            m.db_mean = hm;
-            m.db_std = hs;
-            out[sc.cnt] = m;
+            typedef __attribute__((address_space(1))) int64_t gi64;
+            typedef __attribute__((address_space(1))) double gf64;
+            msd_meteor *m = out + sc.cnt;  // fields stored through global pointers (global_store)
+            *(gi64 *)&m->start_block = sc.trig;
+            *(gi64 *)&m->stop_block = i;
+            *(gf64 *)&m->time_start = sc.t_start;
+            *(gf64 *)&m->time_stop = t0;
+            *(gf64 *)&m->duration = dur;
+            *(gf64 *)&m->db_min = mn;
+            *(gf64 *)&m->db_max = mx;
+            *(gf64 *)&m->db_mean = hm;
+            *(gf64 *)&m->db_std = hs;
         }
         ++sc.cnt;
     }
     sc.state = 1;
-    sc.until = t0 + C.after_tracking_wait_sec;
+    sc.until = t0 + wait_sec;
+    return sc;
 }
 
 // processor.py:391: block_db_2_ms = block_db_ms - np.mean([n1, n2])
@@ -383,9 +388,10 @@ __global__ __launch_bounds__(LV_SEGS * 64) void live_detect_kernel(const double 
                 sc.lock = -1.0;
                 sc.until = -1.0;
             } else if (sc.state == 1) {
-                live_trigger(sc, ov, ov, 0, e, te, t0e, C);
+                sc = live_trigger(sc, ov, e, te, t0e, C.avg_win_blocks);
             } else {
-                live_close(sc, ov, ov, 0, e, t0e, C, out + f * A.cap, A.cap, emit && lane == 0);
+                sc = live_close(sc, ov, e, t0e, C.min_db_mean, C.min_dur_sec, C.after_tracking_wait_sec, out + f * A.cap,
+                                A.cap, emit && lane == 0);
             }
             k = e + 1;
         }

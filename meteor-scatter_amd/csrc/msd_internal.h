@@ -113,6 +113,13 @@ struct msd_stft_plan {
     int64_t *d_sched = nullptr;
     int64_t sched_cap = 0, sched_total = -1, sched_wgs = -1, sched_n = 0;
     unsigned long long *d_ticket = nullptr;
+    // stft1024_kernel, integer samples: the frame mean m = tot / 1024 = a + b / 1024 (a = floor) comes
+    // off as the exact integer a before the FFT and as b / 1024 times the window's DFT after it, which
+    // is exact when that DFT vanishes past bin 1 (periodic Hann: W_0 = N/2, W_1 = -N/4).  win_dft01:
+    // W_0, W_1 of the float32 window in float64; win_dft_compact: max |W_k|, 2 <= k <= M, below
+    // 1e-6 |W_0| (else integer input takes the generic kernel's exact two-part mean)
+    double2 win_dft01[2] = {};
+    int win_dft_compact = 0;
 };
 
 struct msd_block_plan {
@@ -263,6 +270,7 @@ int launch_stft_any(msd_stft_plan *plan, const void *x, int dtype, const int64_t
 int launch_stft1024(msd_stft_plan *plan, const void *x, int dtype, const int64_t *off, const int64_t *len,
                     int64_t nfiles, float *out, int64_t ld);
 bool block_i8_shape(int64_t L, int nbins);
+bool block_i8_window(const double *window, int64_t L);
 int block_i8_build(msd_block_plan *p, const double *window, const int *bins, int nbins);
 int launch_block_i8(msd_block_plan *p, const int16_t *x, const int64_t *off, const int64_t *len, int64_t nfiles,
                     int64_t max_blocks);

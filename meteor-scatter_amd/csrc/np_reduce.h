@@ -161,6 +161,29 @@ struct SqDevRef {
     }
 };
 
+// Global memory typed as such (address space 1), for data read by out-of-line device functions.  A
+// pointer that reaches a callee is generic, and generic loads are flat instructions, which pick LDS,
+// scratch or global from the high bits of the address register alone -- the instruction's offset is
+// not looked at.  A loop pointer the compiler displaces below an LDS object (base - 64 with offsets
+// +128 ..) therefore leaves the LDS aperture: round 5's one GPU fault.  Out-of-line
+// code reads global data through these (global_load) and never receives an LDS pointer;
+// tests/test_build_check.py holds every function of the library to zero flat instructions.
+typedef const __attribute__((address_space(1))) double gdouble_t;
+__device__ __forceinline__ gdouble_t *as_global(const double *p) { return (gdouble_t *)p; }
+struct GArrRef {
+    gdouble_t *p;
+    __device__ double operator()(int64_t i) const { return p[i]; }
+};
+struct GSqDevRef {
+    gdouble_t *p;
+    double mean;
+    __device__ double operator()(int64_t i) const {
+#pragma clang fp contract(off)
+        const double d = p[i] - mean;
+        return d * d;
+    }
+};
+
 // numpy mean/std of p[base .. base+n), n <= NP_ITER_MAX[DMAX], by np_pairwise_iter
 template <int DMAX>
 __device__ __forceinline__ void np_mean_std_iter(const double *p, int64_t base, int n, double &mean, double &std) {
@@ -174,6 +197,18 @@ __device__ __forceinline__ void np_mean_std_iter(const double *p, int64_t base, 
 // numpy mean/std of p[base .. base+n).  n <= 128 (one pairwise leaf) stays inline: the general
 // np_sum is a large out-of-line function whose call and instruction-cache misses cost more
 // than the sum itself in the event handlers of the live scan (live.hip)
+// numpy mean/std of global p[base .. base+n) through global loads (GArrRef): for out-of-line callers
+__device__ __forceinline__ void np_mean_std_global(const double *p, int64_t base, int64_t n, double &mean,
+                                                   double &std) {
+#pragma clang fp contract(off)
+    const GArrRef a{as_global(p)};
+    const double s = n <= 128 ? np_sum_small(a, base, n) : np_sum(a, base, n);
+    mean = s / (double)n;
+    const GSqDevRef q{a.p, mean};
+    const double v = n <= 128 ? np_sum_small(q, base, n) : np_sum(q, base, n);
+    std = sqrt(v / (double)n);
+}
+
 __device__ __forceinline__ void np_mean_std(const double *p, int64_t base, int64_t n, double &mean, double &std) {
 #pragma clang fp contract(off)
     if (n <= 128) {

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     int64_t tiles_per_file, int64_t ntiles, int64_t tiles_per_wg, int hop, float wscale, int detrend,
     const float *__restrict__ g_win, const float2 *__restrict__ g_tw, const float2 *__restrict__ g_post,
     float *__restrict__ out, int64_t ld, const int64_t *__restrict__ sched, int64_t nchunks,
-    unsigned long long *__restrict__ ticket) {
+    unsigned long long *__restrict__ ticket, float2 dcw0, float2 dcw1) {
     using IO = PairIO<T>;
     using raw_t = typename IO::raw_t;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -270,6 +270,10 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
     // the table entries as ds_read_b128 (two float2 each) / ds_read_b64
     auto tab4 = [&](int c) { return *reinterpret_cast<const float4 *>(tab + c); };
     const int pi = pi_of(l);
+    // integer samples: the coefficient of the mean's fractional part b / 1024 at this lane's bin of
+    // register 0 -- 2 ws W_k / 1024 at k = 0 (lane pi = 0) and k = 1 (pi = 1), zero elsewhere
+    // (launch_fast_t: the window's DFT vanishes past bin 1)
+    const float2 dcw = pi == 0 ? dcw0 : (pi == 1 ? dcw1 : make_float2(0.f, 0.f));
     __syncthreads();
 
     __shared__ int64_t slot[2];  // DYN: drawn chunk tickets
@@ -283,6 +287,9 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         tb = uniform_i64(sched[k]);
         te = uniform_i64(sched[k + 1]);
         if (tid == 0) slot[1] = (int64_t)atomicAdd(ticket, 1ull);  // the chunk after
+        // published before any wave reads it: a one-tile first chunk (ntiles = 1, the schedule's only
+        // chunk below cmin) reads slot[1] at its first loop head, with no tile barrier in between
+        __syncthreads();
         par = 1;
     } else {
         tb = (int64_t)blockIdx.x * tiles_per_wg;
@@ -367,6 +374,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
         const bool b_cur = b_ok;
         float2 v[2][8], wv[8];
         // ---- detrend (consumes raw); the window is applied inside pass 1
+        float rb[2] = {0.f, 0.f};  // integer samples: the mean's fractional part, times 1024
         {
             float mean[2], xr[2] = {0.f, 0.f};
 #pragma unroll
@@ -385,13 +393,13 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                     s = row_sum_i(s);
                     const int tot = __builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16) +
                                     __builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48);
-                    // float(tot) rounds tot to 24 bits exactly as rounding tot / 1024 would (a
-                    // power-of-two scale), so this equals float((double)tot / 1024) without FP64.
-                    // It is the exact mean while |tot| < 2^24, i.e. |mean| < 16384 (half of int16 full
-                    // scale); beyond, the detrended samples keep a common offset below 2^-10.  The
-                    // two-part mean of the C5 kernel (hi + lo behind a wave-uniform branch) measured
-                    // +7.9 % on this loop (tools/stft_ab, round 5), so it stays single here.
-                    mean[q] = detrend ? (float)tot * (1.0f / 1024.0f) : 0.f;
+                    // the mean tot / 1024 = a + b / 1024 exactly (a = floor, 0 <= b < 1024): x - a is
+                    // an exact integer (|x - a| < 2^16), so the frame is detrended by one subtraction
+                    // at any offset, and b / 1024 times the window's DFT comes off bins 0 and 1 after
+                    // the FFT (post pass).  (float(tot) / 1024, rounds 1-5, was exact only while
+                    // |tot| < 2^24; the two-part mean hi + lo measured +7.9 % on this loop.)
+                    mean[q] = detrend ? (float)(tot >> 10) : 0.f;
+                    rb[q] = detrend ? (float)(tot & 1023) : 0.f;
                 } else {
                     // float samples: the frame's first sample (lane 0's first value) comes off before
                     // the float sums, so that they accumulate the variation and not a DC offset (a
@@ -433,6 +441,7 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
             if (SH && !b_cur) {  // no second frame: its tile column must be zero (the loads were not)
 #pragma unroll
                 for (int r = 0; r < 8; ++r) v[1][r] = make_float2(0.f, 0.f);
+                rb[1] = 0.f;
             }
         }
         // ---- prefetch the next tile's frame pair into the (now free) sample registers
@@ -544,7 +553,14 @@ __global__ __launch_bounds__(F_NW * 64, 1) void stft1024_kernel(
                 const float2 e = make_float2(z.x + m.x, z.y - m.y);
                 const float2 o = make_float2(z.y + m.y, m.x - z.x);  // -i (z - conj m)
                 const float2 t = cmul(wk, o);
-                const float2 X1 = cadd(e, t), X2 = csub(e, t);
+                float2 X1 = cadd(e, t);
+                const float2 X2 = csub(e, t);
+                if constexpr (IO::kInt) {
+                    if (r == 0) {  // bins 0, 1: X' -= (b / 1024) 2 ws W_k, the mean's fractional part
+                        X1.x = __builtin_fmaf(-rb[q], dcw.x, X1.x);
+                        X1.y = __builtin_fmaf(-rb[q], dcw.y, X1.y);
+                    }
+                }
                 pa[q][r] = X1.x * X1.x + X1.y * X1.y;
                 pb[q][r] = X2.x * X2.x + X2.y * X2.y;
                 if (r == 0) {
@@ -600,6 +616,10 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
     int64_t wgs = cus;  // one 16-wave workgroup per CU (LDS-bound residency)
     if (wgs > ntiles) wgs = ntiles;
     const float ws = static_cast<float>(std::sqrt(p->scale * 0.5));
+    // the mean's fractional part b / 1024 on bins 0, 1: X' = 2 ws X, so the coefficient is 2 ws W_k / 1024
+    const double cf = 2.0 * std::sqrt(p->scale * 0.5) / 1024.0;
+    const float2 dcw0 = make_float2((float)(cf * p->win_dft01[0].x), (float)(cf * p->win_dft01[0].y));
+    const float2 dcw1 = make_float2((float)(cf * p->win_dft01[1].x), (float)(cf * p->win_dft01[1].y));
     if (p->ctx->stft_sched == 2) {
         // guided schedule of tile chunks (>= 2 tiles), rebuilt when (ntiles, wgs) change
         auto dkern = wide ? (sh ? stft1024_kernel<T, 1, PairIO<T>::kInt, true> : stft1024_kernel<T, 1, false, true>)
@@ -635,7 +655,7 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
         MSD_HIP(hipMemsetAsync(p->d_ticket, 0, sizeof(unsigned long long), p->ctx->stream));
         hipLaunchKernelGGL(dkern, dim3((unsigned)wgs), dim3(F_NW * 64), F_LDS, p->ctx->stream, static_cast<const T *>(x),
                            off, len, tiles_per_file, ntiles, (int64_t)0, p->hop, ws, p->detrend, p->d_window, p->d_tw,
-                           p->d_post, out, ld, p->d_sched, p->sched_n, p->d_ticket);
+                           p->d_post, out, ld, p->d_sched, p->sched_n, p->d_ticket, dcw0, dcw1);
         MSD_HIP(hipGetLastError());
         return MSD_OK;
     }
@@ -643,7 +663,7 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
     wgs = (ntiles + per - 1) / per;
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(F_NW * 64), F_LDS, p->ctx->stream, static_cast<const T *>(x),
                        off, len, tiles_per_file, ntiles, per, p->hop, ws, p->detrend, p->d_window, p->d_tw, p->d_post,
-                       out, ld, nullptr, (int64_t)0, nullptr);
+                       out, ld, nullptr, (int64_t)0, nullptr, dcw0, dcw1);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }
@@ -654,6 +674,9 @@ int launch_fast_t(msd_stft_plan *p, const void *x, const int64_t *off, const int
 int launch_stft1024(msd_stft_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len,
                     int64_t nfiles, float *out, int64_t ld) {
     if (p->nperseg != 1024 || (p->hop & 1)) return 0;
+    // integer samples need a window whose DFT vanishes past bin 1 (the mean's fractional part is
+    // corrected on bins 0, 1 only); others take the generic kernel's exact two-part mean
+    if ((dtype == MSD_I16 || dtype == MSD_U8) && p->detrend && !p->win_dft_compact) return 0;
     int rc;
     switch (dtype) {
         case MSD_I16: rc = launch_fast_t<int16_t>(p, x, off, len, nfiles, out, ld); break;

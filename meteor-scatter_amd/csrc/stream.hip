@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void chunk_sums_kernel(const double *__restric
     const int64_t g = (first_chunk + c) * CHUNK;
     const int64_t m = n_total - g < CHUNK ? n_total - g : CHUNK;
     const double *p = x + (g - x0);
-    const double r = SQ ? wave_chunk_sum(SqDevRef{p, mean}, 0, m) : wave_chunk_sum(ArrRef{p}, 0, m);
+    const double r = SQ ? wave_chunk_sum(GSqDevRef{as_global(p), mean}, 0, m) : wave_chunk_sum(GArrRef{as_global(p)}, 0, m);
     if (lane == 0) out[c] = r;
 }
 
@@ -335,11 +335,18 @@ struct FreshParams {
     double eps_scale; // test hook (MSD_STREAM_EPS_SCALE): widens the bound, more frames made exact
 };
 
+// record i of the program through a pointer typed with its address space (LDS or global int32s, so
+// that the loads are ds_read / global_load, never flat: np_reduce.h)
+template <typename IntPtr>
+__device__ __forceinline__ int4 load_rec(IntPtr recs, int i) {
+    return make_int4(recs[4 * i], recs[4 * i + 1], recs[4 * i + 2], recs[4 * i + 3]);
+}
+
 // one pass of the program over this lane's 8 frames: out[f] = numpy np.sum of the window of frame f
 // (SQ: of (x - mean[f])^2)
-template <bool SQ>
+template <bool SQ, typename RecPtr>
 __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t xbase, int64_t x_len,
-                                           const int4 *recs, int nleaf, double *stage,
+                                           RecPtr recs, int nleaf, double *stage,
                                            const double (&mean)[FR_F], double (&out)[FR_F]) {
     const int tid = threadIdx.x;
     // 8 frames: the pending partial sums live in scratch (a runtime-indexed array; 8 x 7 doubles
@@ -383,14 +390,14 @@ __device__ __forceinline__ void fresh_pass(const double *__restrict__ x, int64_t
         }
     };
     int buf = 0;
-    int4 cur = recs[0];
+    int4 cur = load_rec(recs, 0);
     fetch(cur.x);
     commit(stage);
     __syncthreads();
     for (int li = 0; li < nleaf; ++li) {
         // prefetch the following leaf while this one is summed
         const bool has_next = li + 1 < nleaf;
-        const int4 nxt = has_next ? recs[li + 1] : cur;
+        const int4 nxt = has_next ? load_rec(recs, li + 1) : cur;
         if (has_next) fetch(nxt.x);
         const int len = cur.y;
         const double *st = stage + buf * FR_PADDED;
@@ -516,12 +523,18 @@ __global__ __launch_bounds__(FR_THREADS) void fresh_kernel(const double *__restr
     const bool in_lds = P.nleaf <= FR_MAXREC_LDS;
     if (in_lds)
         for (int i = threadIdx.x; i < P.nleaf; i += FR_THREADS) s_rec[i] = prog[i];
-    const int4 *recs = in_lds ? s_rec : prog;
     __syncthreads();
-    fresh_pass<false>(x, xbase, P.x_len, recs, P.nleaf, stage, mean, s);
+    // the two passes instantiated on the LDS copy and on global memory, never on a pointer that may
+    // be either (a generic pointer is read with flat instructions: np_reduce.h)
+    // (typed pointers: the compiler may merge the two copies, but not loads of different address spaces)
+    auto passes = [&](auto recs) {
+        fresh_pass<false>(x, xbase, P.x_len, recs, P.nleaf, stage, mean, s);
 #pragma unroll
-    for (int f = 0; f < FR_F; ++f) mean[f] = s[f] / (double)P.W;
-    fresh_pass<true>(x, xbase, P.x_len, recs, P.nleaf, stage, mean, s);
+        for (int f = 0; f < FR_F; ++f) mean[f] = s[f] / (double)P.W;
+        fresh_pass<true>(x, xbase, P.x_len, recs, P.nleaf, stage, mean, s);
+    };
+    if (in_lds) passes((const __attribute__((address_space(3))) int *)s_rec);
+    else passes((const __attribute__((address_space(1))) int *)prog);
 #pragma unroll
     for (int f = 0; f < FR_F; ++f) {
         const int64_t j = j0 + f;
@@ -764,8 +777,8 @@ __global__ __launch_bounds__(256) void fresh_short_kernel(const double *__restri
         const int64_t i = P.frame0 + j;
         if (i < P.F0) continue;
         const int64_t base = P.n_tail + j - i;  // x index of global frame 0 = n_tail - frame0
-        const double m = wave_np_sum(ArrRef{x}, base, i) / (double)i;
-        const double v = wave_np_sum(SqDevRef{x, m}, base, i);
+        const double m = wave_np_sum(GArrRef{as_global(x)}, base, i) / (double)i;
+        const double v = wave_np_sum(GSqDevRef{as_global(x), m}, base, i);
         if (lane == 0) fresh[j] = m + P.k * sqrt(v / (double)i);
     }
 }
@@ -791,8 +804,8 @@ __global__ __launch_bounds__(256) void fresh_list_kernel(const double *__restric
         const int64_t nch = (len + NP_BUFSIZE - 1) / NP_BUFSIZE;
         if (nch > FL_MAXCH) {
             if (w == 0) {
-                const double m = wave_np_sum(ArrRef{x}, base, len) / (double)len;
-                const double v = wave_np_sum(SqDevRef{x, m}, base, len);
+                const double m = wave_np_sum(GArrRef{as_global(x)}, base, len) / (double)len;
+                const double v = wave_np_sum(GSqDevRef{as_global(x), m}, base, len);
                 if (lane == 0) {
                     fresh[j] = m + P.k * sqrt(v / (double)len);
                     exact[j] = 1;
@@ -802,7 +815,7 @@ __global__ __launch_bounds__(256) void fresh_list_kernel(const double *__restric
         }
         auto chunk_len = [&](int64_t c) { return len - c * NP_BUFSIZE < NP_BUFSIZE ? len - c * NP_BUFSIZE : NP_BUFSIZE; };
         for (int64_t c = w; c < nch; c += 4) {
-            const double r = wave_chunk_sum(ArrRef{x}, base + c * NP_BUFSIZE, chunk_len(c));
+            const double r = wave_chunk_sum(GArrRef{as_global(x)}, base + c * NP_BUFSIZE, chunk_len(c));
             if (lane == 0) csum[0][c] = r;
         }
         __syncthreads();
@@ -810,7 +823,7 @@ __global__ __launch_bounds__(256) void fresh_list_kernel(const double *__restric
         for (int64_t c = 0; c < nch; ++c) s += csum[0][c];
         const double m = s / (double)len;
         for (int64_t c = w; c < nch; c += 4) {
-            const double r = wave_chunk_sum(SqDevRef{x, m}, base + c * NP_BUFSIZE, chunk_len(c));
+            const double r = wave_chunk_sum(GSqDevRef{as_global(x), m}, base + c * NP_BUFSIZE, chunk_len(c));
             if (lane == 0) csum[1][c] = r;
         }
         __syncthreads();
@@ -1179,7 +1192,7 @@ __global__ void db_kernel(const double *__restrict__ x, int64_t x0, msd_det *__r
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const int64_t a = d[j].start, m = d[j].stop - d[j].start;
-    d[j].db = np_sum(ArrRef{x}, a - x0, m) / (double)m;
+    d[j].db = np_sum(GArrRef{as_global(x)}, a - x0, m) / (double)m;
 }
 
 }  // namespace

@@ -261,3 +261,37 @@ def test_block_i8_ragged_batch(fs, bs, n_fft, band, noise):
         ref = O.block_powers_ref(f, fs, bs, band, noise, n_fft)
         for j in range(3):
             np.testing.assert_allclose(got[j][i, :k], ref[j], rtol=0, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_block_window_beyond_unit_takes_goertzel():
+    """the int8 coefficients are round(w cos * 2^54) in seven balanced digits, which holds
+    for |w_n| <= 1 only.  A plan whose window exceeds that (1.5 x Hann here) keeps the float64
+    Goertzel kernel: the default launch is bit-identical to MSD_OPT_BLOCK_GOERTZEL, and both match
+    numpy's rFFT band energies of the same window within 1e-9 dB"""
+    from meteorgpu import _lib, dsp
+    fs, bs, n_fft, band, noise = 48000, 0.2, 512, (950, 1050), (2950, 3050)
+    B, nfft = int(fs * bs), 2 * n_fft
+    L = min(B, nfft)
+    bb, nb = dsp.band_bins(nfft, fs, band), dsp.band_bins(nfft, fs, noise)
+    from meteorgpu import synth
+    x, _ = synth.synth_real(seed=31, fs=fs, duration_s=6.0, f0=1000.0, rate_per_min=20)
+    w = 1.5 * dsp.hanning_sym(B)[:L]
+    ctx = dsp.context(0)
+    plan = _lib.BlockPlan(ctx, B, nfft, w, bb, nb)
+    try:
+        got = plan.run(x)
+        ctx.set_option(_lib.OPT_BLOCK_GOERTZEL, 1)
+        ref_g = plan.run(x)
+    finally:
+        ctx.set_option(_lib.OPT_BLOCK_GOERTZEL, 0)
+        plan.close()
+    for a, b in zip(got, ref_g):
+        np.testing.assert_array_equal(a, b)
+    nblk = x.size // B
+    X = np.fft.rfft(x[: nblk * B].reshape(nblk, B)[:, :L].astype(np.float64) * w, n=nfft)
+    P = np.abs(X) ** 2
+    eb = 10 * np.log10(P[:, bb[0]: bb[1] + 1].sum(axis=1) + 1e-12)
+    en = 10 * np.log10(P[:, nb[0]: nb[1] + 1].sum(axis=1) + 1e-12)
+    np.testing.assert_allclose(got[0], eb, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(got[1], en, rtol=0, atol=1e-9)

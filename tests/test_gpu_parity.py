@@ -240,17 +240,16 @@ def test_spectrogram_vs_scipy(case):
     assert _frame_err(S, Sr) <= SPEC_TOL
 
 
-@pytest.mark.parametrize("dc,sigma", [(700, 600.0), (700, 3.0), (12000, 3.0), (-16000, 30.0), (-30000, 30.0)])
+@pytest.mark.parametrize("dc,sigma", [(700, 600.0), (700, 3.0), (12000, 3.0), (-16000, 30.0), (-30000, 30.0),
+                                      (30000, 30.0), (-32000, 3.0), (32000, 3.0)])
 @pytest.mark.parametrize("N,nov", [(1024, 512), (2048, 1024), (256, 128)])
 def test_spectrogram_dc_offset(dc, sigma, N, nov):
     """a DC offset on the int16 audio (tests/test_iq.py's offset-700 case, and large offsets over quiet
-    noise): scipy's spectrogram holds per frame and at bins 0, 1 -- where a residual of the mean lands --
-    against each frame's mean power.  stft1024_kernel (1024 / 512, C3) subtracts float(sum) / 1024, the
-    exact mean while |mean| < 16384; the generic kernel (stft.hip) subtracts an exact two-part mean at
-    any offset.  (stft1024 at |mean| >= 16384, half of full scale, keeps a common offset < 2^-10 per
-    sample: DESIGN.md §4.1.)"""
-    if N == 1024 and abs(dc) >= 16384:
-        pytest.skip("stft1024_kernel: exact mean below |mean| 16384 only (DESIGN.md §4.1)")
+    noise, up to +-32000 over sigma 3): scipy's spectrogram holds per frame and at bins 0, 1 -- where a
+    residual of the mean lands -- against each frame's mean power.  stft1024_kernel (1024 / 512, C3)
+    subtracts the mean's exact integer part before the FFT and its fractional part times the window's
+    DFT from bins 0, 1 after it (round 6); the generic kernel (stft.hip) subtracts an
+    exact two-part mean.  Both are exact at any offset."""
     rng = np.random.default_rng(abs(dc) + N)
     n = 48000 * 2
     t = np.arange(n) / 48000
@@ -665,3 +664,45 @@ def test_stft1024_chunked_schedule_identical(hop_case):
         finally:
             ctx.close()
     np.testing.assert_array_equal(out[1], out[2])
+
+
+@pytest.mark.parametrize("frames", [1, 5, 32, 33])
+def test_stft1024_chunked_schedule_single_tile(frames):
+    """MSD_OPT_STFT_SCHED = 2 on one short file: one or two 32-frame tiles, so the guided schedule's only
+    chunk holds a single tile (the first chunk's second ticket must be published before the
+    first loop head reads it) -- identical to the static launch and to scipy"""
+    from meteorgpu import _lib
+    from scipy.signal import spectrogram as sp_spec
+    base = dsp.context(0)
+    rng = np.random.default_rng(frames)
+    fs = 48000
+    n = 1024 + 512 * (frames - 1)
+    x = rng.integers(-9000, 9000, n).astype(np.int16)
+    _, _, R = sp_spec(x, fs=fs, window="hann", nperseg=1024, noverlap=512, nfft=1024, scaling="density", mode="psd")
+    out = {}
+    for sched in (1, 2):
+        ctx = base.sibling()
+        try:
+            ctx.set_option(_lib.OPT_STFT_SCHED, sched)
+            w = dsp.hann_periodic(1024).astype(np.float32)
+            plan = _lib.StftPlan(ctx, 1024, 512, w, float(1.0 / (fs * (w.astype(np.float64) ** 2).sum())))
+            ld = (frames + 31) // 32 * 32
+            d_x, d_off, d_len = ctx.alloc(2 * n), ctx.alloc(8), ctx.alloc(8)
+            d_x.upload(x)
+            d_off.upload(np.zeros(1, np.int64))
+            d_len.upload(np.array([n], np.int64))
+            d_out = ctx.alloc(4 * 513 * ld)
+            for _ in range(3):
+                plan.run_dev(d_x, np.int16, d_off, d_len, 1, frames, d_out, ld)
+                S = np.empty((513, ld), np.float32)
+                d_out.download(S)
+                out.setdefault(sched, S)
+                np.testing.assert_array_equal(S, out[sched])
+            for b in (d_x, d_off, d_len, d_out):
+                b.free()
+            plan.close()
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(out[1], out[2])
+    assert not out[1][:, frames:].any()
+    assert _frame_err(out[1][:, :frames], R) <= SPEC_TOL
