@@ -119,6 +119,8 @@ def parse():
                     "(the GPU box's CPU share is 16)")
     ap.add_argument("--no-spectrogram", action="store_true", help="detect-only mode (not the headline)")
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 run appended to the line (key \"c5\")")
+    ap.add_argument("--no-live", action="store_true", help="c3: skip the live-detector run appended to the line "
+                    "(key \"live\")")
     ap.add_argument("--c5-mode", choices=("all",) + tuple(C5_MODES), default="all",
                     help="C5 decisions: exact = the drop-in default (proc_iq_samples): every frame's delta in "
                          "float64 from the samples (exact integer DFT on the matrix cores), every decision "
@@ -226,21 +228,42 @@ def cpu_baseline_live(pool, seconds):
     return len(x) / dt / 1e6, dt
 
 
+def live_rows(rank):
+    """the rank's day of live audio: 24 distinct seeded 1 h 4 kHz recordings (seed 6000 + 24 rank + j),
+    made by forked workers before any GPU call"""
+    return synth_rows("real", [6000 + LIVE_FILES * rank + j for j in range(LIVE_FILES)], LIVE_FS * LIVE_FILE_S,
+                      fs=LIVE_FS, duration_s=LIVE_FILE_S, f0=1000.0, sigma=300.0, rate_per_min=5, band_hz=100.0,
+                      snr_db=(10, 30), dur_s=(0.3, 2.0))
+
+
 def main_live(a, world, rank, local, job_of):
-    """Phase-2 live detector over a day of 4 kHz audio per GPU: 24 x 1 h int16 files."""
-    from meteorgpu import _lib, synth
-    from meteorgpu import live as LV
+    """--workload live: the live line alone."""
+    from meteorgpu import _lib
+    rows = live_rows(rank)
     ctx = _lib.Context(local)
     job = job_of(ctx)
+    out = run_live(a, ctx, job, rank, world, rows)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if job is not None:
+        job.close()
+
+
+I8_PEAK_TOPS = 5000.0  # MI355X int8 MFMA, dense: 2x the BF16 rate (MI355X_MICROARCH.md, matrix cores)
+
+
+def run_live(a, ctx, job, rank, world, rows):
+    """Phase-2 live detector over a day of 4 kHz audio per GPU: 24 x 1 h int16 files.  Returns the
+    line (cpu_baseline on rank 0 at N = 1 only)."""
+    from meteorgpu import _lib
+    from meteorgpu import live as LV
     cfg = LV.ConfigDetection(proc_block_sec=0.2, n_fft=4096, signal_freq=1000,
                              detection_db_over_noise_mean_min=1, detection_dur_min_sec=0.5)
     n = LIVE_FS * LIVE_FILE_S
     F = LIVE_FILES
     lb = LV.LiveBatch(ctx, F, n, LIVE_FS, cfg)
-    pool = [synth.synth_real(seed=3000 + j, fs=LIVE_FS, duration_s=LIVE_FILE_S, f0=1000.0, sigma=300.0,
-                             rate_per_min=5, band_hz=100.0, snr_db=(10, 30), dur_s=(0.3, 2.0))[0] for j in range(4)]
     for i in range(F):
-        lb.upload_file(i, pool[(i + rank) % len(pool)])
+        lb.upload_file(i, rows[i])
 
     def sync_all():
         ctx.synchronize()
@@ -267,27 +290,36 @@ def main_live(a, world, rank, local, job_of):
     lb.run()
     sync_all()
     l_ms, l_n = ctx.timing_get(_lib.K_LIVE)
+    ctx.timing(False)
     wc = lb.plan.cfg
     nseg = (wc.block_size - wc.nperseg) // (wc.nperseg - wc.noverlap) + 1
     nslots = sum(wc.band_hi[j] - wc.band_lo[j] + 1 for j in range(wc.nbands))
     blocks = F * lb.nb
-    flops = blocks * nseg * nslots * wc.nperseg * 3.0  # Goertzel: one fma + one subtract per sample and bin
     avg_s = w_ms / max(w_n, 1) / 1e3
+    # int16 input takes the exact integer GEMM (csrc/welch_i8.hip): the dominant work is int8 MFMA,
+    # per segment nperseg samples x 2 nslots components x (7 coefficient x 2 sample digits), 2 ops
+    # per multiply-add, in 16-row tiles of whole blocks (16 // nseg blocks per tile)
+    bpt = 16 // nseg
+    tiles = -(-blocks // bpt)
+    ncol = -(-2 * nslots // 16) * 16
+    i8_ops = tiles * 16 * wc.nperseg * ncol * 14 * 2.0
+    useful = blocks * nseg * wc.nperseg * 2 * nslots * 14 * 2.0
     out = {
         "metric": "Msamples/s processed (4 kHz live detector: Welch band powers + state machine)",
         "value": round(world * F * n * a.steps / elapsed / 1e6, 1),
         "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic: 4 seeded 1 h 4 kHz int16 noise+ping recordings replicated over 24 files/GPU",
+        "vs_baseline": None, "dtype": "int8 MFMA (exact) / f64",
+        "data": f"synthetic: {F} distinct seeded 1 h 4 kHz int16 noise+ping recordings per GPU "
+                f"(seed 6000 + 24 rank + file index)",
         "config": {"workload": "phase-2 live detector day: 24 x 1 h 4 kHz int16 per GPU, 0.2 s blocks, "
                                "welch(nperseg 256, nfft 4096) on 3 x 100 Hz bands, 8 s history, k = 4",
                    "files_per_gpu": F, "samples_per_file": n, "blocks_per_file": lb.nb, "band_bins": nslots},
         "meteors_per_step": int(counts.sum()),
-        "roofline": {"bound": "fp64-valu", "achieved": round(flops / avg_s / 1e12, 2), "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(flops / avg_s / 1e12 / FP64_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": "welch_bands_kernel<int16>", "kernel_ms": round(avg_s * 1e3, 4),
-                     "algorithmic_flops_per_launch": flops},
+        "roofline": {"bound": "mfma", "achieved": round(i8_ops / avg_s / 1e12, 1), "peak": I8_PEAK_TOPS,
+                     "unit": "TOPS (int8)", "frac": round(i8_ops / avg_s / 1e12 / I8_PEAK_TOPS, 4), "traffic": None,
+                     "kernel": "welch_i8_kernel<4> + welch_i8_bands_kernel", "kernel_ms": round(avg_s * 1e3, 4),
+                     "int8_ops_per_launch": i8_ops, "useful_int8_ops_per_launch": useful},
         "kernel_ms_per_step": {"welch": round(avg_s * 1e3, 4), "live_detect": round(l_ms / max(l_n, 1), 4)},
     }
     # the near-tie guard of every recording (margin.py, live part; outside the timed region): a
@@ -297,16 +329,14 @@ def main_live(a, world, rank, local, job_of):
                        "max_decision_bound_db": float(np.max(lb.decision_bounds)),
                        "min_margin_db": float(np.min(lb.min_margins))}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
-        secs = 1800
-        v, dt = cpu_baseline_live(pool, secs)
+        secs = 900
+        v, dt = cpu_baseline_live(rows, secs)
         out["cpu_baseline"] = {"value": round(v, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
                                "sample": f"{secs} s of one 4 kHz file ({dt:.1f} s): scipy welch per block + "
                                          f"band sums + state machine (oracle/live_oracle.py), 1 thread"}
     out["ranks_seen"] = job.ranks_seen() if job is not None else 1
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if job is not None:
-        job.close()
+    lb.close()
+    return out
 
 
 C5_BAND, C5_NOISE = (950.0, 1050.0), (-3050.0, -2950.0)  # Hz from the SDR centre (two-sided spectrum)
@@ -611,9 +641,10 @@ def dry_run(rank, world, files):
     # files over the ranks, contiguous slices
     strong = {"files_total": files, "files_per_rank": [int(np.subtract(*shard_range(files, r, world)[::-1]))
                                                        for r in range(world)], "scaling": "strong"}
-    # the real line carries ranks_seen for the C3 leg (top level) and for the C5 leg ("c5")
+    # the real line carries ranks_seen for the C3 leg (top level), the C5 leg ("c5") and the live leg
     print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": len(seen), "id_agreed": ok,
-                      "strong_scaling": strong, "c5": {"ranks_seen": len(seen)}}), flush=True)
+                      "strong_scaling": strong, "c5": {"ranks_seen": len(seen)}, "live": {"ranks_seen": len(seen)}}),
+          flush=True)
     if not ok:
         sys.exit(1)
 
@@ -662,8 +693,9 @@ def _main():
         slo, shi = shard_range(a.files, rank, world)
         spool = pool[slo:shi] if day == 0 else synth_rows("real", day_seeds(0, slo, shi), FS * SECONDS, fs=FS,
                                                           duration_s=SECONDS, f0=1000.0)
-    # the C5 line's stream, made before any GPU call as well
+    # the C5 line's stream and the live line's day, made before any GPU call as well
     rows5 = c5_rows(a, rank, world) if not a.no_c5 and not a.shard_day else None
+    rows_live = live_rows(rank) if not a.no_live and not a.shard_day else None
     mp_base = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0 and a.cpu_procs > 1:
         # before any GPU call: the workers are forked from this process
@@ -756,6 +788,14 @@ def _main():
             if world > 1:
                 raise
             out["c5"] = {"error": f"{type(e).__name__}: {e}"}
+    if rows_live is not None:
+        # the phase-2 live detector in the same run, after C3 and C5 (key "live")
+        try:
+            out["live"] = run_live(a, ctx, job, rank, world, rows_live)
+        except Exception as e:  # noqa: BLE001 -- one rank: the C3 line stands; several: fail as one job
+            if world > 1:
+                raise
+            out["live"] = {"error": f"{type(e).__name__}: {e}"}
     out["ranks_seen"] = job.ranks_seen() if job is not None else 1
     if rank == 0:
         print(json.dumps(out), flush=True)

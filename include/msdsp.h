@@ -92,7 +92,11 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
  * Goertzel kernel instead of the exact int8-MFMA one (plans with min(block_size, n_fft) = 256,
  * 512 or 1024 and at most 8 band + noise bins take the latter by default; A/B, both within the
  * near-tie bound of meteorgpu/margin.py; MSD_BLOCK_GOERTZEL=1 in the environment sets it for new
- * contexts). */
+ * contexts).
+ * MSD_OPT_WELCH_GOERTZEL = 1 → msd_welch_bands[_dev] / msd_welch_psd compute int16 samples with the
+ * float64 Goertzel kernel instead of the exact int8-MFMA one (plans with nperseg a multiple of 64
+ * up to 512, <= 16 segments per block and a window in [-1, 1] take the latter by default; A/B,
+ * both within margin.py's live bound; MSD_WELCH_GOERTZEL=1 in the environment). */
 #define MSD_OPT_GENERIC_STFT 1
 #define MSD_OPT_FRESH_ALL 2
 #define MSD_OPT_REFINE_GOERTZEL 3
@@ -101,6 +105,7 @@ int msd_memset_dev(msd_ctx *ctx, void *dst, int value, size_t bytes);
 #define MSD_OPT_CSTFT_SCHED 6
 #define MSD_OPT_STFT_SCHED 7
 #define MSD_OPT_BLOCK_GOERTZEL 8
+#define MSD_OPT_WELCH_GOERTZEL 9
 int msd_set_option(msd_ctx *ctx, int option, int value);
 
 /* Per-kernel device timing with HIP events on the context stream.

@@ -169,6 +169,8 @@ int msd_create(int device, msd_ctx **out) {
         c->stft_sched = !strcmp(e, "static") ? 1 : !strcmp(e, "chunked") ? 2 : 0;
     if (const char *e = getenv("MSD_BLOCK_GOERTZEL"))  // A/B runs: MSD_OPT_BLOCK_GOERTZEL
         c->block_goertzel = atoi(e) != 0;
+    if (const char *e = getenv("MSD_WELCH_GOERTZEL"))  // A/B runs: MSD_OPT_WELCH_GOERTZEL
+        c->welch_goertzel = atoi(e) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -260,6 +262,7 @@ int msd_set_option(msd_ctx *ctx, int option, int value) {
         case MSD_OPT_FRESH_ALL: ctx->fresh_all = value != 0; return MSD_OK;
         case MSD_OPT_REFINE_GOERTZEL: ctx->refine_goertzel = value != 0; return MSD_OK;
         case MSD_OPT_BLOCK_GOERTZEL: ctx->block_goertzel = value != 0; return MSD_OK;
+        case MSD_OPT_WELCH_GOERTZEL: ctx->welch_goertzel = value != 0; return MSD_OK;
         case MSD_OPT_CSTFT_RESERVE:
             if (value < 0) return fail(MSD_ERR_INVALID, "msd_set_option: MSD_OPT_CSTFT_RESERVE must be >= 0");
             ctx->cstft_reserve = value;

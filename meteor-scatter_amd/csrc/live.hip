@@ -495,6 +495,8 @@ int launch_welch_t(msd_welch_plan *p, const void *x, const int64_t *off, const i
 int launch_welch(msd_welch_plan *p, const void *x, int dtype, const int64_t *off, const int64_t *len, int64_t nfiles,
                  int64_t max_blocks, double *band_db, int64_t ld, double *psd) {
     if (nfiles == 0 || max_blocks == 0) return MSD_OK;
+    if (dtype == MSD_I16 && p->d_i8 && !p->ctx->welch_goertzel)  // the exact integer DFT (welch_i8.hip)
+        return launch_welch_i8(p, static_cast<const int16_t *>(x), off, len, nfiles, max_blocks, band_db, ld, psd);
     switch (dtype) {
         case MSD_U8: return launch_welch_t<uint8_t>(p, x, off, len, nfiles, max_blocks, band_db, ld, psd);
         case MSD_I16: return launch_welch_t<int16_t>(p, x, off, len, nfiles, max_blocks, band_db, ld, psd);
@@ -574,6 +576,12 @@ int msd_welch_plan_create(msd_ctx *ctx, const msd_welch_cfg *cfg, const double *
         msd_welch_plan_destroy(p);
         return hip_fail(e, "msd_welch_plan_create");
     }
+    if (welch_i8_shape(c, p->nseg, nslots, window)) {  // int16 samples on the matrix cores
+        if (int rc = welch_i8_build(p, window)) {
+            msd_welch_plan_destroy(p);
+            return rc;
+        }
+    }
     *out = p;
     return MSD_OK;
 }
@@ -584,6 +592,7 @@ void msd_welch_plan_destroy(msd_welch_plan *p) {
     (void)hipStreamSynchronize(p->ctx->stream);
     if (p->d_window) (void)hipFree(p->d_window);
     if (p->d_bins) (void)hipFree(p->d_bins);
+    if (p->d_i8) (void)hipFree(p->d_i8);
     delete p;
 }
 

@@ -75,6 +75,7 @@ struct msd_ctx {
     int i8_km[16] = {};
     bool refine_goertzel = false;  // MSD_OPT_REFINE_GOERTZEL: int16 refinement on the float64 Goertzel
     bool block_goertzel = false;   // MSD_OPT_BLOCK_GOERTZEL: int16 block energies on the float64 Goertzel
+    bool welch_goertzel = false;   // MSD_OPT_WELCH_GOERTZEL: int16 Welch band powers on the float64 Goertzel
     int cstft_reserve = 0;         // MSD_OPT_CSTFT_RESERVE: workgroup slots the C5 spectrogram leaves free
     int cstft_sched = 0;           // MSD_OPT_CSTFT_SCHED: 0 / 2 chunks from a guided schedule, 1 fixed ranges
     int stft_sched = 0;            // MSD_OPT_STFT_SCHED: the same for stft1024_kernel (tiles)
@@ -148,6 +149,10 @@ struct msd_welch_plan {
     int nslots = 0;               // bins computed per block (band ranges concatenated)
     double *d_window = nullptr;   // [nperseg]
     double *d_bins = nullptr;     // [nslots][4]: cos w, sin w, 2 cos w, doubling factor (1 or 2)
+    // int16 samples on the matrix cores (welch_i8.hip): B fragments, column start values and
+    // doubling factors of the nct column tiles; null when the plan's shape does not take that path
+    void *d_i8 = nullptr;
+    int i8_nct = 0;
 };
 
 namespace msd {
@@ -271,6 +276,10 @@ int launch_stft1024(msd_stft_plan *plan, const void *x, int dtype, const int64_t
                     int64_t nfiles, float *out, int64_t ld);
 bool block_i8_shape(int64_t L, int nbins);
 bool block_i8_window(const double *window, int64_t L);
+bool welch_i8_shape(const msd_welch_cfg &c, int nseg, int nslots, const double *window);
+int welch_i8_build(msd_welch_plan *p, const double *window);
+int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, const int64_t *len, int64_t nfiles,
+                    int64_t max_blocks, double *band_db, int64_t ld, double *psd);
 int block_i8_build(msd_block_plan *p, const double *window, const int *bins, int nbins);
 int launch_block_i8(msd_block_plan *p, const int16_t *x, const int64_t *off, const int64_t *len, int64_t nfiles,
                     int64_t max_blocks);

@@ -248,9 +248,12 @@ __device__ __forceinline__ double wave_chunk_sum(const A &a, int64_t cb, int64_t
     return __builtin_bit_cast(double, __shfl(__builtin_bit_cast(long long, v), 0, 64));
 }
 
-// np.sum of a(base .. base+n): s = 0.0; s += pairwise(chunk) over 8192-element chunks
+// np.sum of a(base .. base+n): s = 0.0; s += pairwise(chunk) over 8192-element chunks.  Inline: out of
+// line, with the window read through global loads (GSqDevRef), the callee took 148 VGPRs and its
+// callers 3 waves per SIMD instead of 4 -- the decisions-only fresh thresholds 5.1-5.5 -> 7.8-8.0 ms
+// beside the C5 spectrogram, the step 11.7 -> 12.7 ms (profiles/r6_c5_fresh_inline_ab.txt)
 template <typename A>
-__device__ double wave_np_sum(const A &a, int64_t base, int64_t n) {
+__device__ __forceinline__ double wave_np_sum(const A &a, int64_t base, int64_t n) {
 #pragma clang fp contract(off)
     double s = 0.0;
     for (int64_t c = 0; c < n; c += NP_BUFSIZE) s += wave_chunk_sum(a, base + c, n - c < NP_BUFSIZE ? n - c : NP_BUFSIZE);

@@ -1,0 +1,437 @@
+// The live detector's Welch band powers (dsp/src/live/backend/processor.py:206, :349-369) for int16
+// audio on the matrix cores.  Per processing block scipy.signal.welch detrends each nperseg-sample
+// segment by its mean, windows it and takes the nfft-point rFFT; only the band bins are used.  For
+// integer samples the detrended, windowed DFT at bin k is an integer-by-constant dot product,
+//     X_k = sum_n (x_n - m) w_n e^{-2 pi i k n / nfft} = sum_n x_n c'_kn,
+//     c'_kn = w_n e^{-2 pi i k n / nfft} - W_k / nperseg,  W_k = sum_n w_n e^{-2 pi i k n / nfft},
+// because the mean m = sum_n x_n / nperseg is linear in the samples (the detrend folded into the
+// coefficients: no per-segment mean, no second pass).  As in block_i8.hip, each real coefficient is
+// T = round(c' 2^53) (|c'| <= 2) in seven balanced base-256 digits and each sample x = 256 h + l' + 128,
+// so every inner sum is one v_mfma_i32_16x16x64_i8 accumulation, exact in int32.  The products of
+// equal weight share an accumulator (h with digit b and l' with digit b + 1: weight 256^(7 - b)),
+// eight per component, combined by a float64 Horner sum.  Error against the exact DFT: the
+// coefficients' quantisation 2^-54 sum|x| plus the Horner sum's 8 roundings of partials below
+// 2 sum|x| -- margin.live_over_error's int8 term (16.5 u sum|x| <= 16.5 u nperseg max|x|).
+//
+// GEMM: rows = segments (a 16-row tile holds bpt = 16 / nseg whole blocks, nseg rows each),
+// K = nperseg samples in steps of 64 (the lane's A fragment: 16 samples of its row, 8 at 8 g and 8 at
+// 32 + 8 g of the step, g = lane >> 4, as block_i8.hip), columns = the components of the band bins
+// (bin j's real part 2 j, imaginary part 2 j + 1), 16 per column tile.  The B fragments of all bins
+// (7 digits x KS steps x 1 KB per column tile: 1.1 MB for the live default's 309 bins) do not fit
+// one CU's LDS, so the column tiles are split into groups of cg (<= 144 KB of fragments) and each
+// workgroup holds one group's fragments in LDS for its lifetime, walking the M tiles of its XCD:
+// the workgroups of the column groups on one XCD walk the same tiles in the same order, so the
+// samples come from HBM once per XCD and from its L2 for the other groups.  Per (M tile, column
+// tile) a wave issues 14 MFMAs per K step (2 sample digits x 7 coefficient digits), combines the
+// digits, forms |X|^2 * scale * (2 off DC / Nyquist) and averages each block's nseg segment rows in
+// segment order (scipy: Pxy.mean(axis=-1)); the per-block PSD of the band bins goes to memory and
+// welch_i8_bands_kernel takes numpy's pairwise band sums and 10 log10 (np.sum(psd[mask])).
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "msd_internal.h"
+#include "np_reduce.h"
+
+#pragma clang fp contract(off)
+
+namespace msd {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+constexpr int WI_ND = 7;                  // coefficient digits
+constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
+constexpr int WI_WAVES = 8;               // waves per workgroup (2 per SIMD)
+constexpr int WI_PP = 9;                  // per-wave power scratch: 16 rows x 8 bins, pitch 9 doubles
+constexpr size_t WI_LDS_B = 144 * 1024;   // LDS for one workgroup's B fragments
+constexpr int WI_MAXKS = 8;               // nperseg <= 512 (16 K steps would spill)
+
+struct WelchI8Args {
+    int64_t nfiles, max_blocks, ld;
+    int block_size, step, nseg, bpt;  // bpt: whole blocks per 16-row tile (bpt * nseg <= 16 rows)
+    int nct, cg, ngroups, reps;       // column tiles, tiles per group, groups, workgroups per group and XCD
+    int nslots;
+    double xscale;  // 2^-53 x sample_scale: a component's value from its integer digit sum
+    double scale;   // the density scale 1 / (fs sum w^2)
+};
+
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+    const long long v = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(v & 0xffffffffll), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), CTRL, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// A fragments of one K step from the lane's 16 samples (w[0..7], two per dword): h = x >> 8 and
+// l' = (x & 255) - 128 (offset-binary byte ^ 0x80), as int8
+__device__ __forceinline__ void digits(const uint32_t *w, v4i &hi, v4i &lo) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        hi[o] = (int)__builtin_amdgcn_perm(w[2 * o + 1], w[2 * o], 0x07050301u);
+        lo[o] = (int)(__builtin_amdgcn_perm(w[2 * o + 1], w[2 * o], 0x06040200u) ^ 0x80808080u);
+    }
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// a block of the batch: file f, block b of the file, its first sample; valid = the block exists
+struct BlockRef {
+    int64_t f, b;
+    const int16_t *p;
+    bool valid;
+};
+
+// block g (per lane) of the tile whose blocks are [g0, g0 + bpt): the files are walked with scalar
+// loads (g0 is wave-uniform; at most a few files), a lane's block picked from them
+__device__ __forceinline__ BlockRef block_of(const int16_t *x, const int64_t *off, const int64_t *len,
+                                            const WelchI8Args &A, int64_t g0, int64_t g) {
+    BlockRef r;
+    r.f = g / A.max_blocks;
+    r.b = g - r.f * A.max_blocks;
+    r.valid = false;
+    r.p = x;
+    const int64_t f0 = uniform_i64(g0 / A.max_blocks);
+    const int64_t fl = uniform_i64(std::min((g0 + A.bpt - 1) / A.max_blocks, A.nfiles - 1));
+    for (int64_t f = f0; f <= fl; ++f) {
+        int64_t o = off[f], n = len[f];
+        asm volatile("" : "+s"(o), "+s"(n));
+        const int64_t nb = n >= A.block_size ? (n - A.block_size) / A.block_size + 1 : 0;
+        if (r.f == f && r.b < nb) {
+            r.valid = true;
+            r.p = x + o + r.b * (int64_t)A.block_size;
+        }
+    }
+    return r;
+}
+
+// psd[(f ld + b) nslots + slot] = the Welch PSD of block (f, b) at the band bins (slot = band bins in
+// order), every block of files [0, nfiles) x [0, max_blocks) that exists.  bfrag: [nct][ND][KS][64]
+// B fragments; colinit: [nct][NW][16] the accumulator start values (128 sum_n d of the l' products);
+// dbl: [nct * 8] the onesided doubling (1 at DC / Nyquist, else 2; 0 past nslots).
+template <int KS>
+__global__ __launch_bounds__(64 * WI_WAVES, 1) void welch_i8_kernel(const int16_t *__restrict__ x,
+                                                                    const int64_t *__restrict__ off,
+                                                                    const int64_t *__restrict__ len, WelchI8Args A,
+                                                                    const v4i *__restrict__ bfrag,
+                                                                    const int *__restrict__ colinit,
+                                                                    const double *__restrict__ dbl,
+                                                                    double *__restrict__ psd) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int xcd = blockIdx.x & 7, iw = blockIdx.x >> 3;
+    const int cgi = iw % A.ngroups, rep = iw / A.ngroups;
+    const int ct0 = cgi * A.cg;
+    const int nct = min(A.cg, A.nct - ct0);  // column tiles of this workgroup
+    if (nct <= 0) return;                    // workgroup-uniform, before any barrier
+    v4i *sB = reinterpret_cast<v4i *>(smem);                                        // [cg][ND][KS][64]
+    double *sP = reinterpret_cast<double *>(sB + (size_t)A.cg * WI_ND * KS * 64);   // [WAVES][16][PP]
+    double *sDbl = sP + WI_WAVES * 16 * WI_PP;                                      // [cg][8]
+    int *sInit = reinterpret_cast<int *>(sDbl + A.cg * 8);                          // [cg][NW][16]
+    for (int i = threadIdx.x; i < nct * WI_ND * KS * 64; i += 64 * WI_WAVES) sB[i] = bfrag[(size_t)ct0 * WI_ND * KS * 64 + i];
+    for (int i = threadIdx.x; i < nct * WI_NW * 16; i += 64 * WI_WAVES) sInit[i] = colinit[ct0 * WI_NW * 16 + i];
+    for (int i = threadIdx.x; i < nct * 8; i += 64 * WI_WAVES) sDbl[i] = dbl[ct0 * 8 + i];
+    __syncthreads();
+    const int l = threadIdx.x & 63;
+    const int c = l & 15, g = l >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double *pw = sP + wv * 16 * WI_PP;
+    const int nrow = A.bpt * A.nseg;
+    const int64_t nblocks = A.nfiles * A.max_blocks;
+    const int64_t ntm = (nblocks + A.bpt - 1) / A.bpt;  // M tiles
+    // this XCD's contiguous share of the M tiles; the workgroups of every column group walk it in
+    // the same order (stride = the wave slots of one group on this XCD)
+    const int64_t t_lo = ntm * xcd / 8, t_hi = ntm * (xcd + 1) / 8;
+    const int64_t slot0 = (int64_t)rep * WI_WAVES + wv, nslot = (int64_t)A.reps * WI_WAVES;
+
+    // the lane's A row: row c = segment c % nseg of block c / nseg of the tile (rows past nrow and
+    // missing blocks read the file start, their results unused)
+    auto row_ptr = [&](int64_t t) {
+        const int64_t g0 = uniform_i64(t * A.bpt);
+        const int bi = c < nrow ? c / A.nseg : 0;
+        const int s = c < nrow ? c - bi * A.nseg : 0;
+        const BlockRef r = block_of(x, off, len, A, g0, g0 + bi);
+        return r.valid ? r.p + (int64_t)s * A.step : x;
+    };
+    auto fetch = [&](const int16_t *p, int ks, int half) {
+        v4u v;
+        __builtin_memcpy(&v, p + 64 * ks + 32 * half + 8 * g, 16);
+        return v;
+    };
+    v4u R[2 * KS];
+    int64_t t = t_lo + slot0;
+    if (t >= t_hi) return;  // wave-uniform; no workgroup barrier below
+    {
+        const int16_t *p = row_ptr(t);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
+    }
+    for (; t < t_hi; t += nslot) {
+        // the tile's sample digits, then the next tile's samples into R while this one computes
+        v4i ah[KS], al[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            uint32_t w[8];
+            __builtin_memcpy(w, &R[2 * ks], 32);
+            digits(w, ah[ks], al[ks]);
+        }
+        const int64_t tn = t + nslot < t_hi ? t + nslot : t;  // the last tile re-reads itself (unused)
+        {
+            const int16_t *p = row_ptr(tn);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
+        }
+        // the lanes that average a (block, bin): block l >> 3 of the tile, bin l & 7 of a column tile
+        const int64_t g0 = uniform_i64(t * A.bpt);
+        const int ab = l >> 3;
+        const BlockRef blk = block_of(x, off, len, A, g0, g0 + (ab < A.bpt ? ab : 0));
+        const bool avg_lane = ab < A.bpt && blk.valid;
+        for (int j = 0; j < nct; ++j) {
+            v4i acc[WI_NW];
+#pragma unroll
+            for (int w = 0; w < WI_NW; ++w) {
+                const int ci = sInit[(j * WI_NW + w) * 16 + c];
+                acc[w] = v4i{ci, ci, ci, ci};
+            }
+            const v4i *bj = sB + (size_t)j * WI_ND * KS * 64 + l;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                v4i bk[WI_ND];
+#pragma unroll
+                for (int d = 0; d < WI_ND; ++d) bk[d] = bj[(d * KS + ks) * 64];
+                // h x digit d: weight 256^(7 - d); l' x digit d: 256^(6 - d) (the l' chain second, so
+                // the two MFMAs into one accumulator are 7 apart)
+#pragma unroll
+                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[ks], bk[d], acc[7 - d], 0, 0, 0);
+#pragma unroll
+                for (int d = 0; d < WI_ND; ++d) acc[6 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], bk[d], acc[6 - d], 0, 0, 0);
+            }
+            // component c of rows 4 g + i: sum_w 256^w acc_w x 2^-53 x sample scale
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double v = (double)acc[7][i];
+#pragma unroll
+                for (int w = 6; w >= 0; --w) v = __builtin_fma(v, 256.0, (double)acc[w][i]);
+                v *= A.xscale;
+                const double q = dpp64<0xB1>(v);  // the partner component (c ^ 1)
+                if (!(c & 1)) {                   // processor.py via scipy: conj(X) X, * scale, * 2
+                    double p = v * v + q * q;
+                    p = p * A.scale;
+                    p = p * sDbl[j * 8 + (c >> 1)];
+                    pw[(4 * g + i) * WI_PP + (c >> 1)] = p;
+                }
+            }
+            wave_sync();
+            if (avg_lane) {  // Pxy.mean(axis=-1): the block's segments in order, / nseg
+                const int bin = l & 7;
+                const int slot = (ct0 + j) * 8 + bin;
+                if (slot < A.nslots) {
+                    const double *q = pw + ab * A.nseg * WI_PP + bin;
+                    double s = q[0];
+                    for (int k = 1; k < A.nseg; ++k) s = s + q[k * WI_PP];
+                    psd[(blk.f * A.ld + blk.b) * (int64_t)A.nslots + slot] = s / (double)A.nseg;
+                }
+            }
+            wave_sync();  // pw is rewritten by the next column tile
+        }
+    }
+}
+
+// band_db[(f nbands + j) ld + b] = 10 log10(np.sum(psd[band j])) (-inf when not > 0) of every block
+// (f, b) that exists: one thread per (block, band), numpy's pairwise order over the band's slots
+struct BandArgs {
+    int64_t nfiles, max_blocks, ld;
+    int block_size, nslots, nbands;
+    int slot0[MSD_WELCH_MAX_BANDS], width[MSD_WELCH_MAX_BANDS];
+};
+
+__global__ __launch_bounds__(256) void welch_i8_bands_kernel(const int64_t *__restrict__ len, BandArgs A,
+                                                             const double *__restrict__ psd,
+                                                             double *__restrict__ band_db) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nb_all = A.nfiles * A.max_blocks;
+    if (i >= nb_all * A.nbands) return;
+    const int j = (int)(i % A.nbands);
+    const int64_t gb = i / A.nbands;
+    const int64_t f = gb / A.max_blocks, b = gb - f * A.max_blocks;
+    const int64_t n = len[f];
+    const int64_t nb = n >= A.block_size ? (n - A.block_size) / A.block_size + 1 : 0;
+    if (b >= nb) return;
+    const int w = A.width[j];
+    const GArrRef row{as_global(psd + (f * A.ld + b) * (int64_t)A.nslots)};
+    const double P = w <= 0 ? 0.0 : (w <= 128 ? np_sum_small(row, A.slot0[j], w) : np_sum(row, A.slot0[j], w));
+    band_db[(f * A.nbands + j) * A.ld + b] = P > 0.0 ? 10.0 * log10(P) : -INFINITY;
+}
+
+// one balanced base-256 digit expansion of T: T = sum_b d[b] 256^(6 - b); false if T needs more
+bool balanced_digits7(int64_t T, int8_t (&d)[WI_ND]) {
+    for (int b = WI_ND - 1; b >= 0; --b) {
+        int64_t r = ((T % 256) + 256) % 256;
+        if (r >= 128) r -= 256;
+        d[b] = (int8_t)r;
+        T = (T - r) / 256;
+    }
+    return T == 0;
+}
+
+}  // namespace
+
+// the int8 path applies: int16 samples (checked at launch), nperseg a multiple of 64 up to 512, at
+// most 16 segments per block, a window in [-1, 1] (the quantisation and margin.py's bound), >= 1 bin
+bool welch_i8_shape(const msd_welch_cfg &c, int nseg, int nslots, const double *window) {
+    if (c.nperseg % 64 != 0 || c.nperseg > 64 * WI_MAXKS || nseg < 1 || nseg > 16 || nslots < 1) return false;
+    for (int n = 0; n < c.nperseg; ++n)
+        if (!std::isfinite(window[n]) || std::fabs(window[n]) > 1.0) return false;
+    return true;
+}
+
+// the plan's B fragments, column start values and doubling factors (one device buffer, p->d_i8)
+int welch_i8_build(msd_welch_plan *p, const double *window) {
+    const msd_welch_cfg &c = p->cfg;
+    const int L = c.nperseg, KS = L / 64, nfft = c.nfft;
+    std::vector<int> ks_bins;
+    std::vector<double> dblv;
+    for (int j = 0; j < c.nbands; ++j) {
+        if (c.band_hi[j] < c.band_lo[j]) continue;
+        for (int k = c.band_lo[j]; k <= c.band_hi[j]; ++k) {
+            ks_bins.push_back(k);
+            const bool edge = k == 0 || (nfft % 2 == 0 && k == nfft / 2);
+            dblv.push_back(edge ? 1.0 : 2.0);
+        }
+    }
+    const int nslots = (int)ks_bins.size();
+    const int ncomp = 2 * nslots;
+    const int nct = (ncomp + 15) / 16;
+    std::vector<int8_t> frag((size_t)nct * WI_ND * KS * 64 * 16, 0);
+    std::vector<int> init((size_t)nct * WI_NW * 16, 0);
+    std::vector<double> dbl((size_t)nct * 8, 0.0);
+    for (int s = 0; s < nslots; ++s) dbl[s] = dblv[s];
+    std::vector<int8_t> dig((size_t)WI_ND * L);
+    for (int cp = 0; cp < ncomp; ++cp) {
+        const int64_t k = ks_bins[cp >> 1];
+        const bool im = cp & 1;
+        // W_k = sum_n w_n e^{-i theta n} in long double; c'_n = w_n e^{-i theta n} - W_k / L
+        long double Wre = 0.0L, Wim = 0.0L;
+        std::vector<long double> cr(L), ci(L);
+        for (int n = 0; n < L; ++n) {
+            long double cs, sn;
+            unit_root_ld(k * n, nfft, cs, sn);
+            cr[n] = (long double)window[n] * cs;
+            ci[n] = -(long double)window[n] * sn;
+            Wre += cr[n];
+            Wim += ci[n];
+        }
+        const long double Wc = (im ? Wim : Wre) / (long double)L;
+        for (int n = 0; n < L; ++n) {
+            const long double v = (im ? ci[n] : cr[n]) - Wc;
+            const int64_t T = llroundl(v * 0x1p53L);
+            int8_t d[WI_ND];
+            if (!balanced_digits7(T, d)) return fail(MSD_ERR_INVALID, "welch_i8: coefficient beyond 7 digits");
+            for (int b = 0; b < WI_ND; ++b) dig[(size_t)b * L + n] = d[b];
+        }
+        const int ct = cp / 16, cc = cp % 16;
+        for (int b = 0; b < WI_ND; ++b) {
+            int64_t sd = 0;
+            for (int n = 0; n < L; ++n) sd += dig[(size_t)b * L + n];
+            init[((size_t)ct * WI_NW + (6 - b)) * 16 + cc] += (int)(128 * sd);  // l' x digit b: weight 6 - b
+            for (int ks = 0; ks < KS; ++ks)
+                for (int grp = 0; grp < 4; ++grp)
+                    for (int jj = 0; jj < 16; ++jj) {
+                        const int n = 64 * ks + (jj < 8 ? 8 * grp + jj : 32 + 8 * grp + (jj - 8));
+                        const int lane = grp * 16 + cc;
+                        frag[((((size_t)ct * WI_ND + b) * KS + ks) * 64 + lane) * 16 + jj] = dig[(size_t)b * L + n];
+                    }
+        }
+    }
+    const size_t nb_frag = frag.size(), nb_init = sizeof(int) * init.size(), nb_dbl = sizeof(double) * dbl.size();
+    hipError_t e = hipMalloc(&p->d_i8, nb_frag + nb_init + nb_dbl);
+    char *base = static_cast<char *>(p->d_i8);
+    if (e == hipSuccess) e = hipMemcpy(base, frag.data(), nb_frag, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(base + nb_frag, init.data(), nb_init, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(base + nb_frag + nb_init, dbl.data(), nb_dbl, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "welch plan: int8 tables");
+    p->i8_nct = nct;
+    return MSD_OK;
+}
+
+// the int8 path of msd_welch_bands_dev for int16 samples: the PSD of the band bins per block into
+// psd (the caller's, or the context's scratch), then the band dB
+int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, const int64_t *len, int64_t nfiles,
+                    int64_t max_blocks, double *band_db, int64_t ld, double *psd) {
+    const msd_welch_cfg &c = p->cfg;
+    const int KS = c.nperseg / 64;
+    const int nct = p->i8_nct;
+    if (!psd) {
+        const size_t bytes = sizeof(double) * (size_t)nfiles * (size_t)ld * (size_t)p->nslots;
+        void *s = nullptr;
+        if (int rc = ctx_scratch(p->ctx, 5, bytes, &s)) return rc;
+        psd = static_cast<double *>(s);
+    }
+    WelchI8Args A{};
+    A.nfiles = nfiles;
+    A.max_blocks = max_blocks;
+    A.ld = ld;
+    A.block_size = c.block_size;
+    A.step = p->step;
+    A.nseg = p->nseg;
+    A.bpt = 16 / p->nseg;
+    A.nct = nct;
+    const size_t per_ct = (size_t)WI_ND * KS * 64 * 16 + sizeof(int) * WI_NW * 16 + sizeof(double) * 8;
+    A.cg = (int)std::max<size_t>(1, std::min<size_t>((size_t)nct, WI_LDS_B / per_ct));
+    A.ngroups = (nct + A.cg - 1) / A.cg;
+    A.cg = (nct + A.ngroups - 1) / A.ngroups;  // balance the groups (39 tiles: 8 groups of 5 / 4)
+    const int wg_per_xcd = std::max(1, p->ctx->num_cu / 8);
+    A.reps = std::max(1, wg_per_xcd / A.ngroups);
+    A.nslots = p->nslots;
+    A.xscale = std::ldexp(c.sample_scale, -53);
+    A.scale = c.scale;
+    const size_t lds = (size_t)A.cg * per_ct + sizeof(double) * WI_WAVES * 16 * WI_PP;
+    const v4i *frag = static_cast<const v4i *>(p->d_i8);
+    const char *base = static_cast<const char *>(p->d_i8) + (size_t)nct * WI_ND * KS * 64 * 16;
+    const int *init = reinterpret_cast<const int *>(base);
+    const double *dbl = reinterpret_cast<const double *>(base + sizeof(int) * (size_t)nct * WI_NW * 16);
+    const unsigned grid = (unsigned)(8 * A.ngroups * A.reps);
+    hipStream_t st = p->ctx->stream;
+    KernelTimer timer(p->ctx, K_WELCH);
+    switch (KS) {
+#define WI_CASE(K)                                                                                            \
+    case K:                                                                                                   \
+        if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(welch_i8_kernel<K>), 160 * 1024)) return rc; \
+        hipLaunchKernelGGL(welch_i8_kernel<K>, dim3(grid), dim3(64 * WI_WAVES), lds, st, x, off, len, A, frag, init, \
+                           dbl, psd);                                                                         \
+        break;
+        WI_CASE(1)
+        WI_CASE(2)
+        WI_CASE(3)
+        WI_CASE(4)
+        WI_CASE(8)
+#undef WI_CASE
+        default: return fail(MSD_ERR_UNSUPPORTED, "welch_i8: nperseg");
+    }
+    MSD_HIP(hipGetLastError());
+    BandArgs B{};
+    B.nfiles = nfiles;
+    B.max_blocks = max_blocks;
+    B.ld = ld;
+    B.block_size = c.block_size;
+    B.nslots = p->nslots;
+    B.nbands = c.nbands;
+    int s0 = 0;
+    for (int j = 0; j < c.nbands; ++j) {
+        B.slot0[j] = s0;
+        B.width[j] = c.band_hi[j] >= c.band_lo[j] ? c.band_hi[j] - c.band_lo[j] + 1 : 0;
+        s0 += B.width[j];
+    }
+    const int64_t nthreads = nfiles * max_blocks * c.nbands;
+    hipLaunchKernelGGL(welch_i8_bands_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, st, len, B, psd,
+                       band_db);
+    MSD_HIP(hipGetLastError());
+    return MSD_OK;
+}
+
+}  // namespace msd

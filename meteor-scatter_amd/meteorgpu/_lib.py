@@ -44,6 +44,7 @@ OPT_STREAM_CUS = 5
 OPT_CSTFT_SCHED = 6
 OPT_STFT_SCHED = 7
 OPT_BLOCK_GOERTZEL = 8
+OPT_WELCH_GOERTZEL = 9
 COMM_ID_BYTES = 128
 
 

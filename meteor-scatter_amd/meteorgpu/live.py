@@ -210,15 +210,16 @@ def _first_decision_block(nb: int, fs, cfg: ConfigDetection) -> int:
 
 
 def near_tie_check(band_db: np.ndarray, thr: np.ndarray, over: np.ndarray, span: np.ndarray, fs,
-                   cfg: ConfigDetection, what: str = "", warn: bool = True):
+                   cfg: ConfigDetection, what: str = "", warn: bool = True, absmax=None):
     """(near_tie, min_margin, bound) of one recording from the device's band dB rows, the
     thresholds used and the over-noise values (live_detect), and each block's sample span
-    (margin.block_span); a NearTieWarning when near."""
+    (margin.block_span); ``absmax`` (margin.block_absmax) for int16 samples, which may take the
+    int8 path (csrc/welch_i8.hip); a NearTieWarning when near."""
     c, win = welch_cfg(fs, cfg)
     bands = [(int(c.band_lo[j]), int(c.band_hi[j])) for j in range(3)]
     err = margin.live_over_error(band_db, block_size=int(c.block_size), nperseg=int(c.nperseg),
                                  noverlap=int(c.noverlap), nfft=int(c.nfft), window=win, span=span, bands=bands,
-                                 scale=float(c.scale))
+                                 scale=float(c.scale), absmax=absmax)
     W = int(cfg.avg_win_sec / cfg.proc_block_sec)
     return margin.live_decision_check(over, thr, err, k_std=cfg.threshold_std_factor, W=W,
                                       first_block=_first_decision_block(len(over), fs, cfg), what=what, warn=warn)
@@ -273,8 +274,9 @@ def wav_file_process(wav_file_path: str,
     found, thr, over = live_detect(bdb, file_sample_rate, config_detection, device)
     meteors = LiveMeteors(found)
     span = margin.block_span(x, block_size, sample_scale)[: bdb.shape[1]]
+    absmax = margin.block_absmax(x, block_size, sample_scale)[: bdb.shape[1]] if x.dtype == np.int16 else None
     meteors.near_tie, meteors.min_margin, meteors.decision_bound = near_tie_check(
-        bdb, thr, over, span, file_sample_rate, config_detection, what=f"{wav_file_path}: ")
+        bdb, thr, over, span, file_sample_rate, config_detection, what=f"{wav_file_path}: ", absmax=absmax)
     for i, m in enumerate(meteors):
         print("Detected Meteor:", m, "Now Detected Meteors:", i + 1)
     not_exported = list(meteors)
@@ -429,15 +431,30 @@ class LiveBatch:
         self.cfg = cfg
         self.sample_scale = float(sample_scale)
         self.span = np.zeros((F, self.nb))  # per-block sample span, for the near-tie guard
+        # per-block max |x| of int16 recordings (the int8 path's error term, margin.live_over_error)
+        self.absmax = np.zeros((F, self.nb)) if self.dtype == np.int16 else None
         self.near_tie = np.zeros(F, bool)
         self.min_margins = np.full(F, np.inf)
         self.decision_bounds = np.zeros(F)
+
+    def close(self):
+        """free the batch's device buffers and plan (the context stays)"""
+        if getattr(self, "plan", None) is None:
+            return
+        self.ctx.synchronize()
+        for b in (self.d_x, self.d_off, self.d_len, self.d_nb, self.d_band, self.d_over, self.d_thr, self.d_met,
+                  self.d_counts, self.d_status):
+            b.free()
+        self.plan.close()
+        self.plan = None
 
     def upload_file(self, i: int, x: np.ndarray):
         x = np.ascontiguousarray(x, dtype=self.dtype)
         if x.shape != (self.n,):
             raise ValueError("file length differs from the batch's")
         self.span[i] = margin.block_span(x, int(self.lcfg.block_size), self.sample_scale)[: self.nb]
+        if self.absmax is not None:
+            self.absmax[i] = margin.block_absmax(x, int(self.lcfg.block_size), self.sample_scale)[: self.nb]
         self.d_x.upload(x, byte_offset=i * self.n_pad * self.dtype.itemsize)
 
     def run(self):
@@ -475,7 +492,8 @@ class LiveBatch:
         bdb, thr, over = self.band_db(), self.thresholds(), self.over_noise()
         for i in range(self.nfiles):
             self.near_tie[i], self.min_margins[i], self.decision_bounds[i] = near_tie_check(
-                bdb[i], thr[i], over[i], self.span[i], self.fs, self.cfg, warn=False)
+                bdb[i], thr[i], over[i], self.span[i], self.fs, self.cfg, warn=False,
+                absmax=None if self.absmax is None else self.absmax[i])
         if warn and self.near_tie.any():
             import warnings
             idx = np.nonzero(self.near_tie)[0]

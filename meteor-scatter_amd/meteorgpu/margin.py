@@ -41,7 +41,9 @@ only the transform differs:
 
 * per segment and bin |dX| <= (c_fft + c_goertzel) u S, S = sum |w (x - mean)| <= span sum w with
   span = max x - min x over the block (a constant block is exactly 0 on both sides),
-  c_fft = 4 log2(nfft) + 8, c_goertzel = 3 nperseg G + 24;
+  c_fft = 4 log2(nfft) + 10 (the FFT, the detrend and the window), c_goertzel = 3 nperseg G + 24;
+  int16 samples on the matrix cores (csrc/welch_i8.hip: the detrend folded into int8-digit
+  coefficients) replace c_goertzel u S by 18 u nperseg max|x| -- the larger of the two is taken;
 * a band energy E = scale / nseg * sum_s sum_k c_k |X_sk|^2 (c_k = 2 off DC / Nyquist) moves by
   at most dE = 2 dX sqrt(C scale E) + C scale dX^2 + (n + nseg + 10) u E, C = 2n (Cauchy-Schwarz
   over the n bins and nseg segments);
@@ -184,18 +186,41 @@ def block_span(x: np.ndarray, block_size: int, sample_scale: float = 1.0) -> np.
     return (v.max(axis=1).astype(np.float64) - v.min(axis=1).astype(np.float64)) * abs(float(sample_scale))
 
 
+def block_absmax(x: np.ndarray, block_size: int, sample_scale: float = 1.0) -> np.ndarray:
+    """max |x| of each whole processing block's samples, times the sample scale."""
+    x = np.asarray(x)
+    nb = len(x) // block_size if block_size > 0 else 0
+    if nb == 0:
+        return np.zeros(0)
+    v = np.abs(x[: nb * block_size].reshape(nb, block_size).astype(np.float64))
+    return v.max(axis=1) * abs(float(sample_scale))
+
+
+# the int16 Welch path on the matrix cores (csrc/welch_i8.hip): |dX| <= I8_WELCH u sum_n |x_n| per
+# segment and bin -- the coefficients' 2^-54 quantisation (u / 2), the float64 Horner sum of 8
+# weights (2 u each, of partials below 2 sum|x|) and the mean's rounding for nperseg not a power of 2
+I8_WELCH = 18.0
+
+
 def live_over_error(band_db: np.ndarray, *, block_size: int, nperseg: int, noverlap: int, nfft: int,
-                    window: np.ndarray, span, bands, scale: float) -> np.ndarray:
+                    window: np.ndarray, span, bands, scale: float, absmax=None) -> np.ndarray:
     """Per-block bound on |db2_gpu - db2_scipy| (processor.py:391) from the device's band dB rows
     band_db [3][nb] (signal, noise 1, noise 2); ``bands``: their inclusive bin ranges, ``span``:
-    max - min of each block's (scaled) samples (``block_span``), ``window``: the nperseg window."""
+    max - min of each block's (scaled) samples (``block_span``), ``window``: the nperseg window.
+    ``absmax`` (``block_absmax``, int16 input): the device may have taken the int8 path, whose error
+    is relative to sum |x| rather than to the detrended samples; the bound then takes the larger of
+    the two transforms' terms, so it holds whichever ran."""
     band_db = np.asarray(band_db, dtype=np.float64)
     step = nperseg - noverlap
     nseg = (block_size - nperseg) // step + 1
     s = np.asarray(span, dtype=np.float64) * float(np.abs(np.asarray(window, dtype=np.float64)).sum())
     bins = np.concatenate([np.arange(lo, hi + 1) for lo, hi in bands]) if bands else np.zeros(0)
-    chain = 4.0 * math.log2(nfft) + 8.0 + _goertzel_chain(nperseg, bins, nfft)
-    dx = chain * U * s
+    # scipy's side: pocketfft's chain plus the detrend and window roundings of its input
+    dx = (4.0 * math.log2(nfft) + 10.0) * U * s
+    dev = _goertzel_chain(nperseg, bins, nfft) * U * s
+    if absmax is not None:
+        dev = np.maximum(dev, I8_WELCH * U * float(nperseg) * np.asarray(absmax, dtype=np.float64))
+    dx = dx + dev
     e = [welch_band_db_error(band_db[j], max(0, hi - lo + 1), dx, scale, nseg) for j, (lo, hi) in enumerate(bands)]
     with np.errstate(invalid="ignore"):
         rnd = 4.0 * U * (np.abs(band_db[0]) + np.abs(band_db[1]) + np.abs(band_db[2]))

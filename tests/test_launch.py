@@ -31,8 +31,10 @@ def test_bench_spawns_n_ranks(n, tmp_path):
     d = json.loads(lines[0])
     strong = d.pop("strong_scaling")
     c5 = d.pop("c5")
+    live = d.pop("live")
     assert d == {"dry_run": True, "n_gpus": n, "ranks_seen": n, "id_agreed": True}
     assert c5 == {"ranks_seen": n}  # the C5 leg's own rank count (weak-scaled stream)
+    assert live == {"ranks_seen": n}  # the live leg's (a day of 4 kHz audio per rank)
     # the C4 (strong scaling) pass the real N-rank line carries: one 1440-file day over the n ranks
     assert strong["scaling"] == "strong" and strong["files_total"] == 1440
     assert sum(strong["files_per_rank"]) == 1440 and max(strong["files_per_rank"]) == -(-1440 // n)
