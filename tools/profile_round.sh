@@ -13,7 +13,7 @@ mkdir -p "$OUT"
 timeout -k 10 400 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- \
-    python3 "$ROOT/bench.py" --steps $KS --warmup $KW --no-cpu-baseline --no-c5 > "$OUT/kt.log" 2>&1 || exit 1
+    python3 "$ROOT/bench.py" --steps $KS --warmup $KW --no-cpu-baseline --no-c5 --no-live > "$OUT/kt.log" 2>&1 || exit 1
 for wl in live c5; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_$wl" -o kt -- \
       python3 "$ROOT/bench.py" --workload $wl --steps $KS --warmup $KW --no-cpu-baseline --c5-mode off > "$OUT/kt_$wl.log" 2>&1 || exit 1
