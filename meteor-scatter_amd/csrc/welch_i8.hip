@@ -43,9 +43,17 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 constexpr int WI_ND = 7;                  // coefficient digits
 constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
-constexpr int WI_WAVES = 8;               // waves per workgroup (2 per SIMD)
+#ifndef WI_WAVES_N
+#define WI_WAVES_N 12
+#endif
+#ifndef WI_PREFETCH
+#define WI_PREFETCH 1
+#endif
+// waves per workgroup: 12 = 3 per SIMD (154 VGPRs).  Against 8 (2 per SIMD): 5.52-5.55 vs
+// 5.97-6.04 ms per day (profiles/r6_welch_i8_ab.txt)
+constexpr int WI_WAVES = WI_WAVES_N;
 constexpr int WI_PP = 9;                  // per-wave power scratch: 16 rows x 8 bins, pitch 9 doubles
-constexpr size_t WI_LDS_B = 144 * 1024;   // LDS for one workgroup's B fragments
+constexpr size_t WI_LDS = 160 * 1024;     // LDS of one workgroup: B fragments + per-wave power scratch
 constexpr int WI_MAXKS = 8;               // nperseg <= 512 (16 K steps would spill)
 
 struct WelchI8Args {
@@ -172,6 +180,11 @@ __global__ __launch_bounds__(64 * WI_WAVES, 1) void welch_i8_kernel(const int16_
         for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
     }
     for (; t < t_hi; t += nslot) {
+        if (!WI_PREFETCH && t != t_lo + slot0) {  // (A/B: the tile's samples loaded here)
+            const int16_t *p = row_ptr(t);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
+        }
         // the tile's sample digits, then the next tile's samples into R while this one computes
         v4i ah[KS], al[KS];
 #pragma unroll
@@ -181,7 +194,7 @@ __global__ __launch_bounds__(64 * WI_WAVES, 1) void welch_i8_kernel(const int16_
             digits(w, ah[ks], al[ks]);
         }
         const int64_t tn = t + nslot < t_hi ? t + nslot : t;  // the last tile re-reads itself (unused)
-        {
+        if (WI_PREFETCH) {
             const int16_t *p = row_ptr(tn);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
@@ -382,7 +395,8 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
     A.bpt = 16 / p->nseg;
     A.nct = nct;
     const size_t per_ct = (size_t)WI_ND * KS * 64 * 16 + sizeof(int) * WI_NW * 16 + sizeof(double) * 8;
-    A.cg = (int)std::max<size_t>(1, std::min<size_t>((size_t)nct, WI_LDS_B / per_ct));
+    const size_t scratch = sizeof(double) * WI_WAVES * 16 * WI_PP;
+    A.cg = (int)std::max<size_t>(1, std::min<size_t>((size_t)nct, (WI_LDS - scratch) / per_ct));
     A.ngroups = (nct + A.cg - 1) / A.cg;
     A.cg = (nct + A.ngroups - 1) / A.ngroups;  // balance the groups (39 tiles: 8 groups of 5 / 4)
     const int wg_per_xcd = std::max(1, p->ctx->num_cu / 8);
@@ -390,7 +404,7 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
     A.nslots = p->nslots;
     A.xscale = std::ldexp(c.sample_scale, -53);
     A.scale = c.scale;
-    const size_t lds = (size_t)A.cg * per_ct + sizeof(double) * WI_WAVES * 16 * WI_PP;
+    const size_t lds = (size_t)A.cg * per_ct + scratch;
     const v4i *frag = static_cast<const v4i *>(p->d_i8);
     const char *base = static_cast<const char *>(p->d_i8) + (size_t)nct * WI_ND * KS * 64 * 16;
     const int *init = reinterpret_cast<const int *>(base);
