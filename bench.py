@@ -216,16 +216,17 @@ LIVE_FS, LIVE_FILE_S, LIVE_FILES = 4000, 3600, 24
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec sheet (not listed in MI355X_MICROARCH.md)
 
 
-def cpu_baseline_live(pool, seconds):
+def cpu_baseline_live(pool, nfiles):
     """processor.py:177-507 restated (oracle/live_oracle.py): scipy welch per 0.2 s block, band
-    sums, the state machine — 1 thread, on `seconds` of the same audio."""
+    sums, the state machine — 1 thread, on the first `nfiles` recordings of the day."""
     from oracle import live_oracle as L
-    x = pool[0][: int(seconds * LIVE_FS)].astype(np.float64) / 32768.0
+    xs = [pool[i].astype(np.float64) / 32768.0 for i in range(nfiles)]
     t0 = time.perf_counter()
-    L.wav_file_process_ref(x, LIVE_FS, L.ConfigDetectionRef(detection_db_over_noise_mean_min=1,
-                                                            detection_dur_min_sec=0.5))
+    for x in xs:
+        L.wav_file_process_ref(x, LIVE_FS, L.ConfigDetectionRef(detection_db_over_noise_mean_min=1,
+                                                                detection_dur_min_sec=0.5))
     dt = time.perf_counter() - t0
-    return len(x) / dt / 1e6, dt
+    return sum(len(x) for x in xs) / dt / 1e6, dt
 
 
 def live_rows(rank):
@@ -329,10 +330,10 @@ def run_live(a, ctx, job, rank, world, rows):
                        "max_decision_bound_db": float(np.max(lb.decision_bounds)),
                        "min_margin_db": float(np.min(lb.min_margins))}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
-        secs = 900
-        v, dt = cpu_baseline_live(rows, secs)
+        nf = 6
+        v, dt = cpu_baseline_live(rows, nf)
         out["cpu_baseline"] = {"value": round(v, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
-                               "sample": f"{secs} s of one 4 kHz file ({dt:.1f} s): scipy welch per block + "
+                               "sample": f"{nf} of the 1 h 4 kHz files ({dt:.1f} s): scipy welch per block + "
                                          f"band sums + state machine (oracle/live_oracle.py), 1 thread"}
     out["ranks_seen"] = job.ranks_seen() if job is not None else 1
     lb.close()
@@ -539,13 +540,14 @@ def run_c5(a, ctx, job, rank, world, rows):
                               "frac_of_hbm": round(xb / (dms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dms > 0 else None}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_files > 0:
         from oracle import iq_oracle as Q
-        m = C5_FS * 60  # one minute of the stream
-        z = pool[0]
+        mins = 10
+        m = C5_FS * 60 * mins  # the first 10 minutes of the rank's stream (~8 s on one core)
+        z = pool[:mins].reshape(-1)  # consecutive minutes of the stream
         t1 = time.perf_counter()
         Q.proc_iq_ref(z[0:2 * m:2], z[1:2 * m:2], C5_FS, C5_BAND, C5_NOISE, C5_N, C5_N - C5_HOP, 4.0)
         dt = time.perf_counter() - t1
         out["cpu_baseline"] = {"value": round(m / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
-                               "sample": f"60 s of the 192 kHz I/Q stream ({dt:.1f} s): scipy.signal.spectrogram "
+                               "sample": f"{mins} min of the 192 kHz I/Q stream ({dt:.1f} s): scipy.signal.spectrogram "
                                          f"(complex input, 4096/3072) + per-frame band sums + adaptive detector "
                                          f"(oracle/iq_oracle.py), 1 thread"}
     out["ranks_seen"] = job.ranks_seen() if job is not None else 1

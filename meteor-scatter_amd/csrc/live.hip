@@ -2,9 +2,10 @@
 //   welch_bands_kernel  a8  per processing block: scipy.signal.welch(block, fs, nfft=n_fft)
 //                           (processor.py:206) restricted to the bins of the three bands, and
 //                           the band sums → dB (processor.py:349-369)
-//   live_detect_kernel  a9  the over-noise value, its history threshold and the
+//   live_seg_*_kernel   a9  the over-noise value, its history threshold and the
 //                           Init / Detection / Tracking state machine (processor.py:391-507)
 //
+// (int16 audio takes welch_i8.hip's exact integer GEMM instead of welch_bands_kernel by default.)
 // welch_bands_kernel: one wave per block.  Each Welch segment's samples are staged in the
 // wave's LDS as float64 (times the soundfile scale), detrended with the numpy-order mean and
 // windowed; then every band bin (one lane each) runs a float64 Goertzel recurrence over the
@@ -15,8 +16,9 @@
 // live_over_kernel, live_history_kernel: the over-noise values, then the history thresholds
 // mean + k*std of the previous W of them -- state-free, one thread per block of every file
 // (the whole GPU, not one workgroup per file);
-// live_detect_kernel: one workgroup per file runs the state machine, 16 time segments in
-// parallel (one wave each, ballots) to a fixed point over their entry states.
+// live_seg_{init,scan,link,emit}_kernel: the state machine in 128-block time segments, one wave
+// each over the whole GPU (ballots), rounds of scan + link to a fixed point over their entry states,
+// then one emitting pass.
 #include <cmath>
 
 #include "msd_internal.h"
@@ -306,16 +308,19 @@ __global__ __launch_bounds__(WL_THREADS) void live_history_kernel(const int64_t 
     thr[f * A.ld + i] = mean + A.cfg.k_std * sd;
 }
 
-// the state machine of one file, time-segmented: wave w of the file's workgroup scans blocks
-// [a_w, b_w).  Segment 0 starts from the true initial state (Init); the others start from the
-// memoryless Detection state (no lock), which is where a file spends most of its time.  After
-// each round every segment whose entry differs from its predecessor's exit re-scans from that
-// exit, until no entry changes (normally 2 rounds); the final entries are then exact, and a
-// last pass per segment writes the thresholds used and the meteors at offsets from the
-// segments' meteor counts.  A segment's scan: at position k lane j evaluates block k+j under
-// the current state; the first block whose event condition holds (ballot) is where the state
-// changes, so a 64-block span without events is one step.
-constexpr int LV_SEGS = 16;  // segments (waves) per file
+// the state machine of one file, time-segmented: segment s scans blocks [s L, (s + 1) L) of its file
+// (L = LV_SEGLEN; one wave per segment, every file's segments over the whole GPU).  Segment 0 starts
+// from the true initial state (Init); the others from the memoryless Detection state (no lock),
+// which is where a file spends most of its time.  After each round every segment whose entry
+// differs from its predecessor's exit re-scans from that exit, until no entry changes (normally 2-3
+// rounds); the final entries are then exact, and a last pass per segment writes the thresholds used
+// and the meteors at offsets from the earlier segments' meteor counts.  A segment's scan: at position
+// k lane j evaluates block k + j under the current state; the first block whose event condition holds
+// (ballot) is where the state changes, so a 64-block span without events is one step.
+// (Rounds 1-5 ran one 16-wave workgroup per file with the rounds inside it: 24 files used 24 CUs,
+// 0.65-0.70 ms per day.)
+constexpr int LV_SEGLEN = 128;  // blocks per segment
+constexpr int LV_ROUNDS = 4;    // rounds launched before the convergence flag is read
 
 __device__ __forceinline__ bool live_same_entry(const LiveScan &x, const LiveScan &y, double t1_first) {
     if (x.state != y.state) return false;
@@ -331,124 +336,152 @@ __device__ __forceinline__ bool live_same_entry(const LiveScan &x, const LiveSca
     return true;
 }
 
-__global__ __launch_bounds__(LV_SEGS * 64) void live_detect_kernel(const double *__restrict__ band_db,
-                                                                   const int64_t *__restrict__ nblocks, LiveArgs A,
-                                                                   double *__restrict__ over, double *__restrict__ thr,
-                                                                   msd_meteor *__restrict__ out,
-                                                                   int64_t *__restrict__ counts,
-                                                                   int32_t *__restrict__ status) {
-    const int64_t f = blockIdx.x;
-    if (f >= A.nfiles) return;
+struct LiveSegArgs {
+    LiveArgs L;
+    int64_t smax;  // segments per file slot: ceil(ld / LV_SEGLEN)
+};
+
+__device__ __forceinline__ double live_tblk(const msd_live_cfg &C, int64_t i) {
+    return (double)(i * (int64_t)C.block_size) / C.fs;
+}
+
+// one wave's pass over blocks [a, b) of one file from sc; emit: write the thresholds used and the meteors
+__device__ __forceinline__ void live_scan(LiveScan &sc, int64_t a, int64_t b, bool emit, const double *ov, double *th,
+                                          const msd_live_cfg &C, msd_meteor *outf, int64_t cap, int lane) {
+    int64_t k = a;
+    while (k < b) {
+        const int64_t kk = k + lane;
+        const bool valid = kk < b;
+        const int64_t kc = valid ? kk : b - 1;
+        const double v = ov[kc], fresh = th[kc], t0 = live_tblk(C, kc), t1 = live_tblk(C, kc + 1);
+        double t;
+        bool cand;
+        if (sc.state == 0) {
+            t = fresh;
+            cand = t0 >= C.init_wait_sec;
+        } else if (sc.state == 1) {
+            t = sc.until > t1 ? sc.lock : fresh;
+            cand = v > t;
+        } else {
+            t = sc.lock;
+            cand = v < t;
+        }
+        const uint64_t mask = __ballot(valid && cand);
+        const int first = mask ? __builtin_ctzll(mask) : 64;
+        if (emit && valid && lane <= first) th[kk] = t;  // thresholds used (processor.py:395-412)
+        if (!mask) {
+            k += 64;
+            continue;
+        }
+        const int64_t e = k + first;  // event block
+        const double te = __shfl(t, first), t0e = __shfl(t0, first);
+        if (sc.state == 0) {
+            sc.state = 1;
+            sc.lock = -1.0;
+            sc.until = -1.0;
+        } else if (sc.state == 1) {
+            sc = live_trigger(sc, ov, e, te, t0e, C.avg_win_blocks);
+        } else {
+            sc = live_close(sc, ov, e, t0e, C.min_db_mean, C.min_dur_sec, C.after_tracking_wait_sec, outf, cap,
+                            emit && lane == 0);
+        }
+        k = e + 1;
+    }
+}
+
+// the segments' states: in / out [nfiles][smax] (entry, exit), cnt (meteors), active
+struct LiveSegState {
+    LiveScan *in, *out;
+    int64_t *cnt;
+    int32_t *active;
+    int32_t *changed;  // [1]: some entry changed in the last link
+};
+
+// entries of round 1: Init at each file's start, Detection elsewhere; counts / status of empty files
+__global__ __launch_bounds__(256) void live_seg_init_kernel(const int64_t *__restrict__ nblocks, LiveSegArgs A,
+                                                            LiveSegState S, int64_t *__restrict__ counts,
+                                                            int32_t *__restrict__ status) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.L.nfiles * A.smax) return;
+    const int64_t f = i / A.smax, s = i - f * A.smax;
     const int64_t nb = nblocks[f];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const double *ov = over + f * A.ld;  // over-noise values and fresh history thresholds: the two
-    double *th = thr + f * A.ld;         // kernels above; th is overwritten with the thresholds used
-    const msd_live_cfg &C = A.cfg;
-    const int64_t seg = (nb + LV_SEGS - 1) / LV_SEGS;
-    const int64_t a = w * seg < nb ? w * seg : nb;
-    const int64_t b = a + seg < nb ? a + seg : nb;
-    auto tblk = [&](int64_t i) { return (double)(i * (int64_t)C.block_size) / C.fs; };
-    // (LiveScan has default member initialisers, which __shared__ variables may not have)
-    __shared__ __attribute__((aligned(16))) char s_state[2 * LV_SEGS * sizeof(LiveScan)];
-    LiveScan *s_in = reinterpret_cast<LiveScan *>(s_state), *s_out = s_in + LV_SEGS;
-    __shared__ int64_t s_cnt[LV_SEGS];
-    __shared__ int s_active[LV_SEGS], s_changed;
+    LiveScan e0;
+    if (s > 0) {
+        e0.state = 1;
+        e0.lock = -1.0;
+        e0.until = -1.0;
+    }
+    S.in[i] = e0;
+    S.active[i] = s * LV_SEGLEN < nb;
+    if (s == 0 && nb <= 0) {  // no segment: no meteors
+        counts[f] = 0;
+        if (status) status[f] = 0;
+    }
+}
 
-    // one pass over the segment from sc; emit: write the thresholds used and the meteors
-    auto scan = [&](LiveScan &sc, bool emit) {
-        int64_t k = a;
-        while (k < b) {
-            const int64_t kk = k + lane;
-            const bool valid = kk < b;
-            const int64_t kc = valid ? kk : b - 1;
-            const double v = ov[kc], fresh = th[kc], t0 = tblk(kc), t1 = tblk(kc + 1);
-            double t;
-            bool cand;
-            if (sc.state == 0) {
-                t = fresh;
-                cand = t0 >= C.init_wait_sec;
-            } else if (sc.state == 1) {
-                t = sc.until > t1 ? sc.lock : fresh;
-                cand = v > t;
-            } else {
-                t = sc.lock;
-                cand = v < t;
-            }
-            const uint64_t mask = __ballot(valid && cand);
-            const int first = mask ? __builtin_ctzll(mask) : 64;
-            if (emit && valid && lane <= first) th[kk] = t;  // thresholds used (processor.py:395-412)
-            if (!mask) {
-                k += 64;
-                continue;
-            }
-            const int64_t e = k + first;  // event block
-            const double te = __shfl(t, first), t0e = __shfl(t0, first);
-            if (sc.state == 0) {
-                sc.state = 1;
-                sc.lock = -1.0;
-                sc.until = -1.0;
-            } else if (sc.state == 1) {
-                sc = live_trigger(sc, ov, e, te, t0e, C.avg_win_blocks);
-            } else {
-                sc = live_close(sc, ov, e, t0e, C.min_db_mean, C.min_dur_sec, C.after_tracking_wait_sec, out + f * A.cap,
-                                A.cap, emit && lane == 0);
-            }
-            k = e + 1;
-        }
-    };
-
+// one wave per active segment: scan from its entry, record its exit and meteor count
+__global__ __launch_bounds__(256) void live_seg_scan_kernel(const int64_t *__restrict__ nblocks, LiveSegArgs A,
+                                                            LiveSegState S, const double *__restrict__ over,
+                                                            double *__restrict__ thr) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= A.L.nfiles * A.smax || !S.active[i]) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int64_t f = i / A.smax, s = i - f * A.smax;
+    const int64_t nb = nblocks[f];
+    const int64_t a = s * LV_SEGLEN, b = a + LV_SEGLEN < nb ? a + LV_SEGLEN : nb;
+    LiveScan sc = S.in[i];
+    sc.cnt = 0;
+    live_scan(sc, a, b, false, over + f * A.L.ld, thr + f * A.L.ld, A.L.cfg, nullptr, 0, lane);
     if (lane == 0) {
-        LiveScan e0;  // Init at the file start, memoryless Detection elsewhere (speculative)
-        if (w > 0) {
-            e0.state = 1;
-            e0.lock = -1.0;
-            e0.until = -1.0;
-        }
-        s_in[w] = e0;
-        s_active[w] = 1;
+        S.out[i] = sc;
+        S.cnt[i] = sc.cnt;
     }
-    __syncthreads();
-    for (;;) {
-        if (s_active[w]) {
-            LiveScan sc = s_in[w];
-            sc.cnt = 0;
-            scan(sc, false);
-            if (lane == 0) {
-                s_out[w] = sc;
-                s_cnt[w] = sc.cnt;
-            }
+}
+
+// a segment whose entry differs from its predecessor's exit re-scans from that exit next round
+__global__ __launch_bounds__(256) void live_seg_link_kernel(const int64_t *__restrict__ nblocks, LiveSegArgs A,
+                                                            LiveSegState S) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.L.nfiles * A.smax) return;
+    const int64_t f = i / A.smax, s = i - f * A.smax;
+    const int64_t a = s * LV_SEGLEN;
+    int act = 0;
+    if (s > 0 && a < nblocks[f]) {  // (an empty segment's exit is its entry: its scan does nothing)
+        const LiveScan nw = S.out[i - 1];
+        if (!live_same_entry(nw, S.in[i], live_tblk(A.L.cfg, a + 1))) {
+            S.in[i] = nw;
+            act = 1;
+            *S.changed = 1;
         }
-        if (tid == 0) s_changed = 0;
-        __syncthreads();
-        if (lane == 0) {  // (an empty segment's exit is its entry: the scan does nothing)
-            int act = 0;
-            if (w > 0) {
-                const LiveScan nw = s_out[w - 1];
-                if (!live_same_entry(nw, s_in[w], tblk(a + 1))) {
-                    s_in[w] = nw;
-                    act = 1;
-                    atomicOr(&s_changed, 1);
-                }
-            }
-            s_active[w] = act;
-        }
-        __syncthreads();
-        if (!s_changed) break;
-        __syncthreads();  // everyone has read s_changed before the next round resets it
     }
-    // final pass: exact entries, meteors at the offsets of the earlier segments' counts
-    int64_t off = 0;
-    for (int j = 0; j < w; ++j) off += s_cnt[j];
-    {
-        LiveScan sc = s_in[w];
-        sc.cnt = off;
-        scan(sc, true);
+    S.active[i] = act;
+}
+
+// final pass from the exact entries: the thresholds used and the meteors at the offsets of the
+// earlier segments' counts; the file's last segment writes its count and status
+__global__ __launch_bounds__(256) void live_seg_emit_kernel(const int64_t *__restrict__ nblocks, LiveSegArgs A,
+                                                            LiveSegState S, const double *__restrict__ over,
+                                                            double *__restrict__ thr, msd_meteor *__restrict__ out,
+                                                            int64_t *__restrict__ counts,
+                                                            int32_t *__restrict__ status) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= A.L.nfiles * A.smax) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t f = i / A.smax, s = i - f * A.smax;
+    const int64_t nb = nblocks[f];
+    const int64_t a = s * LV_SEGLEN;
+    if (a >= nb) return;  // wave-uniform
+    const int64_t b = a + LV_SEGLEN < nb ? a + LV_SEGLEN : nb;
+    int64_t off = 0;  // meteors of the file's earlier segments
+    for (int64_t j = lane; j < s; j += 64) off += S.cnt[i - s + j];
+    for (int o = 32; o > 0; o >>= 1) off += __shfl_xor(off, o, 64);
+    LiveScan sc = S.in[i];
+    sc.cnt = off;
+    live_scan(sc, a, b, true, over + f * A.L.ld, thr + f * A.L.ld, A.L.cfg, out + f * A.L.cap, A.L.cap, lane);
+    if (lane == 0 && b == nb) {
+        counts[f] = sc.cnt;
+        if (status) status[f] = sc.cnt > A.L.cap ? 3 : 0;
     }
-    if (tid != 0) return;
-    int64_t cnt = 0;
-    for (int j = 0; j < LV_SEGS; ++j) cnt += s_cnt[j];
-    counts[f] = cnt;
-    if (status) status[f] = cnt > A.cap ? 3 : 0;
 }
 
 template <typename T>
@@ -522,8 +555,41 @@ int launch_live(msd_ctx *ctx, const double *band_db, const int64_t *nblocks, int
         hipLaunchKernelGGL(live_over_kernel, grid, dim3(WL_THREADS), 0, ctx->stream, band_db, nblocks, A, over);
         hipLaunchKernelGGL(live_history_kernel, grid, dim3(WL_THREADS), 0, ctx->stream, nblocks, A, over, thr);
     }
-    hipLaunchKernelGGL(live_detect_kernel, dim3((unsigned)nfiles), dim3(LV_SEGS * 64), 0, ctx->stream, band_db, nblocks,
-                       A, over, thr, out, counts, status);
+    LiveSegArgs G{};
+    G.L = A;
+    G.smax = ld > 0 ? (ld + LV_SEGLEN - 1) / LV_SEGLEN : 1;
+    const int64_t nseg = nfiles * G.smax;
+    const size_t b_state = sizeof(LiveScan) * (size_t)nseg, b_cnt = sizeof(int64_t) * (size_t)nseg,
+                 b_act = sizeof(int32_t) * (size_t)nseg;
+    void *sp = nullptr;
+    if (int rc = ctx_scratch(ctx, 6, 2 * b_state + b_cnt + b_act + 64, &sp)) return rc;
+    char *base = static_cast<char *>(sp);
+    LiveSegState S;
+    S.in = reinterpret_cast<LiveScan *>(base);
+    S.out = reinterpret_cast<LiveScan *>(base + b_state);
+    S.cnt = reinterpret_cast<int64_t *>(base + 2 * b_state);
+    S.active = reinterpret_cast<int32_t *>(base + 2 * b_state + b_cnt);
+    S.changed = reinterpret_cast<int32_t *>(base + 2 * b_state + b_cnt + b_act);
+    if (nseg > 0x7fffffffLL) return fail(MSD_ERR_UNSUPPORTED, "live: too many segments");
+    const unsigned g_thr = (unsigned)((nseg + 255) / 256), g_wave = (unsigned)((nseg + 3) / 4);
+    hipStream_t st = ctx->stream;
+    hipLaunchKernelGGL(live_seg_init_kernel, dim3(g_thr), dim3(256), 0, st, nblocks, G, S, counts, status);
+    // rounds: scan the active segments, then link every segment to its predecessor's exit.  The
+    // first LV_ROUNDS go out unchecked (segments with nothing to do exit at once); then the flag of
+    // the last link is read, and more rounds follow while it is set
+    for (int64_t r = 0;; ++r) {
+        hipLaunchKernelGGL(live_seg_scan_kernel, dim3(g_wave), dim3(256), 0, st, nblocks, G, S, over, thr);
+        MSD_HIP(hipMemsetAsync(S.changed, 0, sizeof(int32_t), st));
+        hipLaunchKernelGGL(live_seg_link_kernel, dim3(g_thr), dim3(256), 0, st, nblocks, G, S);
+        if (r + 1 < LV_ROUNDS) continue;
+        int32_t changed = 0;
+        MSD_HIP(hipMemcpyAsync(&changed, S.changed, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        MSD_HIP(hipStreamSynchronize(st));
+        if (!changed) break;
+        if (r > G.smax + LV_ROUNDS) return fail(MSD_ERR_HIP, "live: segment states did not converge");
+    }
+    hipLaunchKernelGGL(live_seg_emit_kernel, dim3(g_wave), dim3(256), 0, st, nblocks, G, S, over, thr, out, counts,
+                       status);
     MSD_HIP(hipGetLastError());
     return MSD_OK;
 }

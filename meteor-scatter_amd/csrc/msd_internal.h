@@ -52,8 +52,8 @@ struct msd_ctx {
     // scratch device buffers for the host-pointer convenience entry points
     // (slot 4: msd_iq_delta64_dev's block table, rotations and ranges; slot 5 unused since the
     // post-FFT detrend's side records went, round 5)
-    void *scratch[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    size_t scratch_bytes[6] = {0, 0, 0, 0, 0, 0};
+    void *scratch[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t scratch_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // msd_iq_delta64_dev's twiddle table W^m (m < rf_w_n), built once per frame length
     double2 *rf_w = nullptr;
     int rf_w_n = 0;

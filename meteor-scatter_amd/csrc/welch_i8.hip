@@ -52,6 +52,8 @@ constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
 // waves per workgroup: 12 = 3 per SIMD (154 VGPRs).  Against 8 (2 per SIMD): 5.52-5.55 vs
 // 5.97-6.04 ms per day (profiles/r6_welch_i8_ab.txt)
 constexpr int WI_WAVES = WI_WAVES_N;
+// waves per workgroup for KS K steps: 8 K steps (nperseg 512) need 236 VGPRs, 2 waves per SIMD
+constexpr int wi_waves(int KS) { return KS <= 4 ? WI_WAVES : 8; }
 constexpr int WI_PP = 9;                  // per-wave power scratch: 16 rows x 8 bins, pitch 9 doubles
 constexpr size_t WI_LDS = 160 * 1024;     // LDS of one workgroup: B fragments + per-wave power scratch
 constexpr int WI_MAXKS = 8;               // nperseg <= 512 (16 K steps would spill)
@@ -124,13 +126,14 @@ __device__ __forceinline__ BlockRef block_of(const int16_t *x, const int64_t *of
 // B fragments; colinit: [nct][NW][16] the accumulator start values (128 sum_n d of the l' products);
 // dbl: [nct * 8] the onesided doubling (1 at DC / Nyquist, else 2; 0 past nslots).
 template <int KS>
-__global__ __launch_bounds__(64 * WI_WAVES, 1) void welch_i8_kernel(const int16_t *__restrict__ x,
+__global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const int16_t *__restrict__ x,
                                                                     const int64_t *__restrict__ off,
                                                                     const int64_t *__restrict__ len, WelchI8Args A,
                                                                     const v4i *__restrict__ bfrag,
                                                                     const int *__restrict__ colinit,
                                                                     const double *__restrict__ dbl,
                                                                     double *__restrict__ psd) {
+    constexpr int NW = wi_waves(KS);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int xcd = blockIdx.x & 7, iw = blockIdx.x >> 3;
     const int cgi = iw % A.ngroups, rep = iw / A.ngroups;
@@ -139,11 +142,11 @@ __global__ __launch_bounds__(64 * WI_WAVES, 1) void welch_i8_kernel(const int16_
     if (nct <= 0) return;                    // workgroup-uniform, before any barrier
     v4i *sB = reinterpret_cast<v4i *>(smem);                                        // [cg][ND][KS][64]
     double *sP = reinterpret_cast<double *>(sB + (size_t)A.cg * WI_ND * KS * 64);   // [WAVES][16][PP]
-    double *sDbl = sP + WI_WAVES * 16 * WI_PP;                                      // [cg][8]
+    double *sDbl = sP + NW * 16 * WI_PP;                                      // [cg][8]
     int *sInit = reinterpret_cast<int *>(sDbl + A.cg * 8);                          // [cg][NW][16]
-    for (int i = threadIdx.x; i < nct * WI_ND * KS * 64; i += 64 * WI_WAVES) sB[i] = bfrag[(size_t)ct0 * WI_ND * KS * 64 + i];
-    for (int i = threadIdx.x; i < nct * WI_NW * 16; i += 64 * WI_WAVES) sInit[i] = colinit[ct0 * WI_NW * 16 + i];
-    for (int i = threadIdx.x; i < nct * 8; i += 64 * WI_WAVES) sDbl[i] = dbl[ct0 * 8 + i];
+    for (int i = threadIdx.x; i < nct * WI_ND * KS * 64; i += 64 * NW) sB[i] = bfrag[(size_t)ct0 * WI_ND * KS * 64 + i];
+    for (int i = threadIdx.x; i < nct * WI_NW * 16; i += 64 * NW) sInit[i] = colinit[ct0 * WI_NW * 16 + i];
+    for (int i = threadIdx.x; i < nct * 8; i += 64 * NW) sDbl[i] = dbl[ct0 * 8 + i];
     __syncthreads();
     const int l = threadIdx.x & 63;
     const int c = l & 15, g = l >> 4;
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(64 * WI_WAVES, 1) void welch_i8_kernel(const int16_
     // this XCD's contiguous share of the M tiles; the workgroups of every column group walk it in
     // the same order (stride = the wave slots of one group on this XCD)
     const int64_t t_lo = ntm * xcd / 8, t_hi = ntm * (xcd + 1) / 8;
-    const int64_t slot0 = (int64_t)rep * WI_WAVES + wv, nslot = (int64_t)A.reps * WI_WAVES;
+    const int64_t slot0 = (int64_t)rep * NW + wv, nslot = (int64_t)A.reps * NW;
 
     // the lane's A row: row c = segment c % nseg of block c / nseg of the tile (rows past nrow and
     // missing blocks read the file start, their results unused)
@@ -256,7 +259,11 @@ __global__ __launch_bounds__(64 * WI_WAVES, 1) void welch_i8_kernel(const int16_
 }
 
 // band_db[(f nbands + j) ld + b] = 10 log10(np.sum(psd[band j])) (-inf when not > 0) of every block
-// (f, b) that exists: one thread per (block, band), numpy's pairwise order over the band's slots
+// (f, b) that exists.  A wave takes 8 blocks, 8 lanes each: lane r of a block accumulates numpy's
+// interleaved partial r_r = p[r] + p[r + 8] + ... (the pairwise leaf's 8 accumulators, so the 8
+// lanes read 64 contiguous bytes per step), three DPP steps combine them as
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), and the block's lane 0 adds the tail in order:
+// np.sum's association for a band of 8 <= n <= 128 bins.  Other widths take np_sum on lane 0.
 struct BandArgs {
     int64_t nfiles, max_blocks, ld;
     int block_size, nslots, nbands;
@@ -266,19 +273,41 @@ struct BandArgs {
 __global__ __launch_bounds__(256) void welch_i8_bands_kernel(const int64_t *__restrict__ len, BandArgs A,
                                                              const double *__restrict__ psd,
                                                              double *__restrict__ band_db) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, r = lane & 7;
+    const int64_t gb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);  // this lane's block
     const int64_t nb_all = A.nfiles * A.max_blocks;
-    if (i >= nb_all * A.nbands) return;
-    const int j = (int)(i % A.nbands);
-    const int64_t gb = i / A.nbands;
-    const int64_t f = gb / A.max_blocks, b = gb - f * A.max_blocks;
-    const int64_t n = len[f];
-    const int64_t nb = n >= A.block_size ? (n - A.block_size) / A.block_size + 1 : 0;
-    if (b >= nb) return;
-    const int w = A.width[j];
-    const GArrRef row{as_global(psd + (f * A.ld + b) * (int64_t)A.nslots)};
-    const double P = w <= 0 ? 0.0 : (w <= 128 ? np_sum_small(row, A.slot0[j], w) : np_sum(row, A.slot0[j], w));
-    band_db[(f * A.nbands + j) * A.ld + b] = P > 0.0 ? 10.0 * log10(P) : -INFINITY;
+    const bool in = gb < nb_all;
+    const int64_t f = in ? gb / A.max_blocks : 0, b = in ? gb - f * A.max_blocks : 0;
+    bool ok = false;
+    if (in) {
+        const int64_t n = len[f];
+        ok = b < (n >= A.block_size ? (n - A.block_size) / A.block_size + 1 : 0);
+    }
+    const double *rowp = psd + (f * A.ld + b) * (int64_t)A.nslots;
+    const GArrRef row{as_global(rowp)};
+    for (int j = 0; j < A.nbands; ++j) {
+        const int w = A.width[j], s0 = A.slot0[j];
+        double P = 0.0;
+        if (w >= 8 && w <= 128) {
+#pragma clang fp contract(off)
+            const int lim = w - (w % 8);
+            double acc = 0.0;
+            if (ok) {
+                acc = row(s0 + r);
+                for (int k = 8 + r; k < lim; k += 8) acc += row(s0 + k);
+            }
+            acc = acc + dpp64<0xB1>(acc);   // r0 + r1, r2 + r3, ...
+            acc = acc + dpp64<0x4E>(acc);   // (r0 + r1) + (r2 + r3), (r4 + r5) + (r6 + r7)
+            acc = acc + dpp64<0x141>(acc);  // half-row mirror: lane 0 meets lane 7
+            if (r == 0 && ok) {
+                for (int k = lim; k < w; ++k) acc += row(s0 + k);
+                P = 0.0 + acc;
+            }
+        } else if (r == 0 && ok && w > 0) {
+            P = w < 8 ? np_sum_small(row, s0, w) : np_sum(row, s0, w);
+        }
+        if (r == 0 && ok) band_db[(f * A.nbands + j) * A.ld + b] = P > 0.0 ? 10.0 * log10(P) : -INFINITY;
+    }
 }
 
 // one balanced base-256 digit expansion of T: T = sum_b d[b] 256^(6 - b); false if T needs more
@@ -395,7 +424,8 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
     A.bpt = 16 / p->nseg;
     A.nct = nct;
     const size_t per_ct = (size_t)WI_ND * KS * 64 * 16 + sizeof(int) * WI_NW * 16 + sizeof(double) * 8;
-    const size_t scratch = sizeof(double) * WI_WAVES * 16 * WI_PP;
+    const int nw = wi_waves(KS);
+    const size_t scratch = sizeof(double) * nw * 16 * WI_PP;
     A.cg = (int)std::max<size_t>(1, std::min<size_t>((size_t)nct, (WI_LDS - scratch) / per_ct));
     A.ngroups = (nct + A.cg - 1) / A.cg;
     A.cg = (nct + A.ngroups - 1) / A.ngroups;  // balance the groups (39 tiles: 8 groups of 5 / 4)
@@ -416,7 +446,7 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
 #define WI_CASE(K)                                                                                            \
     case K:                                                                                                   \
         if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(welch_i8_kernel<K>), 160 * 1024)) return rc; \
-        hipLaunchKernelGGL(welch_i8_kernel<K>, dim3(grid), dim3(64 * WI_WAVES), lds, st, x, off, len, A, frag, init, \
+        hipLaunchKernelGGL(welch_i8_kernel<K>, dim3(grid), dim3(64 * nw), lds, st, x, off, len, A, frag, init, \
                            dbl, psd);                                                                         \
         break;
         WI_CASE(1)
@@ -441,8 +471,8 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
         B.width[j] = c.band_hi[j] >= c.band_lo[j] ? c.band_hi[j] - c.band_lo[j] + 1 : 0;
         s0 += B.width[j];
     }
-    const int64_t nthreads = nfiles * max_blocks * c.nbands;
-    hipLaunchKernelGGL(welch_i8_bands_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, st, len, B, psd,
+    const int64_t nwg = (nfiles * max_blocks + 31) / 32;  // 8 blocks per wave, 4 waves per workgroup
+    hipLaunchKernelGGL(welch_i8_bands_kernel, dim3((unsigned)nwg), dim3(256), 0, st, len, B, psd,
                        band_db);
     MSD_HIP(hipGetLastError());
     return MSD_OK;

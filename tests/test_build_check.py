@@ -27,12 +27,13 @@ pytestmark = pytest.mark.skipif(not (os.path.exists(SO) and shutil.which("/opt/r
 
 # kernels allowed to call out-of-line device functions (each callee is held to zero flat instructions
 # below): the live scan's two event handlers (one call per meteor)
-CALLERS = ("live_detect_kernel",)
+CALLERS = ("live_seg_scan_kernel", "live_seg_emit_kernel")
 
 # the hot kernels of the benchmarked paths (C3, C5, live): no scratch at all
 NO_SCRATCH = ("stft1024_kernel", "block_band_i8_kernel", "block_i8_kernel", "block_db_kernel", "detect_kernel",
               "welch_bands_kernel", "iq_band_delta_kernel", "scan_kernel", "frame_kernel", "live_over_kernel",
-              "live_history_kernel", "welch_i8_kernel", "welch_i8_bands_kernel")
+              "live_history_kernel", "welch_i8_kernel", "welch_i8_bands_kernel", "live_seg_init_kernel",
+              "live_seg_link_kernel")
 
 
 @pytest.fixture(scope="module")
