@@ -194,6 +194,28 @@ def test_over_noise_within_bound(live, fs, bs, nfft, f0):
     assert err[fin].max() < 1e-6  # not vacuous
 
 
+@pytest.mark.parametrize("wait,dur", [(200.0, 60), (30.0, 400), (0.0, 1000)])
+def test_state_machine_states_across_many_segments(live, wait, dur):
+    """the whole-GPU state machine (128-block segments, rounds of scan / link): a lock held for
+    1000 blocks after tracking, tracking runs of 400 and 1000 blocks -- a segment's entry then
+    depends on states set 8+ segments earlier, so the rounds go past the first four and the
+    convergence flag is read more than once; bit-exact against the oracle"""
+    rng = np.random.default_rng(int(wait) + dur)
+    nb = 9000
+    sig = rng.normal(0, 1, nb)
+    for s in (300, 2100, 5050, 7777):
+        sig[s:s + dur] += 30
+    rows = np.stack([sig, rng.normal(0, 0.5, nb), rng.normal(0, 0.5, nb)])
+    cfg = live.ConfigDetection(after_tracking_wait_sec=wait)
+    m, thr, over = live.live_detect(rows, 4000, cfg)
+    rm, rthr, rover = L.live_detect_ref(rows, 4000, 800, _ref_cfg(cfg))
+    np.testing.assert_array_equal(over, rover)
+    np.testing.assert_array_equal(thr, rthr)
+    got = [(a.time_start, a.time_stop, a.db_min, a.db_max, a.db_mean, a.db_std) for a in m]
+    assert got == [(b.time_start, b.time_stop, b.db_min, b.db_max, b.db_mean, b.db_std) for b in rm]
+    assert len(m) >= 1
+
+
 def test_state_machine_long_rows_cross_chunks(live):
     """nb > the kernel's 2048-block LDS chunk: runs and histories straddling chunk edges."""
     rng = np.random.default_rng(11)
