@@ -31,7 +31,7 @@ def _bench(*args, timeout=240):
 
 
 def test_spawn_c3():
-    """the default line: C3 (weak), the C4 strong-scaling pass over the same ranks, and C5 appended"""
+    """the default line: C3 (weak), the C4 strong-scaling pass over the same ranks, C5 and live appended"""
     d = _bench("--files", "16", "--c5-seconds", "60")
     assert d["scaling"] == "weak" and d["config"]["files_per_gpu"] == 16 and d["roofline"]["frac"] > 0
     s = d["strong_scaling"]
@@ -39,6 +39,9 @@ def test_spawn_c3():
     assert s["hour_total"] == s["detections_per_step"] == d["detections_per_step"]  # same day at N = 1
     c5 = d["c5"]
     assert c5["value"] > 0 and c5["roofline"]["frac"] > 0 and c5["detections_per_step"] > 0
+    lv = d["live"]  # the live detector's day (round 6), through the same launched rank
+    assert lv["value"] > 0 and lv["ranks_seen"] == 1 and lv["meteors_per_step"] > 0
+    assert lv["near_tie"]["files"] == 24 and lv["near_tie"]["files_flagged"] == 0
 
 
 def test_spawn_c4_shard_day():
