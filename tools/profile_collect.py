@@ -38,6 +38,9 @@ for sub, name, kernel, match in ((tag, "stft", "stft1024_kernel<short, 0, true, 
     if name is None:
         continue
     summ = json.load(open(f"{pmc}/{sub}/summary.json"))[kernel]
+    if "hbm_bytes" not in summ:  # a pass missing (FETCH_SIZE or WRITE_SIZE): keep the last traffic file
+        print(f"{sub}: no complete FETCH_SIZE + WRITE_SIZE pair for {kernel}; profiles/{name}_pmc.json kept")
+        continue
     rec = {"kernel": kernel, "hbm_bytes_per_launch": summ["hbm_bytes"], "fetch_size_kib": summ["FETCH_SIZE"],
            "write_size_kib": summ["WRITE_SIZE"],
            "rule": "HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950: FETCH_SIZE reports half of wide "
@@ -58,12 +61,18 @@ lines = ["roofline kernel, per-dispatch durations (ms) from rocprofv3 --kernel-t
          f"bench.py --steps {KS} --warmup {KW}: dispatches 1-{KW} are the warm-up, {KW + 1}-{KW + KS} the timed "
          f"steps, {KW + KS + 1} the step after the timed region that times every kernel for the breakdown"]
 import csv
-for wl, key in (("", "stft1024_kernel"), ("_live", "welch_bands_kernel"), ("_c5", "cstft4096_kernel"),
+for wl, key in (("", "stft1024_kernel"), ("_live", "welch_i8_kernel"), ("_c5", "cstft4096_kernel"),
                 ("_c5x", "cstft4096_kernel")):
     if not os.path.exists(f"{src}/kt{wl}"):
         continue
     rows = list(csv.DictReader(open(f"{src}/kt{wl}/kt_kernel_trace.csv")))
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if key in r["Kernel_Name"]]
+    if wl == "_live":  # the live line's kernel_ms is welch_i8_kernel + welch_i8_bands_kernel (one each per step)
+        bd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows
+              if "welch_i8_bands_kernel" in r["Kernel_Name"]]
+        if len(bd) == len(d):
+            d = [a + b for a, b in zip(d, bd)]
+            key = "welch_i8_kernel + welch_i8_bands_kernel"
     b = last_json(f"{src}/kt{wl}.log")
     live = b["roofline"].get("kernel_ms")
     lines.append(f"{key} ({wl[1:] or 'c3'}): " + " ".join(f"{x:.3f}" for x in d) +

@@ -10,6 +10,10 @@ OUT=$ROOT/gpurun_out/round_$TAG
 # (the first ~5 dispatches of a fresh process run while it ramps)
 KS=${KT_STEPS:-10}; KW=${KT_WARMUP:-10}
 mkdir -p "$OUT"
+# STAGE=kt: the bench line and the kernel traces; STAGE=pmc: the PMC passes; default both (two calls
+# fit gpurun's per-call limit better than one)
+STAGE=${STAGE:-all}
+if [ "$STAGE" != pmc ]; then
 timeout -k 10 400 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- \
@@ -21,6 +25,9 @@ done
 # the certified C5 path (round 3): exact decisions, the float64 refinement kernels in the trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_c5x" -o kt -- \
     python3 "$ROOT/bench.py" --workload c5 --steps $KS --warmup $KW --no-cpu-baseline --c5-mode exact > "$OUT/kt_c5x.log" 2>&1 || exit 1
+fi
+[ "$STAGE" = kt ] && exit 0
+cd /tmp && export TMPDIR=/tmp
 bash "$ROOT/tools/pmc_stft.sh" "$TAG" || exit 1
 REGEX=cstft bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline --c5-mode exact
 REGEX="block_i8|frame_kernel" bash "$ROOT/tools/pmc_stft.sh" "${TAG}_c5i8" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline --c5-mode exact
