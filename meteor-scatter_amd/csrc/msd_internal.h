@@ -149,10 +149,12 @@ struct msd_welch_plan {
     int nslots = 0;               // bins computed per block (band ranges concatenated)
     double *d_window = nullptr;   // [nperseg]
     double *d_bins = nullptr;     // [nslots][4]: cos w, sin w, 2 cos w, doubling factor (1 or 2)
-    // int16 samples on the matrix cores (welch_i8.hip): B fragments, column start values and
-    // doubling factors of the nct column tiles; null when the plan's shape does not take that path
+    // int16 samples on the matrix cores (welch_i8.hip): B fragments and doubling factors of the
+    // nct column tiles; null when the plan's shape does not take that path
     void *d_i8 = nullptr;
     int i8_nct = 0;
+    bool i8_pairs = false;  // the accumulators' digit sums fit int32 pairs (welch_i8_build)
+    bool i8_special = true;  // the live default's shape takes its own instantiation
 };
 
 namespace msd {

@@ -9,9 +9,12 @@
 // T = round(c' 2^53) (|c'| <= 2) in seven balanced base-256 digits and each sample x = 256 h + l' + 128,
 // so every inner sum is one v_mfma_i32_16x16x64_i8 accumulation, exact in int32.  The products of
 // equal weight share an accumulator (h with digit b and l' with digit b + 1: weight 256^(7 - b)),
-// eight per component, combined by a float64 Horner sum.  Error against the exact DFT: the
-// coefficients' quantisation 2^-54 sum|x| plus the Horner sum's 8 roundings of partials below
-// 2 sum|x| -- margin.live_over_error's int8 term (16.5 u sum|x| <= 16.5 u nperseg max|x|).
+// eight per component.  The T of a component are rounded to sum exactly to zero (largest remainder),
+// so the offset's term 128 sum_n T_n vanishes and the accumulators start at zero; the eight are
+// combined exactly in int64 (two Horner groups of four, < 2^49 each) and rounded once to float64:
+// the result is round(sum_n (x_n - 128) T_n) = round(sum_n x_n T_n), zero for a silent block.  Error
+// against the exact DFT: the quantisation (|T - c' 2^53| < 1: 2^-53 sum|x|) and two roundings of
+// |X| <= 2 sum|x|, 5 u sum|x| -- inside margin.live_over_error's int8 term (18 u nperseg max|x|).
 //
 // GEMM: rows = segments (a 16-row tile holds bpt = 16 / nseg whole blocks, nseg rows each),
 // K = nperseg samples in steps of 64 (the lane's A fragment: 16 samples of its row, 8 at 8 g and 8 at
@@ -28,6 +31,7 @@
 // welch_i8_bands_kernel takes numpy's pairwise band sums and 10 log10 (np.sum(psd[mask])).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "msd_internal.h"
@@ -45,6 +49,15 @@ constexpr int WI_ND = 7;                  // coefficient digits
 constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
 #ifndef WI_WAVES_N
 #define WI_WAVES_N 12
+#endif
+// the digit combination in float64 (two exact Horner groups, one rounding) or in int64: 4.77-4.83
+// vs 5.46-5.49 ms per day, the int64 form's 64-bit shifts and sign extensions cost more VALU issue
+// than the float64 conversions they replace (profiles/r6_welch_i8_epi_ab.txt)
+#ifndef WI_EPI_INT
+#define WI_EPI_INT 0
+#endif
+#ifndef WI_SPECIAL
+#define WI_SPECIAL 1
 #endif
 #ifndef WI_PREFETCH
 #define WI_PREFETCH 1
@@ -64,7 +77,10 @@ struct WelchI8Args {
     int nct, cg, ngroups, reps;       // column tiles, tiles per group, groups, workgroups per group and XCD
     int nslots;
     double xscale;  // 2^-53 x sample_scale: a component's value from its integer digit sum
-    double scale;   // the density scale 1 / (fs sum w^2)
+    double pscale;  // the density scale 1 / (fs sum w^2), times xscale^2 when folded
+    int fold;       // xscale a power of two: |X|^2 = xscale^2 (v^2 + q^2) exactly, folded into pscale
+    int pairs;      // the accumulators combine in int32 pairs (digit_sum_pairs)
+    double rnseg;   // 1 / nseg
 };
 
 template <int CTRL>
@@ -85,6 +101,45 @@ __device__ __forceinline__ void digits(const uint32_t *w, v4i &hi, v4i &lo) {
     }
 }
 
+// sum_w 256^w a_w rounded once to float64: each group of four exact in int64 (|a| < 2^25: < 2^49),
+// t = hi + (lo >> 32) and r = lo mod 2^32 give sum = t 2^32 + r; t converts exactly (|t| < 2^50)
+#if WI_EPI_INT
+__device__ __forceinline__ int64_t group4(int a0, int a1, int a2, int a3) {
+    int64_t v = a3;
+    v = (v << 8) + a2;
+    v = (v << 8) + a1;
+    return (v << 8) + a0;
+}
+#endif
+__device__ __forceinline__ double digit_sum(int a0, int a1, int a2, int a3, int a4, int a5, int a6, int a7) {
+#if WI_EPI_INT
+    const int64_t lo = group4(a0, a1, a2, a3), hi = group4(a4, a5, a6, a7);
+    const int64_t t = hi + (lo >> 32);
+    const double tf = __builtin_fma((double)(int)(t >> 32), 0x1p32, (double)(uint32_t)t);
+    return __builtin_fma(tf, 0x1p32, (double)(uint32_t)lo);
+#else
+    // the same value in float64: each group's Horner sum is exact (< 2^49), the last fma rounds once
+    double lo = (double)a3, hi = (double)a7;
+    lo = __builtin_fma(lo, 256.0, (double)a2);
+    hi = __builtin_fma(hi, 256.0, (double)a6);
+    lo = __builtin_fma(lo, 256.0, (double)a1);
+    hi = __builtin_fma(hi, 256.0, (double)a5);
+    lo = __builtin_fma(lo, 256.0, (double)a0);
+    hi = __builtin_fma(hi, 256.0, (double)a4);
+    return __builtin_fma(hi, 0x1p32, lo);
+#endif
+}
+
+// the same value when the plan has checked |a_w| + 256 |a_(w+1)| < 2^31 for w = 0, 2, 4, 6 (every
+// column's digit sums bound each accumulator, welch_i8_build): the pairs exact in int32, four
+// conversions instead of eight, the same single rounding
+__device__ __forceinline__ double digit_sum_pairs(int a0, int a1, int a2, int a3, int a4, int a5, int a6, int a7) {
+    const int p0 = a0 + a1 * 256, p1 = a2 + a3 * 256, p2 = a4 + a5 * 256, p3 = a6 + a7 * 256;
+    const double lo = __builtin_fma((double)p1, 65536.0, (double)p0);  // exact: < 2^48
+    const double hi = __builtin_fma((double)p3, 65536.0, (double)p2);
+    return __builtin_fma(hi, 0x1p32, lo);
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -98,24 +153,61 @@ struct BlockRef {
     bool valid;
 };
 
-// block g (per lane) of the tile whose blocks are [g0, g0 + bpt): the files are walked with scalar
-// loads (g0 is wave-uniform; at most a few files), a lane's block picked from them
-__device__ __forceinline__ BlockRef block_of(const int16_t *x, const int64_t *off, const int64_t *len,
-                                            const WelchI8Args &A, int64_t g0, int64_t g) {
+// an M tile's first block, wave-uniform: block b0 (< max_blocks) of file f0 in the batch's
+// [nfiles][max_blocks] grid of blocks (block g = f max_blocks + b); the tile holds g .. g + bpt - 1
+struct TilePos {
+    int64_t f0, b0;
+};
+
+__device__ __forceinline__ TilePos tile_pos(const WelchI8Args &A, int64_t t) {
+    const int64_t g0 = uniform_i64(t * A.bpt);
+    const int64_t f0 = uniform_i64(g0 / A.max_blocks);
+    return TilePos{f0, g0 - f0 * A.max_blocks};
+}
+
+// the tile dblocks blocks later: a division only when the step leaves file f0 (once in max_blocks /
+// dblocks steps), not two 64-bit divisions per lane and tile
+__device__ __forceinline__ TilePos tile_advance(const WelchI8Args &A, TilePos P, int64_t dblocks) {
+    P.b0 += dblocks;
+    if (P.b0 >= A.max_blocks) {
+        const int64_t q = uniform_i64(P.b0 / A.max_blocks);
+        P.f0 += q;
+        P.b0 -= q * A.max_blocks;
+    }
+    return P;
+}
+
+// the last file a wave looked up (wave-uniform): its sample offset and block count, so that the
+// tiles inside one file (all but one in max_blocks / (nslot bpt)) load and divide nothing
+struct FileCache {
+    int64_t f = -1, o = 0, nb = 0;
+};
+
+// block bi (per lane, < bpt) of the tile at P: the files the tile touches are walked (at most a
+// few, uniform), the lane's block picked from them
+__device__ __forceinline__ BlockRef block_at(const int16_t *x, const int64_t *off, const int64_t *len,
+                                            const WelchI8Args &A, TilePos P, int bi, FileCache &C) {
     BlockRef r;
-    r.f = g / A.max_blocks;
-    r.b = g - r.f * A.max_blocks;
+    r.f = P.f0;
+    r.b = 0;
     r.valid = false;
     r.p = x;
-    const int64_t f0 = uniform_i64(g0 / A.max_blocks);
-    const int64_t fl = uniform_i64(std::min((g0 + A.bpt - 1) / A.max_blocks, A.nfiles - 1));
-    for (int64_t f = f0; f <= fl; ++f) {
-        int64_t o = off[f], n = len[f];
-        asm volatile("" : "+s"(o), "+s"(n));
-        const int64_t nb = n >= A.block_size ? (n - A.block_size) / A.block_size + 1 : 0;
-        if (r.f == f && r.b < nb) {
+    const int64_t last = P.b0 + A.bpt - 1;  // the tile's last block, counted from file f0's first
+    for (int64_t k = 0, kb = 0; kb <= last && P.f0 + k < A.nfiles; ++k, kb += A.max_blocks) {
+        const int64_t f = uniform_i64(P.f0 + k);
+        if (f != C.f) {
+            int64_t o = off[f], n = len[f];
+            asm volatile("" : "+s"(o), "+s"(n));
+            C.f = f;
+            C.o = o;
+            C.nb = uniform_i64(n >= A.block_size ? (n - A.block_size) / A.block_size + 1 : 0);
+        }
+        const int64_t b = P.b0 + bi - kb;
+        if (b >= 0 && b < A.max_blocks && b < C.nb) {
+            r.f = f;
+            r.b = b;
             r.valid = true;
-            r.p = x + o + r.b * (int64_t)A.block_size;
+            r.p = x + C.o + b * (int64_t)A.block_size;
         }
     }
     return r;
@@ -123,17 +215,24 @@ __device__ __forceinline__ BlockRef block_of(const int16_t *x, const int64_t *of
 
 // psd[(f ld + b) nslots + slot] = the Welch PSD of block (f, b) at the band bins (slot = band bins in
 // order), every block of files [0, nfiles) x [0, max_blocks) that exists.  bfrag: [nct][ND][KS][64]
-// B fragments; colinit: [nct][NW][16] the accumulator start values (128 sum_n d of the l' products);
-// dbl: [nct * 8] the onesided doubling (1 at DC / Nyquist, else 2; 0 past nslots).
-template <int KS>
+// B fragments; dbl: [nct * 8] the onesided doubling (1 at DC / Nyquist, else 2; 0 past nslots).
+// NSEG > 0: the instantiation for nseg = NSEG segments per block and a folded sample scale (the
+// live default's shape: the segment loop, the tile's row map and the mean become constants)
+template <int KS, int NSEG>
 __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const int16_t *__restrict__ x,
                                                                     const int64_t *__restrict__ off,
-                                                                    const int64_t *__restrict__ len, WelchI8Args A,
+                                                                    const int64_t *__restrict__ len, WelchI8Args Ain,
                                                                     const v4i *__restrict__ bfrag,
-                                                                    const int *__restrict__ colinit,
                                                                     const double *__restrict__ dbl,
                                                                     double *__restrict__ psd) {
     constexpr int NW = wi_waves(KS);
+    WelchI8Args A = Ain;
+    if constexpr (NSEG > 0) {
+        A.nseg = NSEG;
+        A.bpt = 16 / NSEG;
+        A.fold = 1;
+        A.rnseg = 1.0 / NSEG;
+    }
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int xcd = blockIdx.x & 7, iw = blockIdx.x >> 3;
     const int cgi = iw % A.ngroups, rep = iw / A.ngroups;
@@ -143,9 +242,7 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
     v4i *sB = reinterpret_cast<v4i *>(smem);                                        // [cg][ND][KS][64]
     double *sP = reinterpret_cast<double *>(sB + (size_t)A.cg * WI_ND * KS * 64);   // [WAVES][16][PP]
     double *sDbl = sP + NW * 16 * WI_PP;                                      // [cg][8]
-    int *sInit = reinterpret_cast<int *>(sDbl + A.cg * 8);                          // [cg][NW][16]
     for (int i = threadIdx.x; i < nct * WI_ND * KS * 64; i += 64 * NW) sB[i] = bfrag[(size_t)ct0 * WI_ND * KS * 64 + i];
-    for (int i = threadIdx.x; i < nct * WI_NW * 16; i += 64 * NW) sInit[i] = colinit[ct0 * WI_NW * 16 + i];
     for (int i = threadIdx.x; i < nct * 8; i += 64 * NW) sDbl[i] = dbl[ct0 * 8 + i];
     __syncthreads();
     const int l = threadIdx.x & 63;
@@ -162,12 +259,12 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
 
     // the lane's A row: row c = segment c % nseg of block c / nseg of the tile (rows past nrow and
     // missing blocks read the file start, their results unused)
-    auto row_ptr = [&](int64_t t) {
-        const int64_t g0 = uniform_i64(t * A.bpt);
-        const int bi = c < nrow ? c / A.nseg : 0;
-        const int s = c < nrow ? c - bi * A.nseg : 0;
-        const BlockRef r = block_of(x, off, len, A, g0, g0 + bi);
-        return r.valid ? r.p + (int64_t)s * A.step : x;
+    const int row_bi = c < nrow ? c / A.nseg : 0;
+    const int row_s = c < nrow ? c - row_bi * A.nseg : 0;
+    FileCache fc_row, fc_avg;  // the prefetch walks one tile ahead of the averaging
+    auto row_ptr = [&](TilePos P) {
+        const BlockRef r = block_at(x, off, len, A, P, row_bi, fc_row);
+        return r.valid ? r.p + (int64_t)row_s * A.step : x;
     };
     auto fetch = [&](const int16_t *p, int ks, int half) {
         v4u v;
@@ -177,14 +274,15 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
     v4u R[2 * KS];
     int64_t t = t_lo + slot0;
     if (t >= t_hi) return;  // wave-uniform; no workgroup barrier below
+    TilePos P = tile_pos(A, t);
     {
-        const int16_t *p = row_ptr(t);
+        const int16_t *p = row_ptr(P);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
     }
     for (; t < t_hi; t += nslot) {
         if (!WI_PREFETCH && t != t_lo + slot0) {  // (A/B: the tile's samples loaded here)
-            const int16_t *p = row_ptr(t);
+            const int16_t *p = row_ptr(P);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
         }
@@ -196,24 +294,23 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
             __builtin_memcpy(w, &R[2 * ks], 32);
             digits(w, ah[ks], al[ks]);
         }
-        const int64_t tn = t + nslot < t_hi ? t + nslot : t;  // the last tile re-reads itself (unused)
+        // the next tile (the last re-reads itself, unused)
+        TilePos Pn = t + nslot < t_hi ? tile_advance(A, P, nslot * A.bpt) : P;
+        Pn.f0 = uniform_i64(Pn.f0);
+        Pn.b0 = uniform_i64(Pn.b0);
         if (WI_PREFETCH) {
-            const int16_t *p = row_ptr(tn);
+            const int16_t *p = row_ptr(Pn);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
         }
         // the lanes that average a (block, bin): block l >> 3 of the tile, bin l & 7 of a column tile
-        const int64_t g0 = uniform_i64(t * A.bpt);
         const int ab = l >> 3;
-        const BlockRef blk = block_of(x, off, len, A, g0, g0 + (ab < A.bpt ? ab : 0));
+        const BlockRef blk = block_at(x, off, len, A, P, ab < A.bpt ? ab : 0, fc_avg);
         const bool avg_lane = ab < A.bpt && blk.valid;
         for (int j = 0; j < nct; ++j) {
             v4i acc[WI_NW];
 #pragma unroll
-            for (int w = 0; w < WI_NW; ++w) {
-                const int ci = sInit[(j * WI_NW + w) * 16 + c];
-                acc[w] = v4i{ci, ci, ci, ci};
-            }
+            for (int w = 0; w < WI_NW; ++w) acc[w] = v4i{0, 0, 0, 0};
             const v4i *bj = sB + (size_t)j * WI_ND * KS * 64 + l;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
@@ -228,33 +325,54 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                 for (int d = 0; d < WI_ND; ++d) acc[6 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], bk[d], acc[6 - d], 0, 0, 0);
             }
             // component c of rows 4 g + i: sum_w 256^w acc_w x 2^-53 x sample scale
+            double v[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                double v = (double)acc[7][i];
+                v[i] = A.pairs ? digit_sum_pairs(acc[0][i], acc[1][i], acc[2][i], acc[3][i], acc[4][i], acc[5][i],
+                                                 acc[6][i], acc[7][i])
+                               : digit_sum(acc[0][i], acc[1][i], acc[2][i], acc[3][i], acc[4][i], acc[5][i], acc[6][i],
+                                           acc[7][i]);
+                if (!A.fold) v[i] *= A.xscale;
+            }
+            // processor.py via scipy: conj(X) X = re re + im im, * scale, * 2.  The doubling (a power
+            // of two, exact) and, when folded, xscale^2 enter one product: the same rounding as
+            // scipy's three.  The lane pair (c, c ^ 1) holds a bin's two components; the even lane
+            // forms rows 4 g, 4 g + 1, the odd lane rows 4 g + 2, 4 g + 3, each sending the partner
+            // the two values it needs
+            const bool odd = c & 1;
+            const double sj = A.pscale * sDbl[j * 8 + (c >> 1)];
 #pragma unroll
-                for (int w = 6; w >= 0; --w) v = __builtin_fma(v, 256.0, (double)acc[w][i]);
-                v *= A.xscale;
-                const double q = dpp64<0xB1>(v);  // the partner component (c ^ 1)
-                if (!(c & 1)) {                   // processor.py via scipy: conj(X) X, * scale, * 2
-                    double p = v * v + q * q;
-                    p = p * A.scale;
-                    p = p * sDbl[j * 8 + (c >> 1)];
-                    pw[(4 * g + i) * WI_PP + (c >> 1)] = p;
-                }
+            for (int h = 0; h < 2; ++h) {
+                const double mine = odd ? v[2 + h] : v[h];
+                const double q = dpp64<0xB1>(odd ? v[h] : v[2 + h]);
+                const double p = mine * mine + q * q;  // re re + im im (addition commutes exactly)
+                pw[(4 * g + (odd ? 2 : 0) + h) * WI_PP + (c >> 1)] = p * sj;
             }
             wave_sync();
             if (avg_lane) {  // Pxy.mean(axis=-1): the block's segments in order, / nseg
                 const int bin = l & 7;
                 const int slot = (ct0 + j) * 8 + bin;
                 if (slot < A.nslots) {
+                    // the nseg values loaded together (one LDS round trip, not one per segment), then
+                    // summed in segment order
                     const double *q = pw + ab * A.nseg * WI_PP + bin;
-                    double s = q[0];
-                    for (int k = 1; k < A.nseg; ++k) s = s + q[k * WI_PP];
-                    psd[(blk.f * A.ld + blk.b) * (int64_t)A.nslots + slot] = s / (double)A.nseg;
+                    constexpr int MS = NSEG > 0 ? NSEG : 16;
+                    double qv[MS];
+#pragma unroll
+                    for (int k = 0; k < MS; ++k) qv[k] = q[min(k, A.nseg - 1) * WI_PP];
+                    double s = qv[0];
+#pragma unroll
+                    for (int k = 1; k < MS; ++k)
+                        if (k < A.nseg) s = s + qv[k];
+                    // s / nseg correctly rounded: r = RN(1 / nseg), one Newton correction (Markstein)
+                    const double m = s * A.rnseg;
+                    psd[(blk.f * A.ld + blk.b) * (int64_t)A.nslots + slot] =
+                        __builtin_fma(__builtin_fma(-m, (double)A.nseg, s), A.rnseg, m);
                 }
             }
             wave_sync();  // pw is rewritten by the next column tile
         }
+        P = Pn;
     }
 }
 
@@ -332,7 +450,28 @@ bool welch_i8_shape(const msd_welch_cfg &c, int nseg, int nslots, const double *
     return true;
 }
 
-// the plan's B fragments, column start values and doubling factors (one device buffer, p->d_i8)
+// T_n = round(v_n 2^53) with sum_n T_n = 0 exactly: floors, then the largest remainders rounded up
+// (sum_n v_n = 0 up to long double rounding, so the count to round up lies in [0, L)); |T_n - v_n 2^53| < 1
+bool zero_sum_round(const std::vector<long double> &v, std::vector<int64_t> &T) {
+    const int L = (int)v.size();
+    std::vector<long double> frac(L);
+    std::vector<int> idx(L);
+    int64_t S = 0;
+    for (int n = 0; n < L; ++n) {
+        const long double s = v[n] * 0x1p53L, f = floorl(s);
+        T[n] = (int64_t)f;
+        frac[n] = s - f;
+        S += T[n];
+        idx[n] = n;
+    }
+    const int64_t R = -S;
+    if (R < 0 || R > L) return false;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return frac[a] > frac[b]; });
+    for (int64_t r = 0; r < R; ++r) T[idx[r]] += 1;
+    return true;
+}
+
+// the plan's B fragments and doubling factors (one device buffer, p->d_i8)
 int welch_i8_build(msd_welch_plan *p, const double *window) {
     const msd_welch_cfg &c = p->cfg;
     const int L = c.nperseg, KS = L / 64, nfft = c.nfft;
@@ -350,10 +489,12 @@ int welch_i8_build(msd_welch_plan *p, const double *window) {
     const int ncomp = 2 * nslots;
     const int nct = (ncomp + 15) / 16;
     std::vector<int8_t> frag((size_t)nct * WI_ND * KS * 64 * 16, 0);
-    std::vector<int> init((size_t)nct * WI_NW * 16, 0);
     std::vector<double> dbl((size_t)nct * 8, 0.0);
     for (int s = 0; s < nslots; ++s) dbl[s] = dblv[s];
     std::vector<int8_t> dig((size_t)WI_ND * L);
+    std::vector<long double> cv(L);
+    std::vector<int64_t> T(L);
+    bool pairs = true;
     for (int cp = 0; cp < ncomp; ++cp) {
         const int64_t k = ks_bins[cp >> 1];
         const bool im = cp & 1;
@@ -369,18 +510,25 @@ int welch_i8_build(msd_welch_plan *p, const double *window) {
             Wim += ci[n];
         }
         const long double Wc = (im ? Wim : Wre) / (long double)L;
+        for (int n = 0; n < L; ++n) cv[n] = (im ? ci[n] : cr[n]) - Wc;
+        if (!zero_sum_round(cv, T)) return fail(MSD_ERR_INVALID, "welch_i8: coefficient rounding");
         for (int n = 0; n < L; ++n) {
-            const long double v = (im ? ci[n] : cr[n]) - Wc;
-            const int64_t T = llroundl(v * 0x1p53L);
             int8_t d[WI_ND];
-            if (!balanced_digits7(T, d)) return fail(MSD_ERR_INVALID, "welch_i8: coefficient beyond 7 digits");
+            if (!balanced_digits7(T[n], d)) return fail(MSD_ERR_INVALID, "welch_i8: coefficient beyond 7 digits");
             for (int b = 0; b < WI_ND; ++b) dig[(size_t)b * L + n] = d[b];
         }
+        // |acc_w| <= 128 (sum_n |d_(7-w)n| + sum_n |d_(6-w)n|) (h x digit 7 - w, l' x digit 6 - w;
+        // |h|, |l'| <= 128): the int32 pairs of digit_sum_pairs need |a_w| + 256 |a_(w+1)| < 2^31
+        int64_t sad[WI_ND] = {};
+        for (int b = 0; b < WI_ND; ++b)
+            for (int n = 0; n < L; ++n) sad[b] += std::abs((int)dig[(size_t)b * L + n]);
+        int64_t bound[WI_NW] = {};
+        for (int w = 0; w < WI_NW; ++w)
+            bound[w] = 128 * ((w >= 1 ? sad[7 - w] : 0) + (w <= 6 ? sad[6 - w] : 0));
+        for (int w = 0; w < WI_NW; w += 2)
+            if (bound[w] + 256 * bound[w + 1] >= (int64_t(1) << 31)) pairs = false;
         const int ct = cp / 16, cc = cp % 16;
         for (int b = 0; b < WI_ND; ++b) {
-            int64_t sd = 0;
-            for (int n = 0; n < L; ++n) sd += dig[(size_t)b * L + n];
-            init[((size_t)ct * WI_NW + (6 - b)) * 16 + cc] += (int)(128 * sd);  // l' x digit b: weight 6 - b
             for (int ks = 0; ks < KS; ++ks)
                 for (int grp = 0; grp < 4; ++grp)
                     for (int jj = 0; jj < 16; ++jj) {
@@ -390,14 +538,18 @@ int welch_i8_build(msd_welch_plan *p, const double *window) {
                     }
         }
     }
-    const size_t nb_frag = frag.size(), nb_init = sizeof(int) * init.size(), nb_dbl = sizeof(double) * dbl.size();
-    hipError_t e = hipMalloc(&p->d_i8, nb_frag + nb_init + nb_dbl);
+    const size_t nb_frag = frag.size(), nb_dbl = sizeof(double) * dbl.size();
+    hipError_t e = hipMalloc(&p->d_i8, nb_frag + nb_dbl);
     char *base = static_cast<char *>(p->d_i8);
     if (e == hipSuccess) e = hipMemcpy(base, frag.data(), nb_frag, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(base + nb_frag, init.data(), nb_init, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(base + nb_frag + nb_init, dbl.data(), nb_dbl, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(base + nb_frag, dbl.data(), nb_dbl, hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail(e, "welch plan: int8 tables");
     p->i8_nct = nct;
+#ifdef WI_FORCE_NOPAIRS
+    pairs = false;  // (A/B build)
+#endif
+    p->i8_pairs = pairs && !std::getenv("MSD_WELCH_I8_NOPAIRS");
+    p->i8_special = WI_SPECIAL && !std::getenv("MSD_WELCH_I8_GENERIC");  // (A/B and the identity test)
     return MSD_OK;
 }
 
@@ -423,7 +575,7 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
     A.nseg = p->nseg;
     A.bpt = 16 / p->nseg;
     A.nct = nct;
-    const size_t per_ct = (size_t)WI_ND * KS * 64 * 16 + sizeof(int) * WI_NW * 16 + sizeof(double) * 8;
+    const size_t per_ct = (size_t)WI_ND * KS * 64 * 16 + sizeof(double) * 8;
     const int nw = wi_waves(KS);
     const size_t scratch = sizeof(double) * nw * 16 * WI_PP;
     A.cg = (int)std::max<size_t>(1, std::min<size_t>((size_t)nct, (WI_LDS - scratch) / per_ct));
@@ -433,28 +585,41 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
     A.reps = std::max(1, wg_per_xcd / A.ngroups);
     A.nslots = p->nslots;
     A.xscale = std::ldexp(c.sample_scale, -53);
-    A.scale = c.scale;
+    int ex = 0;
+    const bool pow2 = std::fabs(std::frexp(A.xscale, &ex)) == 0.5;
+    const double folded = c.scale * A.xscale * A.xscale;
+    A.fold = pow2 && std::isnormal(folded) && std::isnormal(A.xscale * A.xscale);
+    A.pscale = A.fold ? folded : c.scale;
+    A.pairs = p->i8_pairs;
+    A.rnseg = 1.0 / (double)A.nseg;
     const size_t lds = (size_t)A.cg * per_ct + scratch;
     const v4i *frag = static_cast<const v4i *>(p->d_i8);
-    const char *base = static_cast<const char *>(p->d_i8) + (size_t)nct * WI_ND * KS * 64 * 16;
-    const int *init = reinterpret_cast<const int *>(base);
-    const double *dbl = reinterpret_cast<const double *>(base + sizeof(int) * (size_t)nct * WI_NW * 16);
+    const double *dbl = reinterpret_cast<const double *>(static_cast<const char *>(p->d_i8) +
+                                                         (size_t)nct * WI_ND * KS * 64 * 16);
     const unsigned grid = (unsigned)(8 * A.ngroups * A.reps);
     hipStream_t st = p->ctx->stream;
     KernelTimer timer(p->ctx, K_WELCH);
     switch (KS) {
-#define WI_CASE(K)                                                                                            \
-    case K:                                                                                                   \
-        if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(welch_i8_kernel<K>), 160 * 1024)) return rc; \
-        hipLaunchKernelGGL(welch_i8_kernel<K>, dim3(grid), dim3(64 * nw), lds, st, x, off, len, A, frag, init, \
-                           dbl, psd);                                                                         \
+#define WI_LAUNCH(K, S)                                                                                        \
+    do {                                                                                                       \
+        if (int rc = ensure_dyn_lds(reinterpret_cast<const void *>(welch_i8_kernel<K, S>), 160 * 1024)) return rc; \
+        hipLaunchKernelGGL((welch_i8_kernel<K, S>), dim3(grid), dim3(64 * nw), lds, st, x, off, len, A, frag, dbl, \
+                           psd);                                                                               \
+    } while (0)
+#define WI_CASE(K)          \
+    case K:                 \
+        WI_LAUNCH(K, 0);    \
         break;
         WI_CASE(1)
         WI_CASE(2)
         WI_CASE(3)
-        WI_CASE(4)
+        case 4:  // the live default (nperseg 256, 5 segments of a 0.2 s block at 4 kHz): its own instantiation
+            if (A.nseg == 5 && A.fold && p->i8_special) WI_LAUNCH(4, 5);
+            else WI_LAUNCH(4, 0);
+            break;
         WI_CASE(8)
 #undef WI_CASE
+#undef WI_LAUNCH
         default: return fail(MSD_ERR_UNSUPPORTED, "welch_i8: nperseg");
     }
     MSD_HIP(hipGetLastError());

@@ -197,8 +197,10 @@ def block_absmax(x: np.ndarray, block_size: int, sample_scale: float = 1.0) -> n
 
 
 # the int16 Welch path on the matrix cores (csrc/welch_i8.hip): |dX| <= I8_WELCH u sum_n |x_n| per
-# segment and bin -- the coefficients' 2^-54 quantisation (u / 2), the float64 Horner sum of 8
-# weights (2 u each, of partials below 2 sum|x|) and the mean's rounding for nperseg not a power of 2
+# segment and bin.  Round 6's kernel needs about 5 u of it: the coefficients' zero-sum quantisation
+# (|T - c' 2^53| < 1: u), the digit sum rounded once and the sample scale's product (u each of
+# |X| <= 2 sum|x|); 18 is the bound of round 6's first form (rounded quantisation, a float64 Horner
+# sum of 8 weights), kept
 I8_WELCH = 18.0
 
 

@@ -5,7 +5,8 @@ scipy (oracle/live_oracle.py, processor.py:206, :349-369) and against the float6
 replaces by default (MSD_OPT_WELCH_GOERTZEL).
 
 CPU: the path's arithmetic restated with Python integers (exact digit sums) stays within margin.py's
-int8 term of the exact detrended DFT, and the digits reconstruct every coefficient.
+int8 term of the exact detrended DFT, the zero-sum rounding makes the offset term vanish, and the
+digits reconstruct every coefficient.
 GPU: band dB within 1e-9 of scipy and of the Goertzel path over the shapes the path takes (nperseg
 64-512, 1-16 segments per block, several bands and widths), DC offsets, digital silence, full
 scale, files at odd offsets and a ragged batch; the psd output; the over-noise bound."""
@@ -25,6 +26,20 @@ def _coeffs(w, k, nfft):
     wl = w.astype(np.longdouble)
     cr, ci = wl * np.cos(a), -wl * np.sin(a)
     return cr - cr.sum() / L, ci - ci.sum() / L
+
+
+def _zero_sum_round(v):
+    """welch_i8_build's rounding: T_n = floor(v_n 2^53), the largest remainders rounded up so that
+    sum T_n = 0 exactly (the offset term 128 sum T_n of x = 256 h + l' + 128 vanishes)"""
+    s = v * np.longdouble(2.0 ** 53)
+    f = np.floor(s)
+    T = [int(a) for a in f.astype(np.int64)]
+    frac = s - f
+    R = -sum(T)
+    assert 0 <= R <= len(T)
+    for n in sorted(range(len(T)), key=lambda n: -frac[n])[:R]:  # stable: ties in index order
+        T[n] += 1
+    return T
 
 
 def _digits7(T):
@@ -54,13 +69,19 @@ def test_folded_detrend_quantisation_within_bound(case):
     absx = float(np.abs(x).sum())
     for k in (0, 1, 100, 1024, 1025, 2048):
         cr, ci = _coeffs(w, k, nfft)
-        Tr = [int(v) for v in np.rint(cr * np.longdouble(2.0 ** 53)).astype(np.int64)]
-        Ti = [int(v) for v in np.rint(ci * np.longdouble(2.0 ** 53)).astype(np.int64)]
+        Tr, Ti = _zero_sum_round(cr), _zero_sum_round(ci)
+        assert sum(Tr) == 0 and sum(Ti) == 0
+        two53 = np.longdouble(2.0 ** 53)
+        assert max(abs(np.longdouble(t) - c * two53) for t, c in zip(Tr + Ti, list(cr) + list(ci))) < 1
         for T in Tr[:8] + Ti[:8]:
             d = _digits7(T)
             assert sum(di * 256 ** (6 - b) for b, di in enumerate(d)) == T
         re = sum(int(a) * b for a, b in zip(x, Tr))
         im = sum(int(a) * b for a, b in zip(x, Ti))
+        # the kernel's accumulators hold the products with x - 128 (h and the offset-binary l'): the
+        # same sums, since the T sum to zero
+        assert re == sum((int(a) - 128) * b for a, b in zip(x, Tr))
+        assert im == sum((int(a) - 128) * b for a, b in zip(x, Ti))
         # the exact detrended DFT: sum (x - mean) w e^{-i theta n}
         xm = x.astype(np.longdouble) - x.astype(np.longdouble).sum() / L
         a = 2 * PI_LD * ((k * np.arange(L, dtype=np.int64)) % nfft).astype(np.longdouble) / np.longdouble(nfft)
@@ -68,8 +89,28 @@ def test_folded_detrend_quantisation_within_bound(case):
         got_r = np.longdouble(re) / np.longdouble(2.0 ** 53)
         got_i = np.longdouble(im) / np.longdouble(2.0 ** 53)
         err = float(np.hypot(got_r - er, got_i - ei))
-        assert err <= 0.75 * M.U * absx + 1e-15 * absx  # the quantisation: 2^-54 sum |x| per part
+        assert err <= 1.5 * M.U * absx  # the quantisation: |T - c' 2^53| < 1, 2^-53 sum |x| per part
         assert err <= M.I8_WELCH * M.U * L * float(np.abs(x).max())
+
+
+def _pair_bound(w, bins, nfft):
+    """max over the plan's components and w = 0, 2, 4, 6 of (|a_w| + 256 |a_(w+1)|) / 2^31, the
+    accumulators bounded by 128 (sum_n |d_(7-w)n| + sum_n |d_(6-w)n|) (welch_i8_build)"""
+    worst = 0.0
+    for k in bins:
+        for comp in _coeffs(w, k, nfft):
+            sad = np.abs(np.array([_digits7(t) for t in _zero_sum_round(comp)])).sum(axis=0)
+            b = [128 * ((sad[7 - i] if i >= 1 else 0) + (sad[6 - i] if i <= 6 else 0)) for i in range(8)]
+            worst = max(worst, max((b[i] + 256 * b[i + 1]) / 2 ** 31 for i in range(0, 8, 2)))
+    return worst
+
+
+def test_pair_bound_live_default():
+    """the live default plan (nperseg 256, 309 band bins) combines its accumulators in int32 pairs:
+    every pair's bound is below 2^31 (0.54 of it)"""
+    w = np.hanning(257)[:-1]
+    bins = list(range(870, 973)) + list(range(1175, 1278)) + list(range(460, 563))
+    assert _pair_bound(w, bins[::8], 4096) < 0.75
 
 
 # ----------------------------------------------------------------------------- GPU
@@ -216,3 +257,23 @@ def test_welch_i8_ragged_batch_and_psd(live):
         for b in (0, k - 1):
             _, P = welch(f[b * B:(b + 1) * B].astype(np.float64) / 32768.0, fs, nfft=int(c.nfft))
             np.testing.assert_allclose(psd[i, b], P[sl], rtol=1e-9, atol=0)
+
+
+@pytest.mark.gpu
+def test_welch_i8_pairs_bit_identical(live, monkeypatch):
+    """the int32-pair digit combination (the default plan's) and the eight-term one give the same
+    float64 values: both round the exact digit sum once; so do the live default's own instantiation
+    (5 segments, folded scale) and the generic one"""
+    from meteorgpu import synth
+    fs = 4000
+    x, _ = synth.synth_real(seed=77, fs=fs, duration_s=9.0, f0=1000, sigma=400, rate_per_min=30)
+    x = _stress(x, fs)
+    c, win = _plan_cfg(live, fs, 0.2, 4096, 1000, 100, 256)
+    got = _run(c, win, x, False)
+    monkeypatch.setenv("MSD_WELCH_I8_NOPAIRS", "1")
+    ref = _run(c, win, x, False)
+    assert np.array_equal(got, ref)
+    # and the generic instantiation (runtime segment count) against the live default's own
+    monkeypatch.setenv("MSD_WELCH_I8_GENERIC", "1")
+    assert np.array_equal(_run(c, win, x, False), ref)
+    np.testing.assert_allclose(got[np.isfinite(got)], _scipy_band_db(x, fs, c)[np.isfinite(got)], rtol=0, atol=1e-9)
