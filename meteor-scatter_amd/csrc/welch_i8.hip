@@ -56,6 +56,9 @@ constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
 #ifndef WI_EPI_INT
 #define WI_EPI_INT 0
 #endif
+#ifndef WI_SCHED
+#define WI_SCHED 1
+#endif
 #ifndef WI_SPECIAL
 #define WI_SPECIAL 1
 #endif
@@ -307,11 +310,39 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
         const int ab = l >> 3;
         const BlockRef blk = block_at(x, off, len, A, P, ab < A.bpt ? ab : 0, fc_avg);
         const bool avg_lane = ab < A.bpt && blk.valid;
+#if WI_SCHED
+        // the B fragments run one K step ahead: digit d of step ks + 1 (or of the next column tile's
+        // step 0) is read into bk[d] as soon as step ks's second MFMA on it has issued, 7 MFMAs
+        // before its first use, and the MFMA / LDS order is pinned (the scheduler otherwise waits on
+        // each fragment right after requesting it)
+        v4i bk[WI_ND];
+#pragma unroll
+        for (int d = 0; d < WI_ND; ++d) bk[d] = sB[(size_t)(d * KS) * 64 + l];
+#endif
         for (int j = 0; j < nct; ++j) {
             v4i acc[WI_NW];
 #pragma unroll
             for (int w = 0; w < WI_NW; ++w) acc[w] = v4i{0, 0, 0, 0};
             const v4i *bj = sB + (size_t)j * WI_ND * KS * 64 + l;
+#if WI_SCHED
+            const v4i *bn = j + 1 < nct ? bj + (size_t)WI_ND * KS * 64 : bj;  // the last tile re-reads its own (unused)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[ks], bk[d], acc[7 - d], 0, 0, 0);
+#pragma unroll
+                for (int d = 0; d < WI_ND; ++d) {
+                    acc[6 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], bk[d], acc[6 - d], 0, 0, 0);
+                    bk[d] = ks + 1 < KS ? bj[(d * KS + ks + 1) * 64] : bn[(d * KS) * 64];
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);  // the 7 h MFMAs
+#pragma unroll
+                for (int d = 0; d < WI_ND; ++d) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // an l' MFMA, then its fragment's refill
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+            }
+#else
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 v4i bk[WI_ND];
@@ -324,6 +355,7 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
 #pragma unroll
                 for (int d = 0; d < WI_ND; ++d) acc[6 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], bk[d], acc[6 - d], 0, 0, 0);
             }
+#endif
             // component c of rows 4 g + i: sum_w 256^w acc_w x 2^-53 x sample scale
             double v[4];
 #pragma unroll
