@@ -440,17 +440,24 @@ __global__ __launch_bounds__(256) void welch_i8_bands_kernel(const int64_t *__re
         double P = 0.0;
         if (w >= 8 && w <= 128) {
 #pragma clang fp contract(off)
-            const int lim = w - (w % 8);
-            double acc = 0.0;
-            if (ok) {
-                acc = row(s0 + r);
-                for (int k = 8 + r; k < lim; k += 8) acc += row(s0 + k);
-            }
+            // every load first (one memory round trip, not one per step), then the sums in order;
+            // the entries past the band are +0.0, an exact no-op on the non-negative powers
+            const int lim = w - (w % 8), nq = lim / 8;
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = ok && q < nq ? row(s0 + r + 8 * q) : 0.0;
+            double acc = v[0];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) acc += v[q];
             acc = acc + dpp64<0xB1>(acc);   // r0 + r1, r2 + r3, ...
             acc = acc + dpp64<0x4E>(acc);   // (r0 + r1) + (r2 + r3), (r4 + r5) + (r6 + r7)
             acc = acc + dpp64<0x141>(acc);  // half-row mirror: lane 0 meets lane 7
             if (r == 0 && ok) {
-                for (int k = lim; k < w; ++k) acc += row(s0 + k);
+                double t[7];
+#pragma unroll
+                for (int k = 0; k < 7; ++k) t[k] = lim + k < w ? row(s0 + lim + k) : 0.0;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) acc += t[k];
                 P = 0.0 + acc;
             }
         } else if (r == 0 && ok && w > 0) {
