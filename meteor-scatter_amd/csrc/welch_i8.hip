@@ -56,6 +56,16 @@ constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
 #ifndef WI_EPI_INT
 #define WI_EPI_INT 0
 #endif
+// the MFMA with the coefficients as its A operand and the samples as B (the fragments' register
+// layouts are the same): the output tile transposed, so a lane holds one segment's re and im of two
+// bins and forms their powers itself (no partner exchange, no selects)
+#ifndef WI_TRANS
+#define WI_TRANS 1
+#endif
+// (the 5-segment instantiation only: the generic one spills 14 registers in this form)
+#define WI_MFMA(samp, coef, acc)                                                                   \
+    (TR ? __builtin_amdgcn_mfma_i32_16x16x64_i8(coef, samp, acc, 0, 0, 0)                         \
+        : __builtin_amdgcn_mfma_i32_16x16x64_i8(samp, coef, acc, 0, 0, 0))
 #ifndef WI_SCHED
 #define WI_SCHED 1
 #endif
@@ -71,6 +81,8 @@ constexpr int WI_WAVES = WI_WAVES_N;
 // waves per workgroup for KS K steps: 8 K steps (nperseg 512) need 236 VGPRs, 2 waves per SIMD
 constexpr int wi_waves(int KS) { return KS <= 4 ? WI_WAVES : 8; }
 constexpr int WI_PP = 9;                  // per-wave power scratch: 16 rows x 8 bins, pitch 9 doubles
+constexpr int WI_PT = 17;                 // (transposed: 8 bins x 16 segment rows, pitch 17 doubles)
+static_assert(8 * WI_PT <= 16 * WI_PP, "power scratch");
 constexpr size_t WI_LDS = 160 * 1024;     // LDS of one workgroup: B fragments + per-wave power scratch
 constexpr int WI_MAXKS = 8;               // nperseg <= 512 (16 K steps would spill)
 
@@ -229,6 +241,7 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                                                                     const double *__restrict__ dbl,
                                                                     double *__restrict__ psd) {
     constexpr int NW = wi_waves(KS);
+    constexpr bool TR = WI_TRANS && NSEG > 0;  // the transposed tile (WI_MFMA)
     WelchI8Args A = Ain;
     if constexpr (NSEG > 0) {
         A.nseg = NSEG;
@@ -246,7 +259,9 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
     double *sP = reinterpret_cast<double *>(sB + (size_t)A.cg * WI_ND * KS * 64);   // [WAVES][16][PP]
     double *sDbl = sP + NW * 16 * WI_PP;                                      // [cg][8]
     for (int i = threadIdx.x; i < nct * WI_ND * KS * 64; i += 64 * NW) sB[i] = bfrag[(size_t)ct0 * WI_ND * KS * 64 + i];
-    for (int i = threadIdx.x; i < nct * 8; i += 64 * NW) sDbl[i] = dbl[ct0 * 8 + i];
+    // the power scale per slot: the density scale (times xscale^2 when folded) times the onesided
+    // doubling, a power of two (exact)
+    for (int i = threadIdx.x; i < nct * 8; i += 64 * NW) sDbl[i] = A.pscale * dbl[ct0 * 8 + i];
     __syncthreads();
     const int l = threadIdx.x & 63;
     const int c = l & 15, g = l >> 4;
@@ -329,10 +344,10 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[ks], bk[d], acc[7 - d], 0, 0, 0);
+                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = WI_MFMA(ah[ks], bk[d], acc[7 - d]);
 #pragma unroll
                 for (int d = 0; d < WI_ND; ++d) {
-                    acc[6 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], bk[d], acc[6 - d], 0, 0, 0);
+                    acc[6 - d] = WI_MFMA(al[ks], bk[d], acc[6 - d]);
                     bk[d] = ks + 1 < KS ? bj[(d * KS + ks + 1) * 64] : bn[(d * KS) * 64];
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);  // the 7 h MFMAs
@@ -351,9 +366,9 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                 // h x digit d: weight 256^(7 - d); l' x digit d: 256^(6 - d) (the l' chain second, so
                 // the two MFMAs into one accumulator are 7 apart)
 #pragma unroll
-                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[ks], bk[d], acc[7 - d], 0, 0, 0);
+                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = WI_MFMA(ah[ks], bk[d], acc[7 - d]);
 #pragma unroll
-                for (int d = 0; d < WI_ND; ++d) acc[6 - d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[ks], bk[d], acc[6 - d], 0, 0, 0);
+                for (int d = 0; d < WI_ND; ++d) acc[6 - d] = WI_MFMA(al[ks], bk[d], acc[6 - d]);
             }
 #endif
             // component c of rows 4 g + i: sum_w 256^w acc_w x 2^-53 x sample scale
@@ -367,18 +382,27 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                 if (!A.fold) v[i] *= A.xscale;
             }
             // processor.py via scipy: conj(X) X = re re + im im, * scale, * 2.  The doubling (a power
-            // of two, exact) and, when folded, xscale^2 enter one product: the same rounding as
-            // scipy's three.  The lane pair (c, c ^ 1) holds a bin's two components; the even lane
-            // forms rows 4 g, 4 g + 1, the odd lane rows 4 g + 2, 4 g + 3, each sending the partner
-            // the two values it needs
+            // of two, exact) and, when folded, xscale^2 enter one product with the scale: the same
+            // rounding as scipy's three
+            if constexpr (TR) {
+                // lane (c, g): segment row c of the tile, components 4 g .. 4 g + 3 = bins 2 g, 2 g + 1
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const double p = v[2 * h] * v[2 * h] + v[2 * h + 1] * v[2 * h + 1];
+                    pw[(2 * g + h) * WI_PT + c] = p * sDbl[j * 8 + 2 * g + h];
+                }
+            } else {
+            // the lane pair (c, c ^ 1) holds a bin's two components; the even lane forms rows 4 g,
+            // 4 g + 1, the odd lane rows 4 g + 2, 4 g + 3, each sending the partner the two values it needs
             const bool odd = c & 1;
-            const double sj = A.pscale * sDbl[j * 8 + (c >> 1)];
+            const double sj = sDbl[j * 8 + (c >> 1)];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const double mine = odd ? v[2 + h] : v[h];
                 const double q = dpp64<0xB1>(odd ? v[h] : v[2 + h]);
                 const double p = mine * mine + q * q;  // re re + im im (addition commutes exactly)
                 pw[(4 * g + (odd ? 2 : 0) + h) * WI_PP + (c >> 1)] = p * sj;
+            }
             }
             wave_sync();
             if (avg_lane) {  // Pxy.mean(axis=-1): the block's segments in order, / nseg
@@ -387,11 +411,12 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                 if (slot < A.nslots) {
                     // the nseg values loaded together (one LDS round trip, not one per segment), then
                     // summed in segment order
-                    const double *q = pw + ab * A.nseg * WI_PP + bin;
+                    const double *q = TR ? pw + bin * WI_PT + ab * A.nseg : pw + ab * A.nseg * WI_PP + bin;
+                    constexpr int QS = TR ? 1 : WI_PP;
                     constexpr int MS = NSEG > 0 ? NSEG : 16;
                     double qv[MS];
 #pragma unroll
-                    for (int k = 0; k < MS; ++k) qv[k] = q[min(k, A.nseg - 1) * WI_PP];
+                    for (int k = 0; k < MS; ++k) qv[k] = q[min(k, A.nseg - 1) * QS];
                     double s = qv[0];
 #pragma unroll
                     for (int k = 1; k < MS; ++k)
