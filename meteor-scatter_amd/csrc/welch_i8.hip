@@ -72,8 +72,11 @@ constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
 #ifndef WI_SPECIAL
 #define WI_SPECIAL 1
 #endif
+// the next M tile's samples prefetched into registers while this one computes (1), or loaded at
+// its start (0): 4.11-4.13 vs 4.14-4.17 ms per day, the other waves hide the load
+// (profiles/r6_welch_i8_epi_ab.txt)
 #ifndef WI_PREFETCH
-#define WI_PREFETCH 1
+#define WI_PREFETCH 0
 #endif
 // waves per workgroup: 12 = 3 per SIMD (154 VGPRs).  Against 8 (2 per SIMD): 5.52-5.55 vs
 // 5.97-6.04 ms per day (profiles/r6_welch_i8_ab.txt)
@@ -334,8 +337,8 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
 #pragma unroll
         for (int d = 0; d < WI_ND; ++d) bk[d] = sB[(size_t)(d * KS) * 64 + l];
 #endif
-        for (int j = 0; j < nct; ++j) {
-            v4i acc[WI_NW];
+        // one column tile's MFMAs into acc (the B fragments one K step ahead when WI_SCHED)
+        auto mm = [&](v4i(&acc)[WI_NW], int j) __attribute__((always_inline)) {
 #pragma unroll
             for (int w = 0; w < WI_NW; ++w) acc[w] = v4i{0, 0, 0, 0};
             const v4i *bj = sB + (size_t)j * WI_ND * KS * 64 + l;
@@ -371,6 +374,9 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                 for (int d = 0; d < WI_ND; ++d) acc[6 - d] = WI_MFMA(al[ks], bk[d], acc[6 - d]);
             }
 #endif
+        };
+        // tile j's powers from its accumulators into the wave's scratch pw
+        auto epa = [&](const v4i(&acc)[WI_NW], int j) __attribute__((always_inline)) {
             // component c of rows 4 g + i: sum_w 256^w acc_w x 2^-53 x sample scale
             double v[4];
 #pragma unroll
@@ -404,6 +410,9 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                 pw[(4 * g + (odd ? 2 : 0) + h) * WI_PP + (c >> 1)] = p * sj;
             }
             }
+        };
+        // tile j's block means from pw to psd
+        auto epb = [&](int j) __attribute__((always_inline)) {
             wave_sync();
             if (avg_lane) {  // Pxy.mean(axis=-1): the block's segments in order, / nseg
                 const int bin = l & 7;
@@ -428,6 +437,14 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                 }
             }
             wave_sync();  // pw is rewritten by the next column tile
+        };
+        {
+            for (int j = 0; j < nct; ++j) {
+                v4i acc[WI_NW];
+                mm(acc, j);
+                epa(acc, j);
+                epb(j);
+            }
         }
         P = Pn;
     }
