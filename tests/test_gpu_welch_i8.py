@@ -107,10 +107,12 @@ def _pair_bound(w, bins, nfft):
 
 def test_pair_bound_live_default():
     """the live default plan (nperseg 256, 309 band bins) combines its accumulators in int32 pairs:
-    every pair's bound is below 2^31 (0.54 of it)"""
+    every pair's bound is below 2^31 (0.54 of it); at nperseg 512 the bound exceeds 2^31, so the
+    GPU sweep's nperseg-512 case runs the eight-term digit sum"""
     w = np.hanning(257)[:-1]
     bins = list(range(870, 973)) + list(range(1175, 1278)) + list(range(460, 563))
     assert _pair_bound(w, bins[::8], 4096) < 0.75
+    assert _pair_bound(np.hanning(513)[:-1], list(range(1850, 2160, 31)), 4096) > 1.0
 
 
 # ----------------------------------------------------------------------------- GPU
