@@ -6,13 +6,14 @@
 //     c'_kn = w_n e^{-2 pi i k n / nfft} - W_k / nperseg,  W_k = sum_n w_n e^{-2 pi i k n / nfft},
 // because the mean m = sum_n x_n / nperseg is linear in the samples (the detrend folded into the
 // coefficients: no per-segment mean, no second pass).  As in block_i8.hip, each real coefficient is
-// T = round(c' 2^53) (|c'| <= 2) in seven balanced base-256 digits and each sample x = 256 h + l' + 128,
+// T ~ c' 2^53 (|c'| <= 2) in seven balanced base-256 digits and each sample x = 256 h + l' + 128,
 // so every inner sum is one v_mfma_i32_16x16x64_i8 accumulation, exact in int32.  The products of
 // equal weight share an accumulator (h with digit b and l' with digit b + 1: weight 256^(7 - b)),
 // eight per component.  The T of a component are rounded to sum exactly to zero (largest remainder),
 // so the offset's term 128 sum_n T_n vanishes and the accumulators start at zero; the eight are
-// combined exactly in int64 (two Horner groups of four, < 2^49 each) and rounded once to float64:
-// the result is round(sum_n (x_n - 128) T_n) = round(sum_n x_n T_n), zero for a silent block.  Error
+// combined exactly (as int32 pairs a_w + 256 a_(w+1) where the plan's bound allows, then two float64
+// Horner groups below 2^49) and rounded once to float64: the result is
+// round(sum_n (x_n - 128) T_n) = round(sum_n x_n T_n), zero for a silent block.  Error
 // against the exact DFT: the quantisation (|T - c' 2^53| < 1: 2^-53 sum|x|) and two roundings of
 // |X| <= 2 sum|x|, 5 u sum|x| -- inside margin.live_over_error's int8 term (18 u nperseg max|x|).
 //
@@ -78,8 +79,9 @@ constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
 #ifndef WI_PREFETCH
 #define WI_PREFETCH 0
 #endif
-// waves per workgroup: 12 = 3 per SIMD (154 VGPRs).  Against 8 (2 per SIMD): 5.52-5.55 vs
-// 5.97-6.04 ms per day (profiles/r6_welch_i8_ab.txt)
+// waves per workgroup: 12 = 3 per SIMD (<= 168 VGPRs).  Against 8 (2 per SIMD): 5.52-5.55 vs
+// 5.97-6.04 ms per day in the first form (profiles/r6_welch_i8_ab.txt), 4.14-4.17 vs 4.31-4.33 in
+// this one (profiles/r6_welch_i8_epi_ab.txt)
 constexpr int WI_WAVES = WI_WAVES_N;
 // waves per workgroup for KS K steps: 8 K steps (nperseg 512) need 236 VGPRs, 2 waves per SIMD
 constexpr int wi_waves(int KS) { return KS <= 4 ? WI_WAVES : 8; }
