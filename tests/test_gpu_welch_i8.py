@@ -279,3 +279,30 @@ def test_welch_i8_pairs_bit_identical(live, monkeypatch):
     monkeypatch.setenv("MSD_WELCH_I8_GENERIC", "1")
     assert np.array_equal(_run(c, win, x, False), ref)
     np.testing.assert_allclose(got[np.isfinite(got)], _scipy_band_db(x, fs, c)[np.isfinite(got)], rtol=0, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale", [1 / 30000.0, 3.0e-5, 1.0])
+def test_welch_i8_sample_scale_not_folded(live, scale):
+    """a sample scale that is not a power of two (1/30000, 3e-5) leaves the digit units' scale out of
+    the power's product (each component scaled first, as scipy scales the samples) and takes the
+    generic instantiation; 1.0 folds.  Band dB within 1e-9 of scipy on x * scale either way"""
+    from meteorgpu import synth
+    from scipy.signal import welch
+    fs = 4000
+    x, _ = synth.synth_real(seed=91, fs=fs, duration_s=6.0, f0=1000, sigma=400, rate_per_min=40)
+    x = _stress(x, fs)
+    c, win = _plan_cfg(live, fs, 0.2, 4096, 1000, 100, 256)
+    c.sample_scale = scale
+    got = _run(c, win, x, False)
+    B = int(c.block_size)
+    nb = (len(x) - B) // B + 1
+    ref = np.empty((3, nb))
+    for b in range(nb):
+        _, P = welch(x[b * B:(b + 1) * B].astype(np.float64) * scale, fs, nperseg=256, noverlap=128, nfft=4096)
+        for j in range(3):
+            e = np.sum(P[int(c.band_lo[j]): int(c.band_hi[j]) + 1])
+            ref[j, b] = 10 * np.log10(e) if e > 0 else -np.inf
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(got), fin)
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=0, atol=1e-9)
