@@ -67,18 +67,18 @@ constexpr int WI_NW = 8;                  // accumulator weights 256^0 .. 256^7
 #define WI_MFMA(samp, coef, acc)                                                                   \
     (TR ? __builtin_amdgcn_mfma_i32_16x16x64_i8(coef, samp, acc, 0, 0, 0)                         \
         : __builtin_amdgcn_mfma_i32_16x16x64_i8(samp, coef, acc, 0, 0, 0))
+#ifndef WI_SUPER
+#define WI_SUPER 1
+#endif
 #ifndef WI_SCHED
 #define WI_SCHED 1
 #endif
 #ifndef WI_SPECIAL
 #define WI_SPECIAL 1
 #endif
-// the next M tile's samples prefetched into registers while this one computes (1), or loaded at
-// its start (0): 4.11-4.13 vs 4.14-4.17 ms per day, the other waves hide the load
+// an M tile's samples are loaded at its start: prefetching the next tile's into 32 registers
+// during this one measured 4.14-4.17 against 4.11-4.13 ms per day, the other waves hide the load
 // (profiles/r6_welch_i8_epi_ab.txt)
-#ifndef WI_PREFETCH
-#define WI_PREFETCH 0
-#endif
 // waves per workgroup: 12 = 3 per SIMD (<= 168 VGPRs).  Against 8 (2 per SIMD): 5.52-5.55 vs
 // 5.97-6.04 ms per day in the first form (profiles/r6_welch_i8_ab.txt), 4.14-4.17 vs 4.31-4.33 in
 // this one (profiles/r6_welch_i8_epi_ab.txt)
@@ -203,16 +203,16 @@ struct FileCache {
     int64_t f = -1, o = 0, nb = 0;
 };
 
-// block bi (per lane, < bpt) of the tile at P: the files the tile touches are walked (at most a
-// few, uniform), the lane's block picked from them
+// block bi (per lane, < span) of the span of blocks starting at P: the files the span touches are
+// walked (at most a few, uniform), the lane's block picked from them
 __device__ __forceinline__ BlockRef block_at(const int16_t *x, const int64_t *off, const int64_t *len,
-                                            const WelchI8Args &A, TilePos P, int bi, FileCache &C) {
+                                            const WelchI8Args &A, TilePos P, int bi, FileCache &C, int span) {
     BlockRef r;
     r.f = P.f0;
     r.b = 0;
     r.valid = false;
     r.p = x;
-    const int64_t last = P.b0 + A.bpt - 1;  // the tile's last block, counted from file f0's first
+    const int64_t last = P.b0 + span - 1;  // the span's last block, counted from file f0's first
     for (int64_t k = 0, kb = 0; kb <= last && P.f0 + k < A.nfiles; ++k, kb += A.max_blocks) {
         const int64_t f = uniform_i64(P.f0 + k);
         if (f != C.f) {
@@ -247,6 +247,7 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
                                                                     double *__restrict__ psd) {
     constexpr int NW = wi_waves(KS);
     constexpr bool TR = WI_TRANS && NSEG > 0;  // the transposed tile (WI_MFMA)
+    constexpr bool SUPER = WI_SUPER && TR && NSEG == 5;  // 16-block units (below)
     WelchI8Args A = Ain;
     if constexpr (NSEG > 0) {
         A.nseg = NSEG;
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
     const int row_s = c < nrow ? c - row_bi * A.nseg : 0;
     FileCache fc_row, fc_avg;  // the prefetch walks one tile ahead of the averaging
     auto row_ptr = [&](TilePos P) {
-        const BlockRef r = block_at(x, off, len, A, P, row_bi, fc_row);
+        const BlockRef r = block_at(x, off, len, A, P, row_bi, fc_row, A.bpt);
         return r.valid ? r.p + (int64_t)row_s * A.step : x;
     };
     auto fetch = [&](const int16_t *p, int ks, int half) {
@@ -295,124 +296,172 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
         return v;
     };
     v4u R[2 * KS];
-    int64_t t = t_lo + slot0;
-    if (t >= t_hi) return;  // wave-uniform; no workgroup barrier below
-    TilePos P = tile_pos(A, t);
-    {
-        const int16_t *p = row_ptr(P);
+    v4i ah[KS], al[KS];  // the current M tile's sample digits
+#if WI_SCHED
+    // the B fragments run one K step ahead: digit d of step ks + 1 (or of the next column tile's
+    // step 0) is read into bk[d] as soon as step ks's second MFMA on it has issued, 7 MFMAs
+    // before its first use, and the MFMA / LDS order is pinned (the scheduler otherwise waits on
+    // each fragment right after requesting it)
+    v4i bk[WI_ND];
+#endif
+    auto load_digits = [&](const int16_t *p) __attribute__((always_inline)) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
-    }
-    for (; t < t_hi; t += nslot) {
-        if (!WI_PREFETCH && t != t_lo + slot0) {  // (A/B: the tile's samples loaded here)
-            const int16_t *p = row_ptr(P);
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
-        }
-        // the tile's sample digits, then the next tile's samples into R while this one computes
-        v4i ah[KS], al[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             uint32_t w[8];
             __builtin_memcpy(w, &R[2 * ks], 32);
             digits(w, ah[ks], al[ks]);
         }
+#if WI_SCHED
+#pragma unroll
+        for (int d = 0; d < WI_ND; ++d) bk[d] = sB[(size_t)(d * KS) * 64 + l];
+#endif
+    };
+    // one column tile's MFMAs into acc (the B fragments one K step ahead when WI_SCHED)
+    auto mm = [&](v4i(&acc)[WI_NW], int j) __attribute__((always_inline)) {
+#pragma unroll
+        for (int w = 0; w < WI_NW; ++w) acc[w] = v4i{0, 0, 0, 0};
+        const v4i *bj = sB + (size_t)j * WI_ND * KS * 64 + l;
+#if WI_SCHED
+        const v4i *bn = j + 1 < nct ? bj + (size_t)WI_ND * KS * 64 : bj;  // the last tile re-reads its own (unused)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+            for (int d = 0; d < WI_ND; ++d) acc[7 - d] = WI_MFMA(ah[ks], bk[d], acc[7 - d]);
+#pragma unroll
+            for (int d = 0; d < WI_ND; ++d) {
+                acc[6 - d] = WI_MFMA(al[ks], bk[d], acc[6 - d]);
+                bk[d] = ks + 1 < KS ? bj[(d * KS + ks + 1) * 64] : bn[(d * KS) * 64];
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);  // the 7 h MFMAs
+#pragma unroll
+            for (int d = 0; d < WI_ND; ++d) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // an l' MFMA, then its fragment's refill
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+        }
+#else
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            v4i bk[WI_ND];
+#pragma unroll
+            for (int d = 0; d < WI_ND; ++d) bk[d] = bj[(d * KS + ks) * 64];
+            // h x digit d: weight 256^(7 - d); l' x digit d: 256^(6 - d) (the l' chain second, so
+            // the two MFMAs into one accumulator are 7 apart)
+#pragma unroll
+            for (int d = 0; d < WI_ND; ++d) acc[7 - d] = WI_MFMA(ah[ks], bk[d], acc[7 - d]);
+#pragma unroll
+            for (int d = 0; d < WI_ND; ++d) acc[6 - d] = WI_MFMA(al[ks], bk[d], acc[6 - d]);
+        }
+#endif
+    };
+    // tile j's powers from its accumulators into the wave's scratch pw
+    auto epa = [&](const v4i(&acc)[WI_NW], int j) __attribute__((always_inline)) {
+        // component c of rows 4 g + i: sum_w 256^w acc_w x 2^-53 x sample scale
+        double v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[i] = A.pairs ? digit_sum_pairs(acc[0][i], acc[1][i], acc[2][i], acc[3][i], acc[4][i], acc[5][i],
+                                             acc[6][i], acc[7][i])
+                           : digit_sum(acc[0][i], acc[1][i], acc[2][i], acc[3][i], acc[4][i], acc[5][i], acc[6][i],
+                                       acc[7][i]);
+            if (!A.fold) v[i] *= A.xscale;
+        }
+        // processor.py via scipy: conj(X) X = re re + im im, * scale, * 2.  The doubling (a power
+        // of two, exact) and, when folded, xscale^2 enter one product with the scale: the same
+        // rounding as scipy's three
+        if constexpr (TR) {
+            // lane (c, g): segment row c of the tile, components 4 g .. 4 g + 3 = bins 2 g, 2 g + 1
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const double p = v[2 * h] * v[2 * h] + v[2 * h + 1] * v[2 * h + 1];
+                pw[(2 * g + h) * WI_PT + c] = p * sDbl[j * 8 + 2 * g + h];
+            }
+        } else {
+        // the lane pair (c, c ^ 1) holds a bin's two components; the even lane forms rows 4 g,
+        // 4 g + 1, the odd lane rows 4 g + 2, 4 g + 3, each sending the partner the two values it needs
+        const bool odd = c & 1;
+        const double sj = sDbl[j * 8 + (c >> 1)];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const double mine = odd ? v[2 + h] : v[h];
+            const double q = dpp64<0xB1>(odd ? v[h] : v[2 + h]);
+            const double p = mine * mine + q * q;  // re re + im im (addition commutes exactly)
+            pw[(4 * g + (odd ? 2 : 0) + h) * WI_PP + (c >> 1)] = p * sj;
+        }
+        }
+    };
+
+    if constexpr (SUPER) {
+        // The live default's shape (5 segments per block) in units of 16 blocks = 80 segment rows =
+        // 5 full M tiles (no idle row: 16 of 16 against 15 of 16).  A block's segments may straddle
+        // two tiles of its unit; its running sum is carried in LDS from one tile to the next, in
+        // segment order (the same association as summing the 5 rows at once).  Tile m holds the
+        // rows of blocks 16 m / 5 .. 16 m / 5 + 3 of the unit.
+        double *carry = sDbl + A.cg * 8 + (size_t)wv * A.cg * 8;  // [cg][8] per wave
+        if (l < 8) pw[l * WI_PT + 16] = 0.0;                      // the pad column: an exact no-op term
+        const int64_t nun = (nblocks + 15) / 16;
+        const int64_t u_lo = nun * xcd / 8, u_hi = nun * (xcd + 1) / 8;
+        const int ab = l >> 3, bin = l & 7;
+        for (int64_t u = u_lo + slot0; u < u_hi; u += nslot) {
+            const int64_t g0 = uniform_i64(u * 16);
+            const int64_t uf = uniform_i64(g0 / A.max_blocks);
+            const TilePos PU{uf, g0 - uf * A.max_blocks};
+            for (int m = 0; m < 5; ++m) {
+                {
+                    const int G = 16 * m + c, bi = G / 5;
+                    const BlockRef rr = block_at(x, off, len, A, PU, bi, fc_row, 16);
+                    load_digits(rr.valid ? rr.p + (int64_t)(G - 5 * bi) * A.step : x);
+                }
+                const int bf = (16 * m) / 5;                      // the tile's first block
+                const int bi = bf + (ab < 4 ? ab : 0);            // this lane's block (lanes ab < 4)
+                const BlockRef blk = block_at(x, off, len, A, PU, bi, fc_avg, 16);
+                const int lo = max(5 * bi - 16 * m, 0), hi = min(5 * bi + 5 - 16 * m, 16);
+                const bool cin = 5 * bi < 16 * m, cout = 5 * bi + 5 > 16 * m + 16;
+                for (int j = 0; j < nct; ++j) {
+                    v4i acc[WI_NW];
+                    mm(acc, j);
+                    epa(acc, j);
+                    wave_sync();
+                    const int slot = (ct0 + j) * 8 + bin;
+                    if (ab < 4 && slot < A.nslots) {
+                        // the block's rows of this tile in order (the pad column past them), after
+                        // the running sum carried from the previous tile
+                        const double *q = pw + bin * WI_PT;
+                        double qv[5];
+#pragma unroll
+                        for (int k = 0; k < 5; ++k) qv[k] = q[lo + k < hi ? lo + k : 16];
+                        double s = cin ? carry[j * 8 + bin] : 0.0;
+#pragma unroll
+                        for (int k = 0; k < 5; ++k) s = s + qv[k];
+                        if (cout) {
+                            carry[j * 8 + bin] = s;
+                        } else if (blk.valid) {
+                            const double mn = s * A.rnseg;  // s / nseg correctly rounded (Markstein)
+                            psd[(blk.f * A.ld + blk.b) * (int64_t)A.nslots + slot] =
+                                __builtin_fma(__builtin_fma(-mn, (double)A.nseg, s), A.rnseg, mn);
+                        }
+                    }
+                    wave_sync();  // pw is rewritten by the next column tile
+                }
+            }
+        }
+        return;
+    }
+    int64_t t = t_lo + slot0;
+    if (t >= t_hi) return;  // wave-uniform; no workgroup barrier below
+    TilePos P = tile_pos(A, t);
+    for (; t < t_hi; t += nslot) {
+        load_digits(row_ptr(P));
         // the next tile (the last re-reads itself, unused)
         TilePos Pn = t + nslot < t_hi ? tile_advance(A, P, nslot * A.bpt) : P;
         Pn.f0 = uniform_i64(Pn.f0);
         Pn.b0 = uniform_i64(Pn.b0);
-        if (WI_PREFETCH) {
-            const int16_t *p = row_ptr(Pn);
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) R[2 * ks] = fetch(p, ks, 0), R[2 * ks + 1] = fetch(p, ks, 1);
-        }
         // the lanes that average a (block, bin): block l >> 3 of the tile, bin l & 7 of a column tile
         const int ab = l >> 3;
-        const BlockRef blk = block_at(x, off, len, A, P, ab < A.bpt ? ab : 0, fc_avg);
+        const BlockRef blk = block_at(x, off, len, A, P, ab < A.bpt ? ab : 0, fc_avg, A.bpt);
         const bool avg_lane = ab < A.bpt && blk.valid;
-#if WI_SCHED
-        // the B fragments run one K step ahead: digit d of step ks + 1 (or of the next column tile's
-        // step 0) is read into bk[d] as soon as step ks's second MFMA on it has issued, 7 MFMAs
-        // before its first use, and the MFMA / LDS order is pinned (the scheduler otherwise waits on
-        // each fragment right after requesting it)
-        v4i bk[WI_ND];
-#pragma unroll
-        for (int d = 0; d < WI_ND; ++d) bk[d] = sB[(size_t)(d * KS) * 64 + l];
-#endif
-        // one column tile's MFMAs into acc (the B fragments one K step ahead when WI_SCHED)
-        auto mm = [&](v4i(&acc)[WI_NW], int j) __attribute__((always_inline)) {
-#pragma unroll
-            for (int w = 0; w < WI_NW; ++w) acc[w] = v4i{0, 0, 0, 0};
-            const v4i *bj = sB + (size_t)j * WI_ND * KS * 64 + l;
-#if WI_SCHED
-            const v4i *bn = j + 1 < nct ? bj + (size_t)WI_ND * KS * 64 : bj;  // the last tile re-reads its own (unused)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = WI_MFMA(ah[ks], bk[d], acc[7 - d]);
-#pragma unroll
-                for (int d = 0; d < WI_ND; ++d) {
-                    acc[6 - d] = WI_MFMA(al[ks], bk[d], acc[6 - d]);
-                    bk[d] = ks + 1 < KS ? bj[(d * KS + ks + 1) * 64] : bn[(d * KS) * 64];
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);  // the 7 h MFMAs
-#pragma unroll
-                for (int d = 0; d < WI_ND; ++d) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // an l' MFMA, then its fragment's refill
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
-            }
-#else
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                v4i bk[WI_ND];
-#pragma unroll
-                for (int d = 0; d < WI_ND; ++d) bk[d] = bj[(d * KS + ks) * 64];
-                // h x digit d: weight 256^(7 - d); l' x digit d: 256^(6 - d) (the l' chain second, so
-                // the two MFMAs into one accumulator are 7 apart)
-#pragma unroll
-                for (int d = 0; d < WI_ND; ++d) acc[7 - d] = WI_MFMA(ah[ks], bk[d], acc[7 - d]);
-#pragma unroll
-                for (int d = 0; d < WI_ND; ++d) acc[6 - d] = WI_MFMA(al[ks], bk[d], acc[6 - d]);
-            }
-#endif
-        };
-        // tile j's powers from its accumulators into the wave's scratch pw
-        auto epa = [&](const v4i(&acc)[WI_NW], int j) __attribute__((always_inline)) {
-            // component c of rows 4 g + i: sum_w 256^w acc_w x 2^-53 x sample scale
-            double v[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                v[i] = A.pairs ? digit_sum_pairs(acc[0][i], acc[1][i], acc[2][i], acc[3][i], acc[4][i], acc[5][i],
-                                                 acc[6][i], acc[7][i])
-                               : digit_sum(acc[0][i], acc[1][i], acc[2][i], acc[3][i], acc[4][i], acc[5][i], acc[6][i],
-                                           acc[7][i]);
-                if (!A.fold) v[i] *= A.xscale;
-            }
-            // processor.py via scipy: conj(X) X = re re + im im, * scale, * 2.  The doubling (a power
-            // of two, exact) and, when folded, xscale^2 enter one product with the scale: the same
-            // rounding as scipy's three
-            if constexpr (TR) {
-                // lane (c, g): segment row c of the tile, components 4 g .. 4 g + 3 = bins 2 g, 2 g + 1
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const double p = v[2 * h] * v[2 * h] + v[2 * h + 1] * v[2 * h + 1];
-                    pw[(2 * g + h) * WI_PT + c] = p * sDbl[j * 8 + 2 * g + h];
-                }
-            } else {
-            // the lane pair (c, c ^ 1) holds a bin's two components; the even lane forms rows 4 g,
-            // 4 g + 1, the odd lane rows 4 g + 2, 4 g + 3, each sending the partner the two values it needs
-            const bool odd = c & 1;
-            const double sj = sDbl[j * 8 + (c >> 1)];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const double mine = odd ? v[2 + h] : v[h];
-                const double q = dpp64<0xB1>(odd ? v[h] : v[2 + h]);
-                const double p = mine * mine + q * q;  // re re + im im (addition commutes exactly)
-                pw[(4 * g + (odd ? 2 : 0) + h) * WI_PP + (c >> 1)] = p * sj;
-            }
-            }
-        };
         // tile j's block means from pw to psd
         auto epb = [&](int j) __attribute__((always_inline)) {
             wave_sync();
@@ -440,13 +489,11 @@ __global__ __launch_bounds__(64 * wi_waves(KS), 1) void welch_i8_kernel(const in
             }
             wave_sync();  // pw is rewritten by the next column tile
         };
-        {
-            for (int j = 0; j < nct; ++j) {
-                v4i acc[WI_NW];
-                mm(acc, j);
-                epa(acc, j);
-                epb(j);
-            }
+        for (int j = 0; j < nct; ++j) {
+            v4i acc[WI_NW];
+            mm(acc, j);
+            epa(acc, j);
+            epb(j);
         }
         P = Pn;
     }
@@ -658,8 +705,10 @@ int launch_welch_i8(msd_welch_plan *p, const int16_t *x, const int64_t *off, con
     A.nseg = p->nseg;
     A.bpt = 16 / p->nseg;
     A.nct = nct;
-    const size_t per_ct = (size_t)WI_ND * KS * 64 * 16 + sizeof(double) * 8;
     const int nw = wi_waves(KS);
+    // per column tile: its B fragments, its 8 power scales, and every wave's 8 carried block sums
+    // (the 16-block units of the 5-segment instantiation)
+    const size_t per_ct = (size_t)WI_ND * KS * 64 * 16 + sizeof(double) * 8 + sizeof(double) * 8 * nw;
     const size_t scratch = sizeof(double) * nw * 16 * WI_PP;
     A.cg = (int)std::max<size_t>(1, std::min<size_t>((size_t)nct, (WI_LDS - scratch) / per_ct));
     A.ngroups = (nct + A.cg - 1) / A.cg;
