@@ -17,7 +17,8 @@
 // against the exact DFT: the quantisation (|T - c' 2^53| < 1: 2^-53 sum|x|) and two roundings of
 // |X| <= 2 sum|x|, 5 u sum|x| -- inside margin.live_over_error's int8 term (18 u nperseg max|x|).
 //
-// GEMM: rows = segments (a 16-row tile holds bpt = 16 / nseg whole blocks, nseg rows each),
+// GEMM: rows = segments (a 16-row tile holds bpt = 16 / nseg whole blocks, nseg rows each; the
+// 5-segment instantiation walks units of 16 blocks = 5 full tiles, see SUPER),
 // K = nperseg samples in steps of 64 (the lane's A fragment: 16 samples of its row, 8 at 8 g and 8 at
 // 32 + 8 g of the step, g = lane >> 4, as block_i8.hip), columns = the components of the band bins
 // (bin j's real part 2 j, imaginary part 2 j + 1), 16 per column tile.  The B fragments of all bins
