@@ -319,7 +319,10 @@ __global__ __launch_bounds__(WL_THREADS) void live_history_kernel(const int64_t 
 // (ballot) is where the state changes, so a 64-block span without events is one step.
 // (Rounds 1-5 ran one 16-wave workgroup per file with the rounds inside it: 24 files used 24 CUs,
 // 0.65-0.70 ms per day.)
-constexpr int LV_SEGLEN = 128;  // blocks per segment
+#ifndef LV_SEGLEN_N
+#define LV_SEGLEN_N 128
+#endif
+constexpr int LV_SEGLEN = LV_SEGLEN_N;  // blocks per segment
 constexpr int LV_ROUNDS = 4;    // rounds launched before the convergence flag is read
 
 __device__ __forceinline__ bool live_same_entry(const LiveScan &x, const LiveScan &y, double t1_first) {
