@@ -16,7 +16,7 @@
 // live_over_kernel, live_history_kernel: the over-noise values, then the history thresholds
 // mean + k*std of the previous W of them -- state-free, one thread per block of every file
 // (the whole GPU, not one workgroup per file);
-// live_seg_{init,scan,link,emit}_kernel: the state machine in 128-block time segments, one wave
+// live_seg_{init,scan,link,emit}_kernel: the state machine in 256-block time segments, one wave
 // each over the whole GPU (ballots), rounds of scan + link to a fixed point over their entry states,
 // then one emitting pass.
 #include <cmath>
@@ -319,10 +319,12 @@ __global__ __launch_bounds__(WL_THREADS) void live_history_kernel(const int64_t 
 // (ballot) is where the state changes, so a 64-block span without events is one step.
 // (Rounds 1-5 ran one 16-wave workgroup per file with the rounds inside it: 24 files used 24 CUs,
 // 0.65-0.70 ms per day.)
+// blocks per segment: 256 against 64 / 128 / 512 / 1024 measured 0.26-0.31 vs 0.55 / 0.34-0.35 /
+// 0.31-0.32 / 0.42-0.47 ms per day for the state machine (profiles/r6_live_seglen_ab.txt)
 #ifndef LV_SEGLEN_N
-#define LV_SEGLEN_N 128
+#define LV_SEGLEN_N 256
 #endif
-constexpr int LV_SEGLEN = LV_SEGLEN_N;  // blocks per segment
+constexpr int LV_SEGLEN = LV_SEGLEN_N;
 constexpr int LV_ROUNDS = 4;    // rounds launched before the convergence flag is read
 
 __device__ __forceinline__ bool live_same_entry(const LiveScan &x, const LiveScan &y, double t1_first) {
