@@ -299,9 +299,10 @@ def run_live(a, ctx, job, rank, world, rows):
     avg_s = w_ms / max(w_n, 1) / 1e3
     # int16 input takes the exact integer GEMM (csrc/welch_i8.hip): the dominant work is int8 MFMA,
     # per segment nperseg samples x 2 nslots components x (7 coefficient x 2 sample digits), 2 ops
-    # per multiply-add, in 16-row tiles of whole blocks (16 // nseg blocks per tile)
+    # per multiply-add, in 16-row tiles: the live default's 5-segment instantiation walks units of
+    # 16 blocks = 5 full tiles, the generic one tiles of 16 // nseg whole blocks
     bpt = 16 // nseg
-    tiles = -(-blocks // bpt)
+    tiles = 5 * -(-blocks // 16) if (nseg == 5 and wc.nperseg == 256) else -(-blocks // bpt)
     ncol = -(-2 * nslots // 16) * 16
     i8_ops = tiles * 16 * wc.nperseg * ncol * 14 * 2.0
     useful = blocks * nseg * wc.nperseg * 2 * nslots * 14 * 2.0
