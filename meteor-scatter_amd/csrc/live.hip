@@ -325,7 +325,10 @@ __global__ __launch_bounds__(WL_THREADS) void live_history_kernel(const int64_t 
 #define LV_SEGLEN_N 256
 #endif
 constexpr int LV_SEGLEN = LV_SEGLEN_N;
-constexpr int LV_ROUNDS = 4;    // rounds launched before the convergence flag is read
+#ifndef LV_ROUNDS_N
+#define LV_ROUNDS_N 4
+#endif
+constexpr int LV_ROUNDS = LV_ROUNDS_N;  // rounds launched before the convergence flag is read
 
 __device__ __forceinline__ bool live_same_entry(const LiveScan &x, const LiveScan &y, double t1_first) {
     if (x.state != y.state) return false;
