@@ -306,6 +306,7 @@ def run_live(a, ctx, job, rank, world, rows):
     ncol = -(-2 * nslots // 16) * 16
     i8_ops = tiles * 16 * wc.nperseg * ncol * 14 * 2.0
     useful = blocks * nseg * wc.nperseg * 2 * nslots * 14 * 2.0
+    live_traffic = load_pmc_traffic("welch", files=F, nperseg=int(wc.nperseg))
     out = {
         "metric": "Msamples/s processed (4 kHz live detector: Welch band powers + state machine)",
         "value": round(world * F * n * a.steps / elapsed / 1e6, 1),
@@ -319,7 +320,10 @@ def run_live(a, ctx, job, rank, world, rows):
                    "files_per_gpu": F, "samples_per_file": n, "blocks_per_file": lb.nb, "band_bins": nslots},
         "meteors_per_step": int(counts.sum()),
         "roofline": {"bound": "mfma", "achieved": round(i8_ops / avg_s / 1e12, 1), "peak": I8_PEAK_TOPS,
-                     "unit": "TOPS (int8)", "frac": round(i8_ops / avg_s / 1e12 / I8_PEAK_TOPS, 4), "traffic": None,
+                     "unit": "TOPS (int8)", "frac": round(i8_ops / avg_s / 1e12 / I8_PEAK_TOPS, 4),
+                     # HBM bytes of both kernels per launch (samples, the PSD written and read back):
+                     # informational beside the MFMA bound, profile-derived like the C3 / C5 figures
+                     "traffic": live_traffic[0], "traffic_source": live_traffic[1],
                      "kernel": "welch_i8_kernel<4> + welch_i8_bands_kernel", "kernel_ms": round(avg_s * 1e3, 4),
                      "int8_ops_per_launch": i8_ops, "useful_int8_ops_per_launch": useful},
         "kernel_ms_per_step": {"welch": round(avg_s * 1e3, 4), "live_detect": round(l_ms / max(l_n, 1), 4)},
